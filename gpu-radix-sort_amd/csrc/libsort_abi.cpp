@@ -1,0 +1,564 @@
+// libsort_abi.cpp -- the C ABI of include/libsort.h: device pool, host-pointer
+// entry points (reference invokers.cu / utils.cu), additive device-resident
+// entry points, PCG32 host generator and the per-kernel timing registry.
+//
+// NOTE on return types: the reference ABI declares `bool` returns.  ctypes
+// callers (faasTest/pylibsort/sort.py:101,118) never set `restype`, so they
+// read the whole of eax; a `bool` return only defines al.  The entry points
+// are therefore DEFINED here (this TU does not include libsort.h) with an
+// `int` return of 0/1: bool callers (cgo, the C++ harness) read al, int
+// callers read eax, and both see the right value.
+#include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "radix.h"
+
+#define LIBSORT_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace lsort {
+
+// ---------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------
+static thread_local std::string t_last_error;
+
+void set_error(const std::string& msg) {
+  t_last_error = msg;
+  fprintf(stderr, "libsort: %s\n", msg.c_str());
+}
+const char* last_error() { return t_last_error.c_str(); }
+
+static bool hip_ok(hipError_t e, const char* what) {
+  if (e == hipSuccess) return true;
+  set_error(std::string(what) + ": " + hipGetErrorString(e));
+  (void)hipGetLastError();  // clear the sticky-free error state
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// workspaces (one per device, created lazily, reused across calls)
+// ---------------------------------------------------------------------------
+static std::mutex g_ws_mu;
+static std::vector<std::unique_ptr<Workspace>> g_ws;
+
+Workspace* workspace_for(int device) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  if (device < 0) return nullptr;
+  if ((size_t)device >= g_ws.size()) g_ws.resize(device + 1);
+  if (!g_ws[device]) {
+    auto ws = std::make_unique<Workspace>();
+    ws->device = device;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
+    ws->num_cus = cus > 0 ? cus : 256;
+    int prev = -1;
+    (void)hipGetDevice(&prev);
+    (void)hipSetDevice(device);
+    if (hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking) != hipSuccess) ws->stream = nullptr;
+    if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    g_ws[device] = std::move(ws);
+  }
+  return g_ws[device].get();
+}
+
+void release_all_workspaces() {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  for (auto& w : g_ws)
+    if (w) {
+      std::lock_guard<std::mutex> l2(w->mu);
+      w->release();
+    }
+}
+
+// Cross-stream ordering of one workspace: the counters live in device memory
+// and are reused by every call, so a call on stream B waits for the last
+// call's work on stream A.
+struct WsOrder {
+  hipEvent_t evt = nullptr;
+  hipStream_t last = nullptr;
+  bool used = false;
+};
+static std::mutex g_order_mu;
+static std::vector<WsOrder> g_order;
+
+static bool ws_acquire_stream(int dev, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_order_mu);
+  if ((size_t)dev >= g_order.size()) g_order.resize(dev + 1);
+  WsOrder& o = g_order[dev];
+  if (!o.evt && !hip_ok(hipEventCreateWithFlags(&o.evt, hipEventDisableTiming), "hipEventCreate"))
+    return false;
+  if (o.used && o.last != st) return hip_ok(hipStreamWaitEvent(st, o.evt, 0), "hipStreamWaitEvent");
+  return true;
+}
+static void ws_release_stream(int dev, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_order_mu);
+  WsOrder& o = g_order[dev];
+  (void)hipEventRecord(o.evt, st);
+  o.last = st;
+  o.used = true;
+}
+
+// ---------------------------------------------------------------------------
+// timing registry
+// ---------------------------------------------------------------------------
+struct TimingRec {
+  std::string name;
+  hipEvent_t a = nullptr, b = nullptr;
+  uint64_t keys = 0;
+};
+static std::atomic<bool> g_timing_on{false};
+static std::mutex g_tmu;
+static std::vector<TimingRec> g_recs;
+
+bool timing_enabled() { return g_timing_on.load(std::memory_order_relaxed); }
+void timing_enable(bool on) { g_timing_on.store(on); }
+
+void timing_reset() {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  for (auto& r : g_recs) {
+    if (r.a) (void)hipEventDestroy(r.a);
+    if (r.b) (void)hipEventDestroy(r.b);
+  }
+  g_recs.clear();
+}
+
+int timing_start(const char* name, hipStream_t st, uint64_t keys) {
+  if (!timing_enabled()) return -1;
+  TimingRec r;
+  r.name = name;
+  r.keys = keys;
+  if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return -1;
+  if (hipEventRecord(r.a, st) != hipSuccess) return -1;
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_recs.push_back(r);
+  return (int)g_recs.size() - 1;
+}
+
+void timing_stop(int tok, hipStream_t st) {
+  if (tok < 0) return;
+  hipEvent_t b;
+  {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    if ((size_t)tok >= g_recs.size()) return;
+    b = g_recs[tok].b;
+  }
+  (void)hipEventRecord(b, st);
+}
+
+bool timing_query(const char* name, uint64_t* launches, double* total_ms, uint64_t* total_keys) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  uint64_t cnt = 0, keys = 0;
+  double ms = 0.0;
+  for (auto& r : g_recs) {
+    if (r.name != name) continue;
+    if (hipEventSynchronize(r.b) != hipSuccess) return false;
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, r.a, r.b) != hipSuccess) return false;
+    ms += t;
+    ++cnt;
+    keys += r.keys;
+  }
+  if (launches) *launches = cnt;
+  if (total_ms) *total_ms = ms;
+  if (total_keys) *total_keys = keys;
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// device pool (utils.cu:10-61, utils.h:19-68)
+// ---------------------------------------------------------------------------
+class Semaphore {
+ public:
+  explicit Semaphore(int n) : count_(n) {}
+  void down() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return count_ > 0; });
+    --count_;
+  }
+  void up() {
+    std::lock_guard<std::mutex> lk(mu_);
+    ++count_;
+    cv_.notify_one();
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int count_;
+};
+
+static std::mutex g_init_mu;
+static int g_ndev = 0;
+static std::atomic_flag* g_dev_locks = nullptr;
+static Semaphore* g_dev_sem = nullptr;
+
+// RAII reservation of one pool device; releases slot and flag on destruction.
+class Reservation {
+ public:
+  ~Reservation() { release(); }
+  bool reserve() {
+    if (!g_dev_sem) {
+      set_error("initLibSort() must be called before using the GPU entry points");
+      return false;
+    }
+    g_dev_sem->down();
+    for (int i = 0; i < g_ndev; ++i) {
+      if (!g_dev_locks[i].test_and_set()) {
+        hipError_t e = hipSetDevice(i);
+        if (e != hipSuccess) {
+          // the reference leaks the slot here (utils.cu:49-53); give it back
+          g_dev_locks[i].clear();
+          g_dev_sem->up();
+          return hip_ok(e, "hipSetDevice");
+        }
+        dev_ = i;
+        return true;
+      }
+    }
+    g_dev_sem->up();
+    set_error("failed to find an available device (pool invariant broken)");
+    return false;
+  }
+  int device() const { return dev_; }
+
+ private:
+  void release() {
+    if (dev_ >= 0) {
+      g_dev_locks[dev_].clear();
+      g_dev_sem->up();
+      dev_ = -1;
+    }
+  }
+  int dev_ = -1;
+};
+
+// ---------------------------------------------------------------------------
+// configuration
+// ---------------------------------------------------------------------------
+static int env_digit_bits() {
+  const char* s = getenv("LIBSORT_DIGIT_BITS");
+  if (!s) return 8;
+  int b = atoi(s);
+  return (b == 4 || b == 8) ? b : 8;
+}
+static std::atomic<int> g_digit_bits{env_digit_bits()};
+
+// ---------------------------------------------------------------------------
+// PCG32 host generator (utils.cu:65-80); state persists across calls
+// ---------------------------------------------------------------------------
+static std::mutex g_pcg_mu;
+static uint64_t g_pcg_state = kPcgInit;
+
+static inline uint32_t rotr32(uint32_t x, uint32_t r) { return (x >> r) | (x << ((0u - r) & 31u)); }
+
+// ---------------------------------------------------------------------------
+// host-pointer sorts
+// ---------------------------------------------------------------------------
+static bool host_sort(uint32_t* h, uint32_t* bounds, size_t len, uint32_t offset, uint32_t width,
+                      bool partial) {
+  Reservation res;
+  if (!res.reserve()) return false;
+  if (len > 0xffffffffull) {
+    set_error("Input array length must be less than 2^32");
+    return false;
+  }
+  if (partial) {
+    if (width > 31 || offset > 32 || offset + width > 32) {
+      set_error("gpuPartial: need width <= 31 and offset + width <= 32");
+      return false;
+    }
+    if (!bounds) {
+      set_error("gpuPartial: boundaries must not be NULL");
+      return false;
+    }
+  }
+  const uint32_t ngroups = partial ? (1u << width) : 0u;
+  if (len == 0 || (partial && width == 0)) {
+    if (partial) std::fill(bounds, bounds + ngroups, 0u);
+    return true;
+  }
+  Workspace* ws = workspace_for(res.device());
+  if (!ws) return false;
+  std::lock_guard<std::mutex> lk(ws->mu);
+  hipStream_t st = ws->stream;
+  if (!ws_acquire_stream(ws->device, st)) return false;
+  const int bits = g_digit_bits.load();
+  const size_t bytes = len * sizeof(uint32_t);
+  const int lo = partial ? (int)offset : 0;
+  const int hi = partial ? (int)(offset + width) : 32;
+  const int P = num_passes(hi - lo, bits);
+  bool ok = hip_ok(ws->ensure_hbuf(bytes), "hipMalloc(keys)");
+  if (ok && partial) ok = hip_ok(ws->ensure_bounds(ngroups), "hipMalloc(boundaries)");
+  if (ok) ok = hip_ok(hipMemcpyAsync(ws->hbuf[0], h, bytes, hipMemcpyHostToDevice, st), "H2D copy");
+  uint32_t* b0 = static_cast<uint32_t*>(ws->hbuf[0]);
+  uint32_t* b1 = static_cast<uint32_t*>(ws->hbuf[1]);
+  // Odd pass count: hbuf0 -> hbuf1 first, result in hbuf1, hbuf0 is scratch.
+  uint32_t* out = host_result_in_second(P) ? b1 : b0;
+  uint32_t* tmp = host_result_in_second(P) ? b0 : b1;
+  if (ok)
+    ok = hip_ok(sort_u32(*ws, b0, out, tmp, len, lo, hi, bits, partial ? ws->dbounds : nullptr, st),
+                "radix sort");
+  if (ok) ok = hip_ok(hipMemcpyAsync(h, out, bytes, hipMemcpyDeviceToHost, st), "D2H copy");
+  if (ok && partial)
+    ok = hip_ok(hipMemcpyAsync(bounds, ws->dbounds, (size_t)ngroups * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, st),
+                "D2H boundaries");
+  ws_release_stream(ws->device, st);
+  if (ok) ok = hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+  return ok;
+}
+
+static hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Runs fn(workspace) for the caller's current device with cross-stream
+// ordering of the workspace.
+template <typename Fn>
+static bool with_current_ws(hipStream_t st, Fn fn) {
+  int dev = -1;
+  if (!hip_ok(hipGetDevice(&dev), "hipGetDevice")) return false;
+  Workspace* ws = workspace_for(dev);
+  if (!ws) {
+    set_error("no workspace for current device");
+    return false;
+  }
+  std::lock_guard<std::mutex> lk(ws->mu);
+  if (!ws_acquire_stream(dev, st)) return false;
+  bool ok = fn(*ws);
+  ws_release_stream(dev, st);
+  return ok;
+}
+
+}  // namespace lsort
+
+using namespace lsort;
+
+// ===========================================================================
+// Part 1: reference ABI
+// ===========================================================================
+LIBSORT_EXPORT int initLibSort(void) {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  if (g_dev_locks != nullptr) {
+    set_error("attempted to initialize multiple times!");
+    return 0;
+  }
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) {
+    set_error(std::string("Failed to get device count: ") +
+              (e != hipSuccess ? hipGetErrorString(e) : "no HIP device"));
+    (void)hipGetLastError();
+    return 0;
+  }
+  if (const char* s = getenv("LIBSORT_NGPU")) {
+    int lim = atoi(s);
+    if (lim > 0 && lim < n) n = lim;
+  }
+  g_ndev = n;
+  g_dev_locks = new std::atomic_flag[n];
+  for (int i = 0; i < n; ++i) g_dev_locks[i].clear();
+  g_dev_sem = new Semaphore(n);
+  return 1;
+}
+
+LIBSORT_EXPORT int gpuPartial(uint32_t* h_in, uint32_t* boundaries, size_t h_in_len, uint32_t offset,
+                              uint32_t width) {
+  return host_sort(h_in, boundaries, h_in_len, offset, width, true) ? 1 : 0;
+}
+
+LIBSORT_EXPORT int providedGpu(unsigned int* h_in, size_t len) {
+  return host_sort(h_in, nullptr, len, 0, 32, false) ? 1 : 0;
+}
+
+LIBSORT_EXPORT int providedCpu(unsigned int* in, size_t len) {
+  std::sort(in, in + len);
+  return 1;
+}
+
+LIBSORT_EXPORT void populateInput(uint32_t* arr, size_t nelem) {
+  std::lock_guard<std::mutex> lk(g_pcg_mu);  // the reference state is unguarded (utils.cu:67)
+  uint64_t state = g_pcg_state;
+  for (size_t i = 0; i < nelem; ++i) {
+    uint64_t x = state;
+    const uint32_t count = (uint32_t)(x >> 59);
+    state = x * kPcgMult + kPcgInc;
+    x ^= x >> 18;
+    arr[i] = rotr32((uint32_t)(x >> 27), count);
+  }
+  g_pcg_state = state;
+}
+
+LIBSORT_EXPORT int gpuPartialProfile(uint32_t* h_in, uint32_t* boundaries, size_t h_in_len,
+                                     uint32_t offset, uint32_t width) {
+  roctxRangePush("gpuPartialProfile");
+  int r = gpuPartial(h_in, boundaries, h_in_len, offset, width);
+  roctxRangePop();
+  return r;
+}
+
+LIBSORT_EXPORT int providedGpuProfile(unsigned int* h_in, size_t h_in_len) {
+  roctxRangePush("providedGpuProfile");
+  int r = providedGpu(h_in, h_in_len);
+  roctxRangePop();
+  return r;
+}
+
+// ===========================================================================
+// Part 2: additive API
+// ===========================================================================
+LIBSORT_EXPORT int gpuFullSort(unsigned int* h_in, size_t len) { return providedGpu(h_in, len); }
+
+LIBSORT_EXPORT int gpuPartialSort(uint32_t* h_in, uint32_t* boundaries, size_t h_in_len, uint32_t offset,
+                                  uint32_t width) {
+  return gpuPartial(h_in, boundaries, h_in_len, offset, width);
+}
+
+static bool check_range(size_t n, uint32_t offset, uint32_t width, uint32_t keybits) {
+  if (n > 0xffffffffull) {
+    set_error("at most 2^32-1 elements per call");
+    return false;
+  }
+  if (offset > keybits || width > keybits || offset + width > keybits) {
+    set_error("bit range outside the key");
+    return false;
+  }
+  return true;
+}
+
+LIBSORT_EXPORT int libsortSortKeysU32(const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp, size_t n,
+                                      uint32_t offset, uint32_t width, uint32_t* d_boundaries,
+                                      void* stream) {
+  if (!check_range(n, offset, width, 32)) return 0;
+  if (d_boundaries && width > 31) {
+    set_error("boundaries need width <= 31");
+    return 0;
+  }
+  if (n > 0 && (!d_in || !d_out || !d_tmp || d_tmp == d_out || (const uint32_t*)d_tmp == d_in)) {
+    set_error("libsortSortKeysU32: need distinct d_tmp (d_in may equal d_out)");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(sort_u32(ws, d_in, d_out, d_tmp, n, (int)offset, (int)(offset + width),
+                                  g_digit_bits.load(), d_boundaries, st),
+                         "libsortSortKeysU32");
+         })
+             ? 1
+             : 0;
+}
+
+LIBSORT_EXPORT int libsortSortPairsU64U32(const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
+                                          uint32_t* d_vout, uint64_t* d_ktmp, uint32_t* d_vtmp, size_t n,
+                                          uint32_t offset, uint32_t width, void* stream) {
+  if (!check_range(n, offset, width, 64)) return 0;
+  if (n > 0 && (d_ktmp == d_kout || (const uint64_t*)d_ktmp == d_kin || d_vtmp == d_vout ||
+                (const uint32_t*)d_vtmp == d_vin)) {
+    set_error("libsortSortPairsU64U32: scratch buffers must not alias input/output");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(sort_pairs_u64_u32(ws, d_kin, d_vin, d_kout, d_vout, d_ktmp, d_vtmp, n,
+                                            (int)offset, (int)(offset + width), g_digit_bits.load(), st),
+                         "libsortSortPairsU64U32");
+         })
+             ? 1
+             : 0;
+}
+
+LIBSORT_EXPORT int libsortSortPairsU32U32(const uint32_t* d_kin, const uint32_t* d_vin, uint32_t* d_kout,
+                                          uint32_t* d_vout, uint32_t* d_ktmp, uint32_t* d_vtmp, size_t n,
+                                          uint32_t offset, uint32_t width, void* stream) {
+  if (!check_range(n, offset, width, 32)) return 0;
+  if (n > 0 && (d_ktmp == d_kout || (const uint32_t*)d_ktmp == d_kin || d_vtmp == d_vout ||
+                (const uint32_t*)d_vtmp == d_vin)) {
+    set_error("libsortSortPairsU32U32: scratch buffers must not alias input/output");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(sort_pairs_u32_u32(ws, d_kin, d_vin, d_kout, d_vout, d_ktmp, d_vtmp, n,
+                                            (int)offset, (int)(offset + width), g_digit_bits.load(), st),
+                         "libsortSortPairsU32U32");
+         })
+             ? 1
+             : 0;
+}
+
+LIBSORT_EXPORT int libsortHistogramU32(const uint32_t* d_keys, size_t n, uint32_t shift, uint32_t bits,
+                                       uint32_t* d_hist, void* stream) {
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(histogram_u32(ws, d_keys, n, (int)shift, (int)bits, d_hist, st),
+                         "libsortHistogramU32");
+         })
+             ? 1
+             : 0;
+}
+
+LIBSORT_EXPORT int libsortPartitionU32(const uint32_t* d_in, uint32_t* d_out, size_t n,
+                                       const uint32_t* splitters, uint32_t nsplit, uint32_t* d_counts,
+                                       void* stream) {
+  if (nsplit > 0 && !splitters) {
+    set_error("libsortPartitionU32: splitters must not be NULL");
+    return 0;
+  }
+  if (n > 0 && (const uint32_t*)d_out == d_in) {
+    set_error("libsortPartitionU32: out of place only");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(partition_u32(ws, d_in, d_out, n, splitters, (int)nsplit, d_counts, st),
+                         "libsortPartitionU32");
+         })
+             ? 1
+             : 0;
+}
+
+LIBSORT_EXPORT int libsortSegmentCopyU32(const uint32_t* d_src, uint32_t* d_dst, size_t nseg,
+                                         const uint64_t* src_off, const uint64_t* dst_off,
+                                         const uint64_t* len, void* stream) {
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(segment_copy_u32(ws, d_src, d_dst, nseg, src_off, dst_off, len, st),
+                         "libsortSegmentCopyU32");
+         })
+             ? 1
+             : 0;
+}
+
+LIBSORT_EXPORT int libsortPopulateDevice(uint32_t* d_out, size_t n, uint64_t first, void* stream) {
+  return hip_ok(populate_device(d_out, n, first, as_stream(stream)), "libsortPopulateDevice") ? 1 : 0;
+}
+
+LIBSORT_EXPORT int libsortSetDigitBits(int bits) {
+  if (bits != 4 && bits != 8) return -1;
+  return g_digit_bits.exchange(bits);
+}
+
+LIBSORT_EXPORT int libsortGetDigitBits(void) { return g_digit_bits.load(); }
+
+LIBSORT_EXPORT void libsortTimingEnable(bool on) { timing_enable(on); }
+LIBSORT_EXPORT void libsortTimingReset(void) { timing_reset(); }
+LIBSORT_EXPORT int libsortTimingQuery(const char* kernel, uint64_t* launches, double* total_ms,
+                                      uint64_t* total_keys) {
+  return timing_query(kernel, launches, total_ms, total_keys) ? 1 : 0;
+}
+
+LIBSORT_EXPORT int libsortReleaseWorkspace(void) {
+  release_all_workspaces();
+  return 1;
+}
+
+LIBSORT_EXPORT const char* libsortLastError(void) { return last_error(); }

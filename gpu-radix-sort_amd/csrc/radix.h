@@ -1,0 +1,125 @@
+// radix.h -- internal interface between the C ABI (libsort_abi.cpp) and the
+// HIP kernels / pass driver (radix_kernels.hip).  Not installed; the public
+// surface is include/libsort.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include <mutex>
+#include <string>
+
+namespace lsort {
+
+// Tile geometry of the digit-pass kernels (DESIGN.md "Kernels").
+constexpr int kBlock = 256;       // 4 waves of 64 lanes
+constexpr int kItemsU32 = 16;     // keys per thread, u32 keys  -> 4096-key tiles
+constexpr int kItemsU64 = 8;      // keys per thread, u64 keys  -> 2048-key tiles
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 16;
+constexpr int kScanTile = kScanBlock * kScanItems;  // 4096 counters per scan tile
+constexpr int kMaxSplit = 255;    // range partition: up to 256 buckets
+
+struct NoValue {};
+
+// Per-device cached state.  Every entry point holds `mu` while it uses it.
+struct Workspace {
+  int device = -1;
+  int num_cus = 0;
+  std::mutex mu;
+
+  // reduce-then-scan counters: counts[digit][block] and its two-level scan
+  uint32_t* counts = nullptr;
+  uint32_t* scan_l1 = nullptr;
+  uint32_t* scan_l2 = nullptr;
+  size_t counts_cap = 0;  // elements
+  size_t l2_cap = 0;      // elements
+
+  // staging for the host-pointer ABI (providedGpu / gpuPartial)
+  void* hbuf[2] = {nullptr, nullptr};
+  size_t hbuf_cap = 0;  // bytes per buffer
+  uint32_t* dbounds = nullptr;
+  size_t dbounds_cap = 0;  // elements
+
+  // segment tables for libsortSegmentCopyU32 (pinned staging + device copy)
+  uint64_t* seg_dev = nullptr;
+  uint64_t* seg_host = nullptr;
+  size_t seg_cap = 0;  // uint64 elements
+  hipEvent_t seg_evt = nullptr;
+
+  // scratch for histogram partials
+  uint32_t* hist_tmp = nullptr;
+  size_t hist_tmp_cap = 0;
+
+  hipStream_t stream = nullptr;  // used by the host-pointer ABI
+
+  hipError_t ensure_counts(size_t m);
+  hipError_t ensure_hbuf(size_t bytes);
+  hipError_t ensure_bounds(size_t m);
+  hipError_t ensure_seg(size_t m);
+  void release();
+};
+
+// Returns the workspace of `device` (created on first use; never destroyed
+// except by release()).  Thread-safe.
+Workspace* workspace_for(int device);
+void release_all_workspaces();
+
+// Number of LSD passes for `width` bits at `bits` per digit.
+inline int num_passes(int width, int bits) { return width <= 0 ? 0 : (width + bits - 1) / bits; }
+
+// Stable LSD radix sort of bits [lo, hi) of the keys (values carried along).
+// in may equal out; tmp must not alias out; tmp may alias in only when the
+// pass count is odd (used by the host ABI to avoid a copy).  When d_bounds is
+// non-null, it receives the 2^(hi-lo) group boundaries of gpuPartial.
+// All work is enqueued on `stream`; nothing synchronises.
+hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n,
+                    int lo, int hi, int digit_bits, uint32_t* d_bounds, hipStream_t stream);
+hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t* vin,
+                              uint32_t* kout, uint32_t* vout, uint32_t* ktmp, uint32_t* vtmp,
+                              size_t n, int lo, int hi, int digit_bits, hipStream_t stream);
+hipError_t sort_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin,
+                              uint64_t* kout, uint32_t* vout, uint64_t* ktmp, uint32_t* vtmp,
+                              size_t n, int lo, int hi, int digit_bits, hipStream_t stream);
+
+// Host-side choice of the ping-pong pair for the host ABI: returns true when
+// the result of a `passes`-pass sort started from hbuf[0] lands in hbuf[1].
+inline bool host_result_in_second(int passes) { return (passes & 1) != 0; }
+
+hipError_t histogram_u32(Workspace& ws, const uint32_t* keys, size_t n, int shift, int bits,
+                         uint32_t* d_hist, hipStream_t stream);
+hipError_t partition_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n,
+                         const uint32_t* splitters, int nsplit, uint32_t* d_counts,
+                         hipStream_t stream);
+hipError_t segment_copy_u32(Workspace& ws, const uint32_t* src, uint32_t* dst, size_t nseg,
+                            const uint64_t* src_off, const uint64_t* dst_off, const uint64_t* len,
+                            hipStream_t stream);
+hipError_t populate_device(uint32_t* out, size_t n, uint64_t first, hipStream_t stream);
+
+// ---- per-kernel timing (hipEvents on the launch stream) ----
+bool timing_enabled();
+void timing_enable(bool on);
+void timing_reset();
+bool timing_query(const char* name, uint64_t* launches, double* total_ms, uint64_t* total_keys);
+// Records a start event; returns a token (or -1 when timing is off).
+int timing_start(const char* name, hipStream_t stream, uint64_t keys);
+void timing_stop(int token, hipStream_t stream);
+
+struct ScopedTimer {
+  int tok;
+  hipStream_t s;
+  ScopedTimer(const char* name, hipStream_t st, uint64_t keys) : tok(timing_start(name, st, keys)), s(st) {}
+  ~ScopedTimer() { timing_stop(tok, s); }
+};
+
+// ---- host PCG32 (utils.cu:65-80) ----
+constexpr uint64_t kPcgInit = 0x4d595df4d0f33173ull;
+constexpr uint64_t kPcgMult = 6364136223846793005ull;
+constexpr uint64_t kPcgInc = 1442695040888963407ull;
+
+// Error text of the calling thread.
+void set_error(const std::string& msg);
+const char* last_error();
+
+}  // namespace lsort

@@ -1,0 +1,176 @@
+"""Device-resident entry points of libsort on torch tensors.
+
+torch is plumbing here: it owns the HBM buffers and the current HIP stream;
+every computation runs in libsort.so's HIP kernels (there is no torch or CPU
+fallback -- a missing GPU or library raises).
+
+uint32 keys travel in int32 tensors and uint64 keys in int64 tensors (same
+bits); torch's uint32/uint64 dtypes are accepted too.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _state, last_error
+
+_U32 = (torch.int32, torch.uint32)
+_U64 = (torch.int64, torch.uint64)
+
+
+def _lib():
+    return _state.sortLib
+
+
+def _check(ok, what):
+    if not ok:
+        raise RuntimeError("%s failed: %s" % (what, last_error()))
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _need(t, dtypes, name):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError("%s must be a CUDA (HIP) tensor" % name)
+    if t.dtype not in dtypes:
+        raise TypeError("%s has dtype %s, expected one of %s" % (name, t.dtype, dtypes))
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous" % name)
+
+
+def sort_keys_u32(keys, out=None, tmp=None, offset=0, width=None, boundaries=None):
+    """Stable LSD sort of bits [offset, offset+width) of uint32 keys (int32
+    carrier).  Returns `out`.  `boundaries` (optional int32 tensor of 2**width)
+    receives the gpuPartial group boundaries."""
+    _need(keys, _U32, "keys")
+    n = keys.numel()
+    if width is None:
+        width = 32 - offset
+    out = torch.empty_like(keys) if out is None else out
+    tmp = torch.empty_like(keys) if tmp is None else tmp
+    _need(out, _U32, "out")
+    _need(tmp, _U32, "tmp")
+    if boundaries is not None:
+        _need(boundaries, _U32, "boundaries")
+        if boundaries.numel() != (1 << width):
+            raise ValueError("boundaries must hold 2**width entries")
+    _check(_lib().libsortSortKeysU32(_ptr(keys), _ptr(out), _ptr(tmp), n, offset, width,
+                                     _ptr(boundaries), _stream()), "libsortSortKeysU32")
+    return out
+
+
+def sort_pairs_u64_u32(keys, vals, out_keys=None, out_vals=None, tmp_keys=None, tmp_vals=None,
+                       offset=0, width=None):
+    """Stable sort of (uint64 key, uint32 payload) pairs by key bits."""
+    _need(keys, _U64, "keys")
+    _need(vals, _U32, "vals")
+    if keys.numel() != vals.numel():
+        raise ValueError("keys and vals differ in length")
+    if width is None:
+        width = 64 - offset
+    ok_ = torch.empty_like(keys) if out_keys is None else out_keys
+    ov = torch.empty_like(vals) if out_vals is None else out_vals
+    tk = torch.empty_like(keys) if tmp_keys is None else tmp_keys
+    tv = torch.empty_like(vals) if tmp_vals is None else tmp_vals
+    _check(_lib().libsortSortPairsU64U32(_ptr(keys), _ptr(vals), _ptr(ok_), _ptr(ov), _ptr(tk),
+                                         _ptr(tv), keys.numel(), offset, width, _stream()),
+           "libsortSortPairsU64U32")
+    return ok_, ov
+
+
+def sort_pairs_u32_u32(keys, vals, out_keys=None, out_vals=None, tmp_keys=None, tmp_vals=None,
+                       offset=0, width=None):
+    """Stable sort of (uint32 key, uint32 payload) pairs by key bits."""
+    _need(keys, _U32, "keys")
+    _need(vals, _U32, "vals")
+    if keys.numel() != vals.numel():
+        raise ValueError("keys and vals differ in length")
+    if width is None:
+        width = 32 - offset
+    ok_ = torch.empty_like(keys) if out_keys is None else out_keys
+    ov = torch.empty_like(vals) if out_vals is None else out_vals
+    tk = torch.empty_like(keys) if tmp_keys is None else tmp_keys
+    tv = torch.empty_like(vals) if tmp_vals is None else tmp_vals
+    _check(_lib().libsortSortPairsU32U32(_ptr(keys), _ptr(vals), _ptr(ok_), _ptr(ov), _ptr(tk),
+                                         _ptr(tv), keys.numel(), offset, width, _stream()),
+           "libsortSortPairsU32U32")
+    return ok_, ov
+
+
+def histogram_u32(keys, shift, bits, out=None):
+    """Counts of (key >> shift) & (2**bits-1) into an int32 tensor of 2**bits."""
+    _need(keys, _U32, "keys")
+    out = torch.empty(1 << bits, dtype=torch.int32, device=keys.device) if out is None else out
+    _check(_lib().libsortHistogramU32(_ptr(keys), keys.numel(), shift, bits, _ptr(out), _stream()),
+           "libsortHistogramU32")
+    return out
+
+
+def partition_u32(keys, splitters, out=None, counts=None):
+    """Stable range partition: bucket(x) = #{s in splitters : x >= s}."""
+    _need(keys, _U32, "keys")
+    sp = [int(s) for s in splitters]
+    arr = (ctypes.c_uint32 * max(1, len(sp)))(*sp)
+    out = torch.empty_like(keys) if out is None else out
+    counts = (torch.empty(len(sp) + 1, dtype=torch.int32, device=keys.device)
+              if counts is None else counts)
+    _check(_lib().libsortPartitionU32(_ptr(keys), _ptr(out), keys.numel(), arr, len(sp),
+                                      _ptr(counts), _stream()), "libsortPartitionU32")
+    return out, counts
+
+
+def segment_copy_u32(src, dst, src_off, dst_off, lens):
+    """dst[dst_off[i] + j] = src[src_off[i] + j] for j < lens[i]."""
+    _need(src, _U32, "src")
+    _need(dst, _U32, "dst")
+    so = np.ascontiguousarray(src_off, dtype=np.uint64)
+    do = np.ascontiguousarray(dst_off, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint64)
+    if not (so.size == do.size == ln.size):
+        raise ValueError("segment tables differ in length")
+    if so.size and (int((so + ln).max()) > src.numel() or int((do + ln).max()) > dst.numel()):
+        raise ValueError("segment out of range")
+    p = ctypes.POINTER(ctypes.c_uint64)
+    _check(_lib().libsortSegmentCopyU32(_ptr(src), _ptr(dst), so.size, so.ctypes.data_as(p),
+                                        do.ctypes.data_as(p), ln.ctypes.data_as(p), _stream()),
+           "libsortSegmentCopyU32")
+    return dst
+
+
+def populate_u32(n, first=0, device=None, out=None):
+    """Elements [first, first+n) of the reference populateInput stream (fresh
+    process), generated on the device."""
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=device or torch.device("cuda"))
+    _need(out, _U32, "out")
+    _check(_lib().libsortPopulateDevice(_ptr(out), n, first, _stream()), "libsortPopulateDevice")
+    return out
+
+
+def timing_enable(on=True):
+    _lib().libsortTimingEnable(bool(on))
+
+
+def timing_reset():
+    _lib().libsortTimingReset()
+
+
+def timing_query(kernel):
+    """(launches, total_ms, total_keys) of the recorded launches of `kernel`."""
+    n = ctypes.c_uint64()
+    ms = ctypes.c_double()
+    k = ctypes.c_uint64()
+    _check(_lib().libsortTimingQuery(kernel.encode(), ctypes.byref(n), ctypes.byref(ms),
+                                     ctypes.byref(k)), "libsortTimingQuery")
+    return n.value, ms.value, k.value
+
+
+def as_u32_numpy(t):
+    """Host numpy uint32 view of a uint32-carrying tensor."""
+    return t.detach().cpu().numpy().view(np.uint32)

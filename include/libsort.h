@@ -1,0 +1,143 @@
+/*
+ * libsort.h -- C ABI of the MI355X-native libsort (gfx950, HIP).
+ *
+ * Part 1 is the drop-in boundary: the seven entry points of the reference
+ * jssmith/gpu-radix-sort `libsort/libsort.h:12-44`, with the SAME names and the
+ * SAME C types, so that the unchanged callers link and run against this
+ * library:
+ *   - Go (cgo, --std=gnu99)     benchmark/pkg/sort/libsort.go:11-77
+ *   - Python (ctypes)           faasTest/pylibsort/__init__.py:13-20, sort.py:94-126, data.py:313-317
+ *   - C++ harness               localTest/tests.cpp:56,107,117  benchmarks.cpp:44,57,105-109
+ * Under C++ every declaration is extern "C"; under plain C (cgo) they are
+ * ordinary prototypes, as in the reference header.
+ *
+ * Part 2 is additive (new names only; Part 1 is unchanged by it): device-
+ * resident entry points used by the multi-GPU driver and the benchmark, the
+ * north-star aliases gpuFullSort / gpuPartialSort, and timing hooks.
+ *
+ * Error convention (reference invokers.cu:18-20,30-33,49-57): every `bool`
+ * entry point returns false on failure and prints one line to stderr.  Unlike
+ * the reference (utils.h:71-78) a HIP error never calls exit(); the message is
+ * also available from libsortLastError().
+ */
+#ifndef LIBSORT_MI355X_LIBSORT_H
+#define LIBSORT_MI355X_LIBSORT_H
+
+#include <stdint.h>
+#include <stdbool.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+#define LIBSORT_API extern "C"
+#else
+#define LIBSORT_API
+#endif
+
+/* ======================= Part 1: reference ABI ============================ */
+
+/* Replaces utils.cu:10-32.  Must be called exactly once per process before the
+ * host-pointer entry points; a second call prints a message and returns false.
+ * Returns false (loudly) when no HIP device is present. */
+LIBSORT_API bool initLibSort(void);
+
+/* Replaces invokers.cu:15-41 (gpuPartial).  Stable partition of h_in[0..len)
+ * by the group value (x >> offset) & (2^width - 1), in place; prior order is
+ * preserved inside each group.  boundaries (caller-allocated, 2^width uint32)
+ * receives, for every group g, the index of its first element, i.e. the
+ * number of elements whose group is < g (the exclusive prefix of group counts,
+ * the contract checked by localTest/tests.cpp:41-83).  Requires
+ * len <= UINT32_MAX, 1 <= width <= 31 and offset + width <= 32.  Odd widths
+ * are supported exactly (the reference silently sorts one extra bit, sort.cu:323). */
+LIBSORT_API bool gpuPartial(uint32_t* h_in, uint32_t* boundaries, size_t h_in_len,
+                            uint32_t offset, uint32_t width);
+
+/* Replaces invokers.cu:45-64 (providedGpu).  Ascending in-place sort of
+ * len uint32 keys on a GPU taken from the device pool.  len <= UINT32_MAX. */
+LIBSORT_API bool providedGpu(unsigned int* h_in, size_t len);
+
+/* Replaces invokers.cu:68-71 (providedCpu): std::sort on the host. */
+LIBSORT_API bool providedCpu(unsigned int* in, size_t len);
+
+/* Replaces utils.cu:65-80: PCG32 (XSH-RR) stream with process-wide state that
+ * persists across calls; bit-identical to the reference generator. */
+LIBSORT_API void populateInput(uint32_t* arr, size_t nelem);
+
+/* Replaces invokers.cu:73-85: the same calls bracketed by roctx ranges
+ * ("gpuPartialProfile" / "providedGpuProfile") for rocprofv3 --marker-trace. */
+LIBSORT_API bool gpuPartialProfile(uint32_t* h_in, uint32_t* boundaries, size_t h_in_len,
+                                   uint32_t offset, uint32_t width);
+LIBSORT_API bool providedGpuProfile(unsigned int* h_in, size_t h_in_len);
+
+/* ======================= Part 2: additive API ============================= */
+
+/* North-star names (BASELINE.json): aliases of providedGpu / gpuPartial. */
+LIBSORT_API bool gpuFullSort(unsigned int* h_in, size_t len);
+LIBSORT_API bool gpuPartialSort(uint32_t* h_in, uint32_t* boundaries, size_t h_in_len,
+                                uint32_t offset, uint32_t width);
+
+/* Device-resident sort of uint32 keys on the caller's current HIP device,
+ * enqueued on `stream` (a hipStream_t; NULL = the null stream).  Sorts bits
+ * [offset, offset+width) stably (width = 32 - offset for a full sort).
+ * d_in is read-only; the result is written to d_out; d_tmp is scratch of n
+ * keys.  d_in may equal d_out (in place); d_tmp must alias neither.
+ * d_boundaries (nullable, device, 2^width uint32) receives the same
+ * boundaries as gpuPartial.  The call is asynchronous w.r.t. the host. */
+LIBSORT_API bool libsortSortKeysU32(const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp,
+                                    size_t n, uint32_t offset, uint32_t width,
+                                    uint32_t* d_boundaries, void* stream);
+
+/* Stable key-value sort: 64-bit keys, 32-bit payloads (BASELINE config C5). */
+LIBSORT_API bool libsortSortPairsU64U32(const uint64_t* d_kin, const uint32_t* d_vin,
+                                        uint64_t* d_kout, uint32_t* d_vout,
+                                        uint64_t* d_ktmp, uint32_t* d_vtmp, size_t n,
+                                        uint32_t offset, uint32_t width, void* stream);
+
+/* Stable key-value sort: 32-bit keys, 32-bit payloads. */
+LIBSORT_API bool libsortSortPairsU32U32(const uint32_t* d_kin, const uint32_t* d_vin,
+                                        uint32_t* d_kout, uint32_t* d_vout,
+                                        uint32_t* d_ktmp, uint32_t* d_vtmp, size_t n,
+                                        uint32_t offset, uint32_t width, void* stream);
+
+/* Histogram of (key >> shift) & (2^bits - 1), bits <= 16, into d_hist
+ * (2^bits uint32, overwritten). */
+LIBSORT_API bool libsortHistogramU32(const uint32_t* d_keys, size_t n, uint32_t shift,
+                                     uint32_t bits, uint32_t* d_hist, void* stream);
+
+/* Stable partition by range: element x goes to bucket b = #{i : x >= splitters[i]}
+ * (host array, ascending, nsplit <= 255).  d_out receives the buckets in order;
+ * d_counts (nullable, device, nsplit+1 uint32) receives the bucket sizes. */
+LIBSORT_API bool libsortPartitionU32(const uint32_t* d_in, uint32_t* d_out, size_t n,
+                                     const uint32_t* splitters, uint32_t nsplit,
+                                     uint32_t* d_counts, void* stream);
+
+/* Gather-copy of nseg segments: dst[dst_off[i] + j] = src[src_off[i] + j] for
+ * j < len[i].  The three tables are host arrays.  Used to put exchanged
+ * buckets into bucket-major / rank-minor order between distributed rounds. */
+LIBSORT_API bool libsortSegmentCopyU32(const uint32_t* d_src, uint32_t* d_dst, size_t nseg,
+                                       const uint64_t* src_off, const uint64_t* dst_off,
+                                       const uint64_t* len, void* stream);
+
+/* Writes elements [first, first+n) of the populateInput stream of a fresh
+ * process (state 0x4d595df4d0f33173) to device memory, by LCG skip-ahead. */
+LIBSORT_API bool libsortPopulateDevice(uint32_t* d_out, size_t n, uint64_t first, void* stream);
+
+/* Radix digit width used by the sorts (4 or 8 bits; default 8, or the
+ * LIBSORT_DIGIT_BITS environment variable).  Returns the previous value, or
+ * -1 if `bits` is unsupported. */
+LIBSORT_API int libsortSetDigitBits(int bits);
+LIBSORT_API int libsortGetDigitBits(void);
+
+/* Per-kernel timing with hipEvents on the launch stream.  Names: "upsweep",
+ * "scan", "downsweep", "bounds", "populate", "segcopy". */
+LIBSORT_API void libsortTimingEnable(bool on);
+LIBSORT_API void libsortTimingReset(void);
+LIBSORT_API bool libsortTimingQuery(const char* kernel, uint64_t* launches, double* total_ms,
+                                    uint64_t* total_keys);
+
+/* Frees the cached per-device workspaces (they are otherwise kept for reuse). */
+LIBSORT_API bool libsortReleaseWorkspace(void);
+
+/* Last error message of the calling thread ("" if none). */
+LIBSORT_API const char* libsortLastError(void);
+
+#endif /* LIBSORT_MI355X_LIBSORT_H */
