@@ -254,6 +254,24 @@ static int env_digit_bits() {
 }
 static std::atomic<int> g_digit_bits{env_digit_bits()};
 
+static int env_algorithm() {
+  const char* s = getenv("LIBSORT_ALGO");
+  if (!s) return 0;
+  switch (s[0]) {
+    case 'o': case 'O': return 1;
+    case 'r': case 'R': return 2;
+    case 't': case 'T': return 3;
+    default: return 0;
+  }
+}
+static std::atomic<int> g_algorithm{env_algorithm()};
+
+int get_algorithm() { return g_algorithm.load(std::memory_order_relaxed); }
+int set_algorithm(int a) {
+  if (a < 0 || a > 3) return -1;
+  return g_algorithm.exchange(a);
+}
+
 // ---------------------------------------------------------------------------
 // PCG32 host generator (utils.cu:65-80); state persists across calls
 // ---------------------------------------------------------------------------
@@ -549,6 +567,8 @@ LIBSORT_EXPORT int libsortSetDigitBits(int bits) {
 
 LIBSORT_EXPORT int libsortGetDigitBits(void) { return g_digit_bits.load(); }
 
+LIBSORT_EXPORT int libsortSetAlgorithm(int algo) { return set_algorithm(algo); }
+
 LIBSORT_EXPORT void libsortTimingEnable(bool on) { timing_enable(on); }
 LIBSORT_EXPORT void libsortTimingReset(void) { timing_reset(); }
 LIBSORT_EXPORT int libsortTimingQuery(const char* kernel, uint64_t* launches, double* total_ms,
@@ -562,3 +582,19 @@ LIBSORT_EXPORT int libsortReleaseWorkspace(void) {
 }
 
 LIBSORT_EXPORT const char* libsortLastError(void) { return last_error(); }
+
+// Synchronises the current device and returns (then clears) the device-side
+// error word of its workspace: bit 0 = a look-back spin hit its bound.
+LIBSORT_EXPORT uint32_t libsortDeviceErrors(void) {
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return 0xffffffffu;
+  Workspace* ws = workspace_for(dev);
+  if (!ws) return 0xffffffffu;
+  std::lock_guard<std::mutex> lk(ws->mu);
+  if (!ws->os_small) return 0;
+  uint32_t v = 0;
+  if (hipDeviceSynchronize() != hipSuccess) return 0xffffffffu;
+  if (hipMemcpy(&v, ws->os_small + kOsErr, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return 0xffffffffu;
+  if (v) (void)hipMemset(ws->os_small + kOsErr, 0, sizeof(uint32_t));
+  return v;
+}

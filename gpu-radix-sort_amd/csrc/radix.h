@@ -21,6 +21,17 @@ constexpr int kScanItems = 16;
 constexpr int kScanTile = kScanBlock * kScanItems;  // 4096 counters per scan tile
 constexpr int kMaxSplit = 255;    // range partition: up to 256 buckets
 
+// onesweep tiles and the layout of Workspace::os_small (uint32 words)
+constexpr int kOsBlock = 256;
+constexpr int kOsItemsU32 = 16;
+constexpr int kOsItemsU64 = 8;
+constexpr int kOsWhist = 0;              // 8 windows x 256
+constexpr int kOsGbase = 8 * 256;        // 16 passes x 256
+constexpr int kOsCounters = kOsGbase + 16 * 256;  // 16 tile counters
+constexpr int kOsErr = kOsCounters + 16;
+constexpr int kOsSmallWords = kOsErr + 16;
+constexpr int kOsZeroWords = kOsErr;     // memset per sort: histograms, bases, counters
+
 struct NoValue {};
 
 // Per-device cached state.  Every entry point holds `mu` while it uses it.
@@ -54,10 +65,25 @@ struct Workspace {
 
   hipStream_t stream = nullptr;  // used by the host-pointer ABI
 
+  // onesweep path: two look-back status buffers [tiles][RADIX] and a small
+  // block: window histograms | per-pass digit bases | tile counters | error
+  uint32_t* os_status[2] = {nullptr, nullptr};
+  size_t os_status_cap = 0;  // words per buffer
+  uint32_t* os_small = nullptr;
+  int last_algo = 0;  // 1 = onesweep, 2 = reduce-then-scan, 3 = tile offsets (last sort)
+
+  // tile-offset path: per-tile digit counts (two buffers) and chunk totals
+  uint32_t* tc[2] = {nullptr, nullptr};
+  size_t tc_cap = 0;  // words per buffer
+  uint32_t* tb = nullptr;
+  size_t tb_cap = 0;  // words
+  hipError_t ensure_tiles(size_t count_words, size_t chunk_words);
+
   hipError_t ensure_counts(size_t m);
   hipError_t ensure_hbuf(size_t bytes);
   hipError_t ensure_bounds(size_t m);
   hipError_t ensure_seg(size_t m);
+  hipError_t ensure_onesweep(size_t status_words);
   void release();
 };
 
@@ -82,6 +108,13 @@ hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t
 hipError_t sort_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin,
                               uint64_t* kout, uint32_t* vout, uint64_t* ktmp, uint32_t* vtmp,
                               size_t n, int lo, int hi, int digit_bits, hipStream_t stream);
+
+// Pass algorithm: 0 = auto (tile offsets for 4-bit digits, onesweep for 8-bit,
+// reduce-then-scan when n >= 2^30), 1 = onesweep, 2 = reduce-then-scan,
+// 3 = tile offsets.  Initialised from LIBSORT_ALGO ("auto" / "onesweep" /
+// "rts" / "tiles").
+int get_algorithm();
+int set_algorithm(int algo);  // returns the previous value, -1 if invalid
 
 // Host-side choice of the ping-pong pair for the host ABI: returns true when
 // the result of a `passes`-pass sort started from hbuf[0] lands in hbuf[1].

@@ -74,6 +74,77 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Lanes of the wave whose digit equals this lane's (wave64 "match any" from
+// BITS ballots).  Written as an OR of per-bit mismatches so that each bit costs
+// a sign-extended bit extract, one v_cmp for the ballot and one v_bitop3 per
+// 32-bit half, instead of the select/xor/and chain of `x ? m : ~m`.
+template <int BITS>
+__device__ __forceinline__ uint64_t match_peers(uint32_t d, bool ok) {
+  uint32_t mis_lo = 0u, mis_hi = 0u;
+#pragma unroll
+  for (int bit = 0; bit < BITS; ++bit) {
+    const uint32_t X = (uint32_t)((int32_t)(d << (31 - bit)) >> 31);  // 0 or ~0
+    const uint64_t m = __ballot(X != 0u);
+    mis_lo |= (uint32_t)m ^ X;
+    mis_hi |= (uint32_t)(m >> 32) ^ X;
+  }
+  const uint64_t valid = __ballot(ok);
+  return valid & ~(((uint64_t)mis_hi << 32) | mis_lo);
+}
+
+// Stable rank of each item among this wave's items of the same digit, items
+// in order j = 0..ITEMS-1 and lanes in order within an item.  `row` is the
+// wave's zeroed per-digit counter row in LDS; the last lane of each peer group
+// advances it.  (A leader-only ds_add_rtn + ds_bpermute variant, which lets the
+// items' LDS round trips overlap, cost 20-30 VGPRs and one wave/SIMD of
+// occupancy and was slower on MI355X.)
+template <int BITS, int ITEMS, typename K, typename Op>
+__device__ __forceinline__ void rank_items(const K (&k)[ITEMS], uint32_t (&rk)[ITEMS], uint32_t* row,
+                                           bool full, uint32_t valid, uint32_t wbase, uint32_t lane,
+                                           Op op) {
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t d = op(k[j]);
+    const bool ok = full || (wbase + j * kWave + lane < valid);
+    const uint64_t peers = match_peers<BITS>(d, ok);
+    const uint32_t below = mbcnt64(peers);
+    const uint32_t cnt = (uint32_t)__popcll(peers);
+    const uint32_t base = row[d];
+    rk[j] = base + below;
+    if (ok && below + 1u == cnt) row[d] = base + cnt;  // last peer advances the counter
+  }
+}
+
+// Writes the locally sorted tile s_keys[0..valid) (and values) to global
+// memory: position i goes to outbase[digit] + i.  Full tiles are unrolled so
+// each thread's ITEMS LDS reads and stores issue back to back.
+template <int BLOCK, int ITEMS, bool HAS_V, typename K, typename VS, typename V, typename Op>
+__device__ __forceinline__ void write_tile(const K* s_keys, const VS* s_vals, const uint32_t* s_outbase,
+                                           K* __restrict__ kout, V* __restrict__ vout, uint32_t valid,
+                                           Op op) {
+  const uint32_t tid = threadIdx.x;
+  if (valid == (uint32_t)(BLOCK * ITEMS)) {
+    K kk[ITEMS];
+    uint32_t o[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) kk[j] = s_keys[tid + j * BLOCK];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) o[j] = s_outbase[op(kk[j])] + tid + j * BLOCK;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      kout[o[j]] = kk[j];
+      if constexpr (HAS_V) vout[o[j]] = s_vals[tid + j * BLOCK];
+    }
+  } else {
+    for (uint32_t i = tid; i < valid; i += BLOCK) {
+      const K kk = s_keys[i];
+      const uint32_t o = s_outbase[op(kk)] + i;
+      kout[o] = kk;
+      if constexpr (HAS_V) vout[o] = s_vals[i];
+    }
+  }
+}
+
 // Exclusive scan of one value per thread over the block.  Inclusive wave64
 // scan by __shfl_up (6 steps), wave totals through LDS.  The caller must put
 // a barrier between two uses of s_wsum.
@@ -242,52 +313,43 @@ __global__ __launch_bounds__(BLOCK) void k_downsweep(const K* __restrict__ kin, 
     s_gbase[tid] = l1[i] + l2[i / kScanTile];
   }
 
+  const uint32_t wbase = w * WSPAN;
+  // Register double buffer: the loads of tile t+1 are issued before tile t is
+  // ranked, so their HBM latency overlaps the rank / scan / scatter of tile t.
+  K k[ITEMS], kn[ITEMS];
+  VS v[ITEMS], vn[ITEMS];
+#define LS_LOAD_TILE(KK, VV, T)                                                        \
+  do {                                                                                 \
+    const uint64_t tb_ = (uint64_t)(T) * TILE;                                         \
+    const uint32_t va_ = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tb_);          \
+    const K* kp_ = kin + tb_ + wbase + lane;                                           \
+    const V* vp_ = HAS_V ? vin + tb_ + wbase + lane : nullptr;                         \
+    if (va_ == TILE) {                                                                 \
+      _Pragma("unroll") for (int j = 0; j < ITEMS; ++j) {                              \
+        KK[j] = kp_[j * kWave];                                                        \
+        if constexpr (HAS_V) VV[j] = vp_[j * kWave];                                   \
+      }                                                                                \
+    } else {                                                                           \
+      _Pragma("unroll") for (int j = 0; j < ITEMS; ++j) {                              \
+        const bool ok_ = wbase + j * kWave + lane < va_;                               \
+        KK[j] = ok_ ? kp_[j * kWave] : (K)0;                                           \
+        if constexpr (HAS_V) VV[j] = ok_ ? vp_[j * kWave] : (VS)0;                     \
+      }                                                                                \
+    }                                                                                  \
+  } while (0)
+  if (t0 < t1) LS_LOAD_TILE(k, v, t0);
+
   for (uint32_t t = t0; t < t1; ++t) {
     const uint64_t tile_base = (uint64_t)t * TILE;
     const uint32_t valid = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tile_base);
     const bool full = valid == TILE;
-    const uint32_t wbase = w * WSPAN;
 
+    if (t + 1 < t1) LS_LOAD_TILE(kn, vn, t + 1);
     for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0u;
-
-    K k[ITEMS];
-    VS v[ITEMS];
     uint32_t rk[ITEMS];
-    if (full) {
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        const uint64_t e = tile_base + wbase + j * kWave + lane;
-        k[j] = kin[e];
-        if constexpr (HAS_V) v[j] = vin[e];
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        const uint32_t e = wbase + j * kWave + lane;
-        const bool ok = e < valid;
-        k[j] = ok ? kin[tile_base + e] : (K)0;
-        if constexpr (HAS_V) v[j] = ok ? vin[tile_base + e] : (VS)0;
-      }
-    }
 
     // Wave-level multi-split: items in order, lanes in order => stable.
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-      const uint32_t d = op(k[j]);
-      const bool ok = full || (wbase + j * kWave + lane < valid);
-      uint64_t peers = __ballot(ok);
-#pragma unroll
-      for (int bit = 0; bit < BITS; ++bit) {
-        const bool x = (d >> bit) & 1u;
-        const uint64_t m = __ballot(x);
-        peers &= x ? m : ~m;
-      }
-      const uint32_t below = mbcnt64(peers);
-      const uint32_t cnt = (uint32_t)__popcll(peers);
-      const uint32_t base = s_whist[w][d];
-      rk[j] = base + below;
-      if (ok && below + 1u == cnt) s_whist[w][d] = base + cnt;
-    }
+    rank_items<BITS, ITEMS>(k, rk, s_whist[w], full, valid, wbase, lane, op);
     __syncthreads();
 
     // Per digit: tile count, block exclusive scan, wave prefixes.
@@ -325,14 +387,522 @@ __global__ __launch_bounds__(BLOCK) void k_downsweep(const K* __restrict__ kin, 
     __syncthreads();
 
     // Coalesced write of the digit runs.
+    write_tile<BLOCK, ITEMS, HAS_V>(s_keys, s_vals, s_outbase, kout, vout, valid, op);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      k[j] = kn[j];
+      if constexpr (HAS_V) v[j] = vn[j];
+    }
+  }
+#undef LS_LOAD_TILE
+}
+
+// ============================================================================
+// onesweep path: one histogram read for all digits, then ONE kernel per digit
+// pass with decoupled look-back over dynamically numbered tiles.
+// ============================================================================
+constexpr uint32_t kFlagAgg = 1u << 30;  // status word: tile aggregate published
+constexpr uint32_t kFlagInc = 2u << 30;  // status word: inclusive prefix published
+constexpr uint32_t kValMask = (1u << 30) - 1u;
+constexpr uint32_t kSpinLimit = 1u << 24;
+
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Histograms of the 8-bit windows at shifts lo, lo+8, ... (window q keeps
+// min(8, hi - (lo+8q)) bits).  4-bit digit histograms are nibble sums of these.
+// Also zeroes the first look-back status buffer (rows of this sort's tiles).
+template <typename K, int NW>
+__global__ __launch_bounds__(256) void k_window_hist(const K* __restrict__ keys, uint32_t n, uint32_t lo,
+                                                     uint32_t hi, uint32_t* __restrict__ whist,
+                                                     uint32_t* __restrict__ zero_buf, uint32_t zero_words) {
+  constexpr int NWAVE = 4;  // wave-private copies: fewer same-address LDS atomics
+  constexpr int UNROLL = 4;  // 16-byte loads in flight per lane
+  __shared__ uint32_t s_h[NWAVE][NW][256];
+  const int wv = threadIdx.x / kWave;
+  for (int i = threadIdx.x; i < NWAVE * NW * 256; i += 256) (&s_h[0][0][0])[i] = 0u;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  const uint64_t gid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  for (uint64_t i = gid; i < zero_words; i += stride) zero_buf[i] = 0u;
+  uint32_t msk[NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) {
+    const int s = (int)lo + 8 * q;
+    const int nb = min(8, (int)hi - s);
+    msk[q] = nb <= 0 ? 0u : ((1u << nb) - 1u);
+  }
+  __syncthreads();
+  auto count = [&](K k) {
+#pragma unroll
+    for (int q = 0; q < NW; ++q)
+      if (msk[q]) atomicAdd(&s_h[wv][q][(uint32_t)(k >> (lo + 8 * q)) & msk[q]], 1u);
+  };
+  using V = typename VecOf<K>::type;
+  constexpr int PER = VecOf<K>::n;
+  const uint64_t nvec = ((reinterpret_cast<uintptr_t>(keys) % 16) == 0) ? n / PER : 0;
+  const V* vp = reinterpret_cast<const V*>(keys);
+  uint64_t i = gid;
+  for (; i + (UNROLL - 1) * stride < nvec; i += UNROLL * stride) {
+    V v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) v[u] = vp[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+      for (int c = 0; c < PER; ++c) count(vec_elem(v[u], c));
+  }
+  for (; i < nvec; i += stride) {
+    const V v = vp[i];
+#pragma unroll
+    for (int c = 0; c < PER; ++c) count(vec_elem(v, c));
+  }
+  for (uint64_t e = nvec * PER + gid; e < n; e += stride) count(keys[e]);
+  __syncthreads();
+  for (int e = threadIdx.x; e < NW * 256; e += 256) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int x = 0; x < NWAVE; ++x) c += (&s_h[x][0][0])[e];
+    if (c) atomicAdd(&whist[e], c);
+  }
+}
+
+// gbase[p][d] = exclusive scan over digits of pass p's histogram.
+template <int BITS>
+__global__ __launch_bounds__(256) void k_pass_offsets(const uint32_t* __restrict__ whist,
+                                                      uint32_t* __restrict__ gbase) {
+  constexpr int RADIX = 1 << BITS;
+  __shared__ uint32_t s_wsum[4];
+  const int p = blockIdx.x;
+  const int d = threadIdx.x;
+  uint32_t c = 0;
+  if (d < RADIX) {
+    if (BITS == 8) {
+      c = whist[p * 256 + d];
+    } else {  // BITS == 4: nibble of window p/2
+      const uint32_t* w = whist + (p >> 1) * 256;
+      if ((p & 1) == 0) {
+        for (int h = 0; h < 16; ++h) c += w[h * 16 + d];
+      } else {
+        for (int l = 0; l < 16; ++l) c += w[d * 16 + l];
+      }
+    }
+  }
+  uint32_t total;
+  const uint32_t ex = block_exclusive_scan<256>(c, s_wsum, total);
+  if (d < RADIX) gbase[p * RADIX + d] = ex;
+}
+
+template <int BITS, int BLOCK, int ITEMS, typename K, typename V, int ABL = 0>
+__global__ __launch_bounds__(BLOCK) void k_onesweep(const K* __restrict__ kin, K* __restrict__ kout,
+                                                    const V* __restrict__ vin, V* __restrict__ vout,
+                                                    uint32_t n, RadixDigit op, uint32_t* status,
+                                                    uint32_t* __restrict__ status_next,
+                                                    const uint32_t* __restrict__ gbase,
+                                                    uint32_t* tile_counter, uint32_t* err) {
+  constexpr bool HAS_V = !std::is_same<V, NoValue>::value;
+  using VS = typename std::conditional<HAS_V, V, uint8_t>::type;
+  constexpr int RADIX = 1 << BITS;
+  constexpr int WAVES = BLOCK / kWave;
+  constexpr int TILE = BLOCK * ITEMS;
+  constexpr int WSPAN = ITEMS * kWave;
+  static_assert(RADIX <= BLOCK, "one digit per thread in the block phase");
+
+  __shared__ K s_keys[TILE];
+  __shared__ VS s_vals[HAS_V ? TILE : 1];
+  __shared__ uint32_t s_whist[WAVES][RADIX];
+  __shared__ uint32_t s_outbase[RADIX];
+  __shared__ uint32_t s_wsum[WAVES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = tid / kWave;
+
+  // Tile id = dispatch order.  A single ticket counter saturates at ~88
+  // atomics/us (MI355X_MICROARCH "dequeue"), i.e. ~750 us for 64K tiles, so
+  // the look-back relies on the in-order workgroup dispatch observed on
+  // gfx950 instead; every wait is bounded (kSpinLimit) and reported in *err.
+  const uint32_t t = blockIdx.x;
+  for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0u;
+  if (status_next != nullptr && tid < RADIX) status_next[(size_t)t * RADIX + tid] = 0u;
+
+  const uint64_t tile_base = (uint64_t)t * TILE;
+  const uint32_t valid = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tile_base);
+  const bool full = valid == TILE;
+  const uint32_t wbase = w * WSPAN;
+
+  K k[ITEMS];
+  VS v[ITEMS];
+  uint32_t rk[ITEMS];
+  {
+    // one 64-bit base per lane, immediate offsets per item
+    const K* kp = kin + tile_base + wbase + lane;
+    const V* vp = HAS_V ? vin + tile_base + wbase + lane : nullptr;
+    if (full) {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        k[j] = kp[j * kWave];
+        if constexpr (HAS_V) v[j] = vp[j * kWave];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        const bool ok = wbase + j * kWave + lane < valid;
+        k[j] = ok ? kp[j * kWave] : (K)0;
+        if constexpr (HAS_V) v[j] = ok ? vp[j * kWave] : (VS)0;
+      }
+    }
+  }
+
+  rank_items<BITS, ITEMS>(k, rk, s_whist[w], full, valid, wbase, lane, op);
+  __syncthreads();
+
+  uint32_t cnt_d = 0;
+  if (tid < RADIX) {
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) cnt_d += s_whist[i][tid];
+    // publish this tile's aggregate as early as possible
+    st_agent(status + (size_t)t * RADIX + tid, (t == 0 ? kFlagInc : kFlagAgg) | cnt_d);
+  }
+  uint32_t tile_total;
+  const uint32_t excl = block_exclusive_scan<BLOCK>(cnt_d, s_wsum, tile_total);
+  if (tid < RADIX) {
+    uint32_t prefix = 0;
+    if (t > 0 && ABL != 3) {
+      // Windowed look-back: LB predecessor words per round trip (independent
+      // loads in flight), consumed nearest-first until an inclusive prefix.
+      // 64-B rows (4-bit) are cheap to over-read; 1-KB rows (8-bit) are not
+      constexpr int LB = RADIX <= 16 ? 8 : 2;
+      int64_t j = (int64_t)t - 1;
+      uint32_t spins = 0;
+      bool done = false;
+      while (!done) {
+        uint32_t sv[LB];
+#pragma unroll
+        for (int i = 0; i < LB; ++i)
+          sv[i] = (j - i >= 0) ? ld_agent(status + (size_t)(j - i) * RADIX + tid) : kFlagInc;
+        int used = 0;
+#pragma unroll
+        for (int i = 0; i < LB; ++i) {
+          if (done || used < i) continue;  // stop at the first unpublished word
+          if ((sv[i] & ~kValMask) == 0u) continue;
+          prefix += sv[i] & kValMask;
+          used = i + 1;
+          done = (sv[i] & kFlagInc) != 0u;
+        }
+        j -= used;
+        if (!done && used < LB) {
+          if (++spins > kSpinLimit) {
+            atomicOr(err, 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      st_agent(status + (size_t)t * RADIX + tid, kFlagInc | (prefix + cnt_d));
+    }
+    uint32_t run = excl;
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) {
+      const uint32_t c = s_whist[i][tid];
+      s_whist[i][tid] = run;
+      run += c;
+    }
+    s_outbase[tid] = gbase[tid] + prefix - excl;
+  }
+  __syncthreads();
+
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const bool ok = full || (wbase + j * kWave + lane < valid);
+    if (ok) {
+      const uint32_t pos = s_whist[w][op(k[j])] + rk[j];
+      s_keys[pos] = k[j];
+      if constexpr (HAS_V) s_vals[pos] = v[j];
+    }
+  }
+  __syncthreads();
+
+  if constexpr (ABL == 0) {
+    write_tile<BLOCK, ITEMS, HAS_V>(s_keys, s_vals, s_outbase, kout, vout, valid, op);
+    return;
+  }
+  for (uint32_t i = tid; i < valid; i += BLOCK) {
+    const K kk = s_keys[i];
+    const uint32_t o = s_outbase[op(kk)] + i;
+    if constexpr (ABL == 0) {
+    } else if constexpr (ABL == 1) {  // diagnostic: coalesced writes (wrong result)
+      kout[tile_base + i] = kk + o;
+    } else {  // diagnostic: no global writes (wrong result)
+      asm volatile("" ::"v"(kk), "v"(o));
+    }
+  }
+}
+
+// ============================================================================
+// tile-offset path ("tiles"): per-tile digit counts -> two-level column scan
+// -> one pass kernel per digit whose tiles know their global run offsets up
+// front (no look-back).  With 4-bit digits the pass kernel also counts the
+// NEXT digit of every key per destination tile (LDS-aggregated atomics), so
+// the keys are read once per pass plus once per sort.
+// Layout: C[tile][RADIX] uint32; chunk totals B[chunk][RADIX] with
+// kColRows tiles per chunk.  After the scan, tile t's run of digit d starts
+// at C[t][d] + B[t / kColRows][d].
+// ============================================================================
+constexpr int kColRowsPerLane = 16;
+
+// Per-tile digit counts of the first pass; also zeroes `zero_buf` (the
+// next-pass count buffer).  One block per tile.
+template <int BITS, int BLOCK, int ITEMS, typename K>
+__global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ keys, uint32_t n, RadixDigit op,
+                                                       uint32_t* __restrict__ counts,
+                                                       uint32_t* __restrict__ zero_buf, uint32_t zero_words) {
+  constexpr int RADIX = 1 << BITS;
+  constexpr int TILE = BLOCK * ITEMS;
+  constexpr int COPIES = RADIX <= 16 ? 16 : 1;  // spread same-digit LDS atomics
+  __shared__ uint32_t s_h[COPIES][RADIX];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < COPIES * RADIX; i += BLOCK) (&s_h[0][0])[i] = 0u;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + tid; i < zero_words; i += (uint64_t)gridDim.x * BLOCK)
+    zero_buf[i] = 0u;
+  __syncthreads();
+  const uint32_t cp = tid % COPIES;
+  const uint64_t tile_base = (uint64_t)blockIdx.x * TILE;
+  const uint32_t valid = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tile_base);
+  using VT = typename VecOf<K>::type;
+  constexpr int PER = VecOf<K>::n;
+  if (valid == TILE && (reinterpret_cast<uintptr_t>(keys) % 16) == 0) {
+    const VT* vp = reinterpret_cast<const VT*>(keys + tile_base);
+    VT v[ITEMS / PER];
+#pragma unroll
+    for (int j = 0; j < ITEMS / PER; ++j) v[j] = vp[j * BLOCK + tid];
+#pragma unroll
+    for (int j = 0; j < ITEMS / PER; ++j)
+#pragma unroll
+      for (int c = 0; c < PER; ++c) atomicAdd(&s_h[cp][op(vec_elem(v[j], c))], 1u);
+  } else {
+    for (uint32_t i = tid; i < valid; i += BLOCK) atomicAdd(&s_h[cp][op(keys[tile_base + i])], 1u);
+  }
+  __syncthreads();
+  for (uint32_t d = tid; d < RADIX; d += BLOCK) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int c = 0; c < COPIES; ++c) s += s_h[c][d];
+    counts[(size_t)blockIdx.x * RADIX + d] = s;
+  }
+}
+
+// Level 1 of the column scan: block c owns rows [c*CH, (c+1)*CH), CH =
+// kColRowsPerLane * (256 / RADIX).  Thread (row-lane s, column d) sums its
+// kColRowsPerLane contiguous rows, the row-lanes are scanned through LDS, and
+// the rows are rewritten with the chunk-local exclusive prefix.  The chunk
+// totals go to B[c][d].
+template <int RADIX>
+__global__ __launch_bounds__(256) void k_colscan_l1(uint32_t* __restrict__ C, uint32_t rows,
+                                                    uint32_t* __restrict__ B) {
+  constexpr int L = 256 / RADIX;
+  constexpr int CH = kColRowsPerLane * L;
+  __shared__ uint32_t s_sum[256];
+  const uint32_t d = threadIdx.x % RADIX, s = threadIdx.x / RADIX;
+  const uint64_t r0 = (uint64_t)blockIdx.x * CH + (uint64_t)s * kColRowsPerLane;
+  uint32_t x[kColRowsPerLane];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < kColRowsPerLane; ++i) {
+    x[i] = (r0 + i < rows) ? C[(r0 + i) * RADIX + d] : 0u;
+    sum += x[i];
+  }
+  s_sum[threadIdx.x] = sum;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+  for (uint32_t q = 0; q < (uint32_t)L; ++q) {
+    const uint32_t v = s_sum[q * RADIX + d];
+    run += q < s ? v : 0u;
+    tot += v;
+  }
+#pragma unroll
+  for (int i = 0; i < kColRowsPerLane; ++i) {
+    if (r0 + i < rows) C[(r0 + i) * RADIX + d] = run;
+    run += x[i];
+  }
+  if (s == 0) B[(size_t)blockIdx.x * RADIX + d] = tot;
+}
+
+// Level 2 (one block): exclusive column scan of B[nchunks][RADIX] in place,
+// plus the digit starts (exclusive scan of the column totals) added in.
+template <int RADIX>
+__global__ __launch_bounds__(256) void k_colscan_l2(uint32_t* __restrict__ B, uint32_t nchunks) {
+  constexpr int L = 256 / RADIX;
+  __shared__ uint32_t s_sum[256];
+  __shared__ uint32_t s_wsum[4];
+  __shared__ uint32_t s_dstart[RADIX];
+  const uint32_t d = threadIdx.x % RADIX, s = threadIdx.x / RADIX;
+  const uint32_t per = (nchunks + L - 1) / L;  // rows per row-lane
+  const uint32_t a = s * per, b = min(nchunks, a + per);
+  uint32_t sum = 0;
+  for (uint32_t r = a; r < b; ++r) sum += B[(size_t)r * RADIX + d];
+  s_sum[threadIdx.x] = sum;
+  __syncthreads();
+  uint32_t run = 0, tot = 0;
+  for (uint32_t q = 0; q < (uint32_t)L; ++q) {
+    const uint32_t v = s_sum[q * RADIX + d];
+    run += q < s ? v : 0u;
+    tot += v;
+  }
+  // digit starts: exclusive scan over d of the column totals (thread d, s == 0)
+  uint32_t total_unused;
+  const uint32_t ds = block_exclusive_scan<256>(s == 0 ? tot : 0u, s_wsum, total_unused);
+  if (s == 0) s_dstart[d] = ds;
+  __syncthreads();
+  run += s_dstart[d];
+  for (uint32_t r = a; r < b; ++r) {
+    const uint32_t v = B[(size_t)r * RADIX + d];
+    B[(size_t)r * RADIX + d] = run;
+    run += v;
+  }
+}
+
+// The pass kernel of the tile-offset path: the onesweep tile body with the
+// run offsets read from the scanned counts.  FUSE: also count the next digit
+// (op_next) of every written key per destination tile into C_next (4-bit
+// digits: a run of one digit covers at most two destination tiles, so the
+// per-tile aggregate has RADIX x 2 x RADIX entries).  The tile's row of C is
+// zeroed after use (it becomes the C_next of the pass after the next).
+template <int BITS, int BLOCK, int ITEMS, typename K, typename V, bool FUSE>
+__global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, K* __restrict__ kout,
+                                                     const V* __restrict__ vin, V* __restrict__ vout,
+                                                     uint32_t n, RadixDigit op, RadixDigit op_next,
+                                                     uint32_t* __restrict__ C, const uint32_t* __restrict__ B,
+                                                     uint32_t* __restrict__ C_next) {
+  constexpr bool HAS_V = !std::is_same<V, NoValue>::value;
+  using VS = typename std::conditional<HAS_V, V, uint8_t>::type;
+  constexpr int RADIX = 1 << BITS;
+  constexpr int WAVES = BLOCK / kWave;
+  constexpr int TILE = BLOCK * ITEMS;
+  constexpr int WSPAN = ITEMS * kWave;
+  constexpr int CH = kColRowsPerLane * (256 / RADIX);
+  static_assert(RADIX <= BLOCK, "one digit per thread in the block phase");
+  static_assert(!FUSE || RADIX * 2 * RADIX <= 2 * BLOCK, "fused next-count table: two entries per thread");
+
+  __shared__ K s_keys[TILE];
+  __shared__ VS s_vals[HAS_V ? TILE : 1];
+  __shared__ uint32_t s_whist[WAVES][RADIX];
+  __shared__ uint32_t s_outbase[RADIX];
+  __shared__ uint32_t s_tfirst[RADIX];
+  __shared__ uint32_t s_next[FUSE ? RADIX * 2 * RADIX : 1];
+  __shared__ uint32_t s_wsum[WAVES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = tid / kWave;
+  const uint32_t t = blockIdx.x;
+  for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0u;
+  if constexpr (FUSE) {
+    for (int i = tid; i < RADIX * 2 * RADIX; i += BLOCK) s_next[i] = 0u;
+  }
+  // this tile's run offsets (independent of every other tile)
+  uint32_t gofs = 0;
+  if (tid < RADIX) {
+    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid];
+    C[(size_t)t * RADIX + tid] = 0u;
+  }
+
+  const uint64_t tile_base = (uint64_t)t * TILE;
+  const uint32_t valid = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tile_base);
+  const bool full = valid == TILE;
+  const uint32_t wbase = w * WSPAN;
+
+  K k[ITEMS];
+  VS v[ITEMS];
+  uint32_t rk[ITEMS];
+  {
+    const K* kp = kin + tile_base + wbase + lane;
+    const V* vp = HAS_V ? vin + tile_base + wbase + lane : nullptr;
+    if (full) {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        k[j] = kp[j * kWave];
+        if constexpr (HAS_V) v[j] = vp[j * kWave];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        const bool ok = wbase + j * kWave + lane < valid;
+        k[j] = ok ? kp[j * kWave] : (K)0;
+        if constexpr (HAS_V) v[j] = ok ? vp[j * kWave] : (VS)0;
+      }
+    }
+  }
+  rank_items<BITS, ITEMS>(k, rk, s_whist[w], full, valid, wbase, lane, op);
+  __syncthreads();
+
+  uint32_t cnt_d = 0;
+  if (tid < RADIX) {
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) cnt_d += s_whist[i][tid];
+  }
+  uint32_t tile_total;
+  const uint32_t excl = block_exclusive_scan<BLOCK>(cnt_d, s_wsum, tile_total);
+  if (tid < RADIX) {
+    uint32_t run = excl;
+#pragma unroll
+    for (int i = 0; i < WAVES; ++i) {
+      const uint32_t c = s_whist[i][tid];
+      s_whist[i][tid] = run;
+      run += c;
+    }
+    s_outbase[tid] = gofs - excl;
+    s_tfirst[tid] = gofs / TILE;  // first destination tile of this digit's run
+  }
+  __syncthreads();
+
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const bool ok = full || (wbase + j * kWave + lane < valid);
+    if (ok) {
+      const uint32_t pos = s_whist[w][op(k[j])] + rk[j];
+      s_keys[pos] = k[j];
+      if constexpr (HAS_V) s_vals[pos] = v[j];
+    }
+  }
+  __syncthreads();
+
+  if constexpr (!FUSE) {
+    write_tile<BLOCK, ITEMS, HAS_V>(s_keys, s_vals, s_outbase, kout, vout, valid, op);
+  } else {
     for (uint32_t i = tid; i < valid; i += BLOCK) {
       const K kk = s_keys[i];
-      const uint32_t o = s_outbase[op(kk)] + i;
+      const uint32_t d = op(kk);
+      const uint32_t o = s_outbase[d] + i;
       kout[o] = kk;
       if constexpr (HAS_V) vout[o] = s_vals[i];
+      const uint32_t slot = o / TILE - s_tfirst[d];  // 0 or 1
+      atomicAdd(&s_next[(d * 2 + slot) * RADIX + op_next(kk)], 1u);
     }
     __syncthreads();
+    for (int e = tid; e < RADIX * 2 * RADIX; e += BLOCK) {
+      const uint32_t c = s_next[e];
+      if (c) {
+        const uint32_t d = e / (2 * RADIX), slot = (e / RADIX) & 1u, dn = e % RADIX;
+        atomicAdd(&C_next[(size_t)(s_tfirst[d] + slot) * RADIX + dn], c);
+      }
+    }
   }
+}
+
+// bounds[g] = exclusive scan of window 0 (the whole group when width <= 8).
+__global__ __launch_bounds__(256) void k_bounds_from_window(const uint32_t* __restrict__ whist,
+                                                            uint32_t ngroups, uint32_t* __restrict__ bounds) {
+  __shared__ uint32_t s_wsum[4];
+  const uint32_t g = threadIdx.x;
+  const uint32_t c = g < ngroups ? whist[g] : 0u;
+  uint32_t total;
+  const uint32_t ex = block_exclusive_scan<256>(c, s_wsum, total);
+  if (g < ngroups) bounds[g] = ex;
 }
 
 // ----------------------------------------------------------------------------
@@ -525,14 +1095,57 @@ hipError_t Workspace::ensure_seg(size_t m) {
   return hipSuccess;
 }
 
+hipError_t Workspace::ensure_tiles(size_t count_words, size_t chunk_words) {
+  if (count_words > tc_cap) {
+    for (auto& p : tc) {
+      if (p) { (void)hipFree(p); p = nullptr; }
+    }
+    tc_cap = 0;
+    LS_TRY(hipMalloc(&tc[0], count_words * sizeof(uint32_t)));
+    LS_TRY(hipMalloc(&tc[1], count_words * sizeof(uint32_t)));
+    tc_cap = count_words;
+  }
+  if (chunk_words > tb_cap) {
+    if (tb) { (void)hipFree(tb); tb = nullptr; }
+    tb_cap = 0;
+    LS_TRY(hipMalloc(&tb, chunk_words * sizeof(uint32_t)));
+    tb_cap = chunk_words;
+  }
+  return hipSuccess;
+}
+
+hipError_t Workspace::ensure_onesweep(size_t status_words) {
+  if (!os_small) {
+    LS_TRY(hipMalloc(&os_small, kOsSmallWords * sizeof(uint32_t)));
+    LS_TRY(hipMemset(os_small, 0, kOsSmallWords * sizeof(uint32_t)));
+  }
+  if (status_words <= os_status_cap) return hipSuccess;
+  for (auto& p : os_status) {
+    if (p) { (void)hipFree(p); p = nullptr; }
+  }
+  os_status_cap = 0;
+  LS_TRY(hipMalloc(&os_status[0], status_words * sizeof(uint32_t)));
+  LS_TRY(hipMalloc(&os_status[1], status_words * sizeof(uint32_t)));
+  LS_TRY(hipMemset(os_status[1], 0, status_words * sizeof(uint32_t)));
+  os_status_cap = status_words;
+  return hipSuccess;
+}
+
 void Workspace::release() {
   int prev = -1;
   (void)hipGetDevice(&prev);
   (void)hipSetDevice(device);
   if (stream) (void)hipStreamSynchronize(stream);
   for (auto p : {(void*)counts, (void*)scan_l1, (void*)scan_l2, hbuf[0], hbuf[1], (void*)dbounds,
-                 (void*)seg_dev, (void*)hist_tmp})
+                 (void*)seg_dev, (void*)hist_tmp, (void*)os_status[0], (void*)os_status[1],
+                 (void*)os_small})
     if (p) (void)hipFree(p);
+  os_status[0] = os_status[1] = os_small = nullptr;
+  for (auto p : {(void*)tc[0], (void*)tc[1], (void*)tb})
+    if (p) (void)hipFree(p);
+  tc[0] = tc[1] = tb = nullptr;
+  tc_cap = tb_cap = 0;
+  os_status_cap = 0;
   if (seg_host) (void)hipHostFree(seg_host);
   counts = scan_l1 = scan_l2 = dbounds = hist_tmp = nullptr;
   hbuf[0] = hbuf[1] = nullptr;
@@ -602,6 +1215,147 @@ hipError_t run_digit_pass(Workspace& ws, int bits, const K* kin, K* kout, const 
   return hipErrorInvalidValue;
 }
 
+// Algorithm choice: onesweep (default) needs n < 2^30 (30-bit look-back
+// values); LIBSORT_ALGO=rts forces reduce-then-scan.
+bool use_onesweep(size_t n) {
+  if (get_algorithm() == 2) return false;
+  return n < (1ull << 30);
+}
+
+// Which pass algorithm a sort with `bits`-bit digits over n keys runs.
+int choose_algorithm(size_t n, int bits) {
+  const int a = get_algorithm();
+  if (n >= (1ull << 30)) return 2;  // 30-bit look-back values; 32-bit tile offsets
+  if (a == 3) return bits == 4 ? 3 : 1;
+  if (a == 1 || a == 2) return a;
+  return bits == 4 ? 3 : 1;  // auto
+}
+
+constexpr int kTpBlock = 256;
+constexpr int kTpItems = 16;  // 4096-key tiles (u32 keys)
+
+template <typename K>
+constexpr int tp_items() { return sizeof(K) == 8 ? 8 : kTpItems; }
+
+// Per-tile counts of pass 0 (4-bit digit at lo) into tc[0]; zero tc[1].
+template <typename K>
+hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, uint32_t tiles,
+                          hipStream_t st) {
+  constexpr int TILE = kTpBlock * tp_items<K>();
+  (void)TILE;
+  const uint32_t chunks = (tiles + kColRowsPerLane * 16 - 1) / (kColRowsPerLane * 16);
+  LS_TRY(ws.ensure_tiles((size_t)tiles * 16, (size_t)chunks * 16));
+  const int nb = std::min(4, hi - lo);
+  RadixDigit op0{(uint32_t)lo, (1u << nb) - 1u};
+  ScopedTimer tm("tilecounts", st, n);
+  hipLaunchKernelGGL((k_tile_counts<4, kTpBlock, tp_items<K>(), K>), dim3(tiles), dim3(kTpBlock), 0, st, in,
+                     (uint32_t)n, op0, ws.tc[0], ws.tc[1], tiles * 16u);
+  return hipGetLastError();
+}
+
+template <typename K, typename V>
+hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout, size_t n, int p, int P,
+                      int lo, int hi, uint32_t tiles, hipStream_t st) {
+  const uint32_t chunks = (tiles + kColRowsPerLane * 16 - 1) / (kColRowsPerLane * 16);
+  uint32_t* cur = ws.tc[p & 1];
+  uint32_t* nxt = ws.tc[(p + 1) & 1];
+  {
+    ScopedTimer tm("colscan", st, tiles);
+    hipLaunchKernelGGL(k_colscan_l1<16>, dim3(chunks), dim3(256), 0, st, cur, tiles, ws.tb);
+    LS_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_colscan_l2<16>, dim3(1), dim3(256), 0, st, ws.tb, chunks);
+    LS_TRY(hipGetLastError());
+  }
+  const int shift = lo + 4 * p;
+  const int nb = std::min(4, hi - shift);
+  RadixDigit op{(uint32_t)shift, (1u << nb) - 1u};
+  const bool fuse = p + 1 < P;
+  const int nb2 = fuse ? std::min(4, hi - shift - 4) : 1;
+  RadixDigit op_next{(uint32_t)(fuse ? shift + 4 : 0), (1u << nb2) - 1u};
+  ScopedTimer tm("tilepass", st, n);
+  if (fuse)
+    hipLaunchKernelGGL((k_tile_pass<4, kTpBlock, tp_items<K>(), K, V, true>), dim3(tiles), dim3(kTpBlock), 0,
+                       st, kin, kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
+  else
+    hipLaunchKernelGGL((k_tile_pass<4, kTpBlock, tp_items<K>(), K, V, false>), dim3(tiles), dim3(kTpBlock), 0,
+                       st, kin, kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
+  return hipGetLastError();
+}
+
+template <typename K>
+constexpr int os_items() { return sizeof(K) == 8 ? kOsItemsU64 : kOsItemsU32; }
+
+// Threads per onesweep tile (256 / 512 / 1024); LIBSORT_OS_BLOCK overrides.
+int os_block() {
+  const char* s = getenv("LIBSORT_OS_BLOCK");
+  const int b = s ? atoi(s) : kOsBlock;
+  return (b == 512 || b == 1024) ? b : 256;
+}
+
+// memset of the small block, window histograms (+ zero of status buffer 0),
+// per-pass digit bases.
+template <typename K>
+hipError_t onesweep_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, int bits, int P,
+                             uint32_t tiles, hipStream_t st) {
+  const int radix = 1 << bits;
+  LS_TRY(ws.ensure_onesweep((size_t)tiles * radix));
+  LS_TRY(hipMemsetAsync(ws.os_small, 0, kOsZeroWords * sizeof(uint32_t), st));
+  const int nw = (hi - lo + 7) / 8;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 1023) / 1024, (uint64_t)std::max(1, ws.num_cus) * 4);
+  const uint32_t zero_words = tiles * (uint32_t)radix;
+  {
+    ScopedTimer tm("whist", st, n);
+#define LS_W(NW)                                                                                     \
+  case NW:                                                                                         \
+    hipLaunchKernelGGL((k_window_hist<K, NW>), dim3(blocks), dim3(256), 0, st, in, (uint32_t)n,    \
+                       (uint32_t)lo, (uint32_t)hi, ws.os_small + kOsWhist, ws.os_status[0],        \
+                       zero_words);                                                                \
+    break;
+    switch (nw) {
+      LS_W(1) LS_W(2) LS_W(3) LS_W(4) LS_W(5) LS_W(6) LS_W(7) LS_W(8)
+      default: return hipErrorInvalidValue;
+    }
+#undef LS_W
+    LS_TRY(hipGetLastError());
+  }
+  if (bits == 8)
+    hipLaunchKernelGGL(k_pass_offsets<8>, dim3(P), dim3(256), 0, st, ws.os_small + kOsWhist,
+                       ws.os_small + kOsGbase);
+  else
+    hipLaunchKernelGGL(k_pass_offsets<4>, dim3(P), dim3(256), 0, st, ws.os_small + kOsWhist,
+                       ws.os_small + kOsGbase);
+  return hipGetLastError();
+}
+
+template <int BITS, typename K, typename V>
+hipError_t onesweep_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout, size_t n, int p,
+                         int P, uint32_t shift, uint32_t nbits, uint32_t tiles, hipStream_t st) {
+  constexpr int RADIX = 1 << BITS;
+  RadixDigit op{shift, (nbits >= 32) ? 0xffffffffu : ((1u << nbits) - 1u)};
+  uint32_t* status = ws.os_status[p & 1];
+  uint32_t* next = (p + 1 < P) ? ws.os_status[(p + 1) & 1] : nullptr;
+  ScopedTimer tm("onesweep", st, n);
+#define LS_OS(B, A)                                                                                      \
+  hipLaunchKernelGGL((k_onesweep<BITS, B, os_items<K>(), K, V, A>), dim3(tiles), dim3(B), 0, st, kin, kout, \
+                     vin, vout, (uint32_t)n, op, status, next, ws.os_small + kOsGbase + p * RADIX,        \
+                     ws.os_small + kOsCounters + p, ws.os_small + kOsErr)
+  const char* abl = getenv("LIBSORT_DIAG_ABLATION");  // diagnostics only: 1 = coalesced, 2 = no writes
+  const int a = (abl && std::is_same<V, NoValue>::value) ? atoi(abl) : 0;
+  switch (os_block() * 4 + (a >= 1 && a <= 3 ? a : 0)) {
+    case 512 * 4 + 3: LS_OS(512, 3); break;
+    case 256 * 4 + 3: LS_OS(256, 3); break;
+    case 1024 * 4: LS_OS(1024, 0); break;
+    case 512 * 4: LS_OS(512, 0); break;
+    case 512 * 4 + 1: LS_OS(512, 1); break;
+    case 512 * 4 + 2: LS_OS(512, 2); break;
+    case 256 * 4 + 1: LS_OS(256, 1); break;
+    case 256 * 4 + 2: LS_OS(256, 2); break;
+    default: LS_OS(256, 0); break;
+  }
+#undef LS_OS
+  return hipGetLastError();
+}
+
 template <typename K, typename V>
 hipError_t copy_buf(K* dst, const K* src, V* vdst, const V* vsrc, size_t n, hipStream_t st) {
   if (dst != src) LS_TRY(hipMemcpyAsync(dst, src, n * sizeof(K), hipMemcpyDeviceToDevice, st));
@@ -626,12 +1380,31 @@ hipError_t sort_impl(Workspace& ws, const K* in, K* out, K* tmp, const V* vin, V
   auto dst_is_out = [&](int p) { return inplace ? (p & 1) != 0 : ((P - 1 - p) & 1) == 0; };
   const K* ksrc = in;
   const V* vsrc = vin;
+  const int algo = (bits == 4 || bits == 8) ? choose_algorithm(n, bits) : 2;
+  const bool os = algo == 1;
+  const bool tp = algo == 3;
+  ws.last_algo = algo;
+  const int OS_TILE = os_block() * os_items<K>();
+  const uint32_t tiles = (uint32_t)((n + OS_TILE - 1) / OS_TILE);
+  constexpr int TP_TILE = kTpBlock * tp_items<K>();
+  const uint32_t tp_tiles = (uint32_t)((n + TP_TILE - 1) / TP_TILE);
+  if (os) LS_TRY(onesweep_prologue<K>(ws, in, n, lo, hi, bits, P, tiles, st));
+  if (tp) LS_TRY(tiles_prologue<K>(ws, in, n, lo, hi, tp_tiles, st));
   for (int p = 0; p < P; ++p) {
     const int shift = lo + p * bits;
     const int nb = std::min(bits, hi - shift);
     K* kdst = dst_is_out(p) ? out : tmp;
     V* vdst = dst_is_out(p) ? vout : vtmp;
-    LS_TRY(run_digit_pass<K, V>(ws, bits, ksrc, kdst, vsrc, vdst, n, (uint32_t)shift, (uint32_t)nb, st));
+    if (tp) {
+      LS_TRY((tiles_pass<K, V>(ws, ksrc, kdst, vsrc, vdst, n, p, P, lo, hi, tp_tiles, st)));
+    } else if (os) {
+      if (bits == 8)
+        LS_TRY((onesweep_pass<8, K, V>(ws, ksrc, kdst, vsrc, vdst, n, p, P, (uint32_t)shift, (uint32_t)nb, tiles, st)));
+      else
+        LS_TRY((onesweep_pass<4, K, V>(ws, ksrc, kdst, vsrc, vdst, n, p, P, (uint32_t)shift, (uint32_t)nb, tiles, st)));
+    } else {
+      LS_TRY(run_digit_pass<K, V>(ws, bits, ksrc, kdst, vsrc, vdst, n, (uint32_t)shift, (uint32_t)nb, st));
+    }
     ksrc = kdst;
     vsrc = vdst;
   }
@@ -651,6 +1424,19 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
     ScopedTimer tm("bounds", st, n);
     if (n == 0) {
       LS_TRY(hipMemsetAsync(d_bounds, 0, (size_t)ngroups * sizeof(uint32_t), st));
+    } else if (ws.last_algo == 3 && width <= 4) {
+      // tile path, single pass: chunk 0's scanned totals are the digit starts
+      LS_TRY(hipMemcpyAsync(d_bounds, ws.tb, (size_t)ngroups * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    } else if (ws.last_algo == 3) {
+      const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 256) / 256, 4096);
+      hipLaunchKernelGGL(k_group_bounds<uint32_t>, dim3(blocks), dim3(256), 0, st, out, (uint32_t)n,
+                         (uint32_t)lo, ngroups - 1u, ngroups, d_bounds);
+      LS_TRY(hipGetLastError());
+    } else if (ws.last_algo == 1 && width <= 8) {
+      // onesweep: window 0 holds exactly the group histogram
+      hipLaunchKernelGGL(k_bounds_from_window, dim3(1), dim3(256), 0, st, ws.os_small + kOsWhist, ngroups,
+                         d_bounds);
+      LS_TRY(hipGetLastError());
     } else if (num_passes(width, digit_bits) == 1) {
       // single pass: the counters of that pass are still in the workspace
       constexpr int TILE = kBlock * kItemsU32;

@@ -53,12 +53,14 @@ _SIGS = [
     ("libsortPopulateDevice", ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_uint64, _vp]),
     ("libsortSetDigitBits", ctypes.c_int, [ctypes.c_int]),
     ("libsortGetDigitBits", ctypes.c_int, []),
+    ("libsortSetAlgorithm", ctypes.c_int, [ctypes.c_int]),
     ("libsortTimingEnable", None, [ctypes.c_bool]),
     ("libsortTimingReset", None, []),
     ("libsortTimingQuery", ctypes.c_int,
      [ctypes.c_char_p, _u64p, ctypes.POINTER(ctypes.c_double), _u64p]),
     ("libsortReleaseWorkspace", ctypes.c_int, []),
     ("libsortLastError", ctypes.c_char_p, []),
+    ("libsortDeviceErrors", ctypes.c_uint32, []),
 ]
 
 EXPORTED_SYMBOLS = [s[0] for s in _SIGS]

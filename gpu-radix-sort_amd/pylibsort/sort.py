@@ -12,7 +12,7 @@ from . import _state, require_gpu
 __all__ = [
     "sortException", "sortResultException", "groupBits", "bytesToInts", "checkOrder",
     "checkSortFull", "checkPartial", "sortFull", "sortPartial", "generateInputs",
-    "boundariesToCaps", "setDigitBits", "getDigitBits",
+    "boundariesToCaps", "setDigitBits", "getDigitBits", "setAlgorithm",
 ]
 
 
@@ -148,3 +148,14 @@ def setDigitBits(bits):
 
 def getDigitBits():
     return _state.sortLib.libsortGetDigitBits()
+
+
+_ALGOS = {"auto": 0, "onesweep": 1, "rts": 2, "tiles": 3}
+
+
+def setAlgorithm(name):
+    """Select the pass algorithm ("auto", "onesweep", "rts" or "tiles"); returns the previous name."""
+    prev = _state.sortLib.libsortSetAlgorithm(_ALGOS[name])
+    if prev < 0:
+        raise ValueError(name)
+    return {v: k for k, v in _ALGOS.items()}[prev]

@@ -127,8 +127,18 @@ LIBSORT_API bool libsortPopulateDevice(uint32_t* d_out, size_t n, uint64_t first
 LIBSORT_API int libsortSetDigitBits(int bits);
 LIBSORT_API int libsortGetDigitBits(void);
 
-/* Per-kernel timing with hipEvents on the launch stream.  Names: "upsweep",
- * "scan", "downsweep", "bounds", "populate", "segcopy". */
+/* Pass algorithm: 0 = auto (default: tile offsets for 4-bit digits, onesweep
+ * for 8-bit digits, reduce-then-scan for n >= 2^30), 1 = onesweep (one kernel
+ * per digit, decoupled look-back), 2 = reduce-then-scan (upsweep + scan +
+ * downsweep), 3 = tile offsets (per-tile counts + column scan + pass kernel
+ * without look-back; 4-bit digits).  Initial value from LIBSORT_ALGO
+ * ("auto" / "onesweep" / "rts" / "tiles").  Returns the previous value, or -1
+ * if `algo` is invalid. */
+LIBSORT_API int libsortSetAlgorithm(int algo);
+
+/* Per-kernel timing with hipEvents on the launch stream.  Names: "whist",
+ * "onesweep", "upsweep", "scan", "downsweep", "bounds", "histogram",
+ * "populate", "segcopy". */
 LIBSORT_API void libsortTimingEnable(bool on);
 LIBSORT_API void libsortTimingReset(void);
 LIBSORT_API bool libsortTimingQuery(const char* kernel, uint64_t* launches, double* total_ms,
@@ -139,5 +149,9 @@ LIBSORT_API bool libsortReleaseWorkspace(void);
 
 /* Last error message of the calling thread ("" if none). */
 LIBSORT_API const char* libsortLastError(void);
+
+/* Synchronises the current device; returns and clears its device-side error
+ * word (bit 0: a look-back wait hit its spin bound).  0 = healthy. */
+LIBSORT_API uint32_t libsortDeviceErrors(void);
 
 #endif /* LIBSORT_MI355X_LIBSORT_H */

@@ -27,12 +27,18 @@ def dev():
     return D
 
 
-@pytest.fixture(params=[8, 4], ids=["digit8", "digit4"])
+@pytest.fixture(params=[(8, "onesweep"), (4, "onesweep"), (8, "rts"), (4, "rts"), (4, "tiles")],
+                ids=["digit8-onesweep", "digit4-onesweep", "digit8-rts", "digit4-rts", "digit4-tiles"])
 def digit_bits(request, dev):
+    """Every parity case runs under both digit widths and both pass algorithms."""
     import pylibsort
-    prev = pylibsort.setDigitBits(request.param)
-    yield request.param
+    bits, algo = request.param
+    prev = pylibsort.setDigitBits(bits)
+    prev_algo = pylibsort.setAlgorithm(algo)
+    yield bits
+    assert pylibsort.lib().libsortDeviceErrors() == 0, "look-back spin bound hit"
     pylibsort.setDigitBits(prev)
+    pylibsort.setAlgorithm(prev_algo)
 
 
 def _u32(t):
