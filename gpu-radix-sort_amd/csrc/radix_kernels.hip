@@ -766,6 +766,38 @@ __global__ __launch_bounds__(256) void k_colscan_l2(uint32_t* __restrict__ B, ui
   }
 }
 
+// Level 2 for wide digits (RADIX = 256): block d scans column d of
+// B[nchunks][RADIX] in place (exclusive) and writes the column total to tot[d].
+template <int RADIX>
+__global__ __launch_bounds__(256) void k_colscan_l2col(uint32_t* __restrict__ B, uint32_t nchunks,
+                                                       uint32_t* __restrict__ tot) {
+  __shared__ uint32_t s_wsum[4];
+  const uint32_t d = blockIdx.x;
+  const uint32_t per = (nchunks + 255) / 256;
+  const uint32_t a = threadIdx.x * per, b = min(nchunks, a + per);
+  uint32_t sum = 0;
+  for (uint32_t r = a; r < b; ++r) sum += B[(size_t)r * RADIX + d];
+  uint32_t total;
+  uint32_t run = block_exclusive_scan<256>(sum, s_wsum, total);
+  for (uint32_t r = a; r < b; ++r) {
+    const uint32_t v = B[(size_t)r * RADIX + d];
+    B[(size_t)r * RADIX + d] = run;
+    run += v;
+  }
+  if (threadIdx.x == 0) tot[d] = total;
+}
+
+// Level 3 for wide digits: every block recomputes the digit starts (exclusive
+// scan of tot) and adds them to its rows of B.
+template <int RADIX>
+__global__ __launch_bounds__(RADIX) void k_colscan_l3(uint32_t* __restrict__ B, uint32_t nchunks,
+                                                      const uint32_t* __restrict__ tot) {
+  __shared__ uint32_t s_wsum[(RADIX + 63) / 64];
+  uint32_t total;
+  const uint32_t ds = block_exclusive_scan<RADIX>(tot[threadIdx.x], s_wsum, total);
+  for (uint32_t r = blockIdx.x; r < nchunks; r += gridDim.x) B[(size_t)r * RADIX + threadIdx.x] += ds;
+}
+
 // The pass kernel of the tile-offset path: the onesweep tile body with the
 // run offsets read from the scanned counts.  FUSE: also count the next digit
 // (op_next) of every written key per destination tile into C_next (4-bit
@@ -1226,59 +1258,99 @@ bool use_onesweep(size_t n) {
 int choose_algorithm(size_t n, int bits) {
   const int a = get_algorithm();
   if (n >= (1ull << 30)) return 2;  // 30-bit look-back values; 32-bit tile offsets
-  if (a == 3) return bits == 4 ? 3 : 1;
-  if (a == 1 || a == 2) return a;
-  return bits == 4 ? 3 : 1;  // auto
+  if (a == 1 || a == 2 || a == 3) return a;
+  return 3;  // auto: tile offsets
 }
 
-constexpr int kTpBlock = 256;
-constexpr int kTpItems = 16;  // 4096-key tiles (u32 keys)
-
+// Tile-offset path geometry.  4-bit digits: 256-thread tiles of 4096 keys and
+// the next pass's counts fused into the pass kernel.  8-bit digits: 512-thread
+// tiles of 8192 keys (longer digit runs, fewer count rows) and a separate
+// per-tile count kernel per pass.
 template <typename K>
-constexpr int tp_items() { return sizeof(K) == 8 ? 8 : kTpItems; }
-
-// Per-tile counts of pass 0 (4-bit digit at lo) into tc[0]; zero tc[1].
+constexpr int tp_items() { return sizeof(K) == 8 ? 8 : 16; }
+constexpr int tp_block(int bits) { return bits == 4 ? 256 : 512; }
 template <typename K>
-hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, uint32_t tiles,
-                          hipStream_t st) {
-  constexpr int TILE = kTpBlock * tp_items<K>();
-  (void)TILE;
-  const uint32_t chunks = (tiles + kColRowsPerLane * 16 - 1) / (kColRowsPerLane * 16);
-  LS_TRY(ws.ensure_tiles((size_t)tiles * 16, (size_t)chunks * 16));
-  const int nb = std::min(4, hi - lo);
-  RadixDigit op0{(uint32_t)lo, (1u << nb) - 1u};
+uint32_t tp_tiles(size_t n, int bits) {
+  const uint64_t t = (uint64_t)tp_block(bits) * tp_items<K>();
+  return (uint32_t)((n + t - 1) / t);
+}
+inline uint32_t tp_chunks(uint32_t tiles, int bits) {
+  const uint32_t ch = kColRowsPerLane * (256u >> bits);
+  return (tiles + ch - 1) / ch;
+}
+
+template <int BITS, typename K>
+hipError_t tiles_counts(Workspace& ws, const K* in, size_t n, RadixDigit op, uint32_t tiles, uint32_t* C,
+                        uint32_t* zero, uint32_t zero_words, hipStream_t st) {
+  constexpr int B = tp_block(BITS);
   ScopedTimer tm("tilecounts", st, n);
-  hipLaunchKernelGGL((k_tile_counts<4, kTpBlock, tp_items<K>(), K>), dim3(tiles), dim3(kTpBlock), 0, st, in,
-                     (uint32_t)n, op0, ws.tc[0], ws.tc[1], tiles * 16u);
+  hipLaunchKernelGGL((k_tile_counts<BITS, B, tp_items<K>(), K>), dim3(tiles), dim3(B), 0, st, in, (uint32_t)n, op,
+                     C, zero, zero_words);
   return hipGetLastError();
 }
 
-template <typename K, typename V>
-hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout, size_t n, int p, int P,
-                      int lo, int hi, uint32_t tiles, hipStream_t st) {
-  const uint32_t chunks = (tiles + kColRowsPerLane * 16 - 1) / (kColRowsPerLane * 16);
-  uint32_t* cur = ws.tc[p & 1];
-  uint32_t* nxt = ws.tc[(p + 1) & 1];
-  {
-    ScopedTimer tm("colscan", st, tiles);
-    hipLaunchKernelGGL(k_colscan_l1<16>, dim3(chunks), dim3(256), 0, st, cur, tiles, ws.tb);
+template <int BITS>
+hipError_t tiles_colscan(Workspace& ws, uint32_t* C, uint32_t tiles, hipStream_t st) {
+  constexpr int RADIX = 1 << BITS;
+  const uint32_t chunks = tp_chunks(tiles, BITS);
+  ScopedTimer tm("colscan", st, tiles);
+  hipLaunchKernelGGL(k_colscan_l1<RADIX>, dim3(chunks), dim3(256), 0, st, C, tiles, ws.tb);
+  LS_TRY(hipGetLastError());
+  if constexpr (RADIX <= 16) {
+    hipLaunchKernelGGL(k_colscan_l2<RADIX>, dim3(1), dim3(256), 0, st, ws.tb, chunks);
+  } else {
+    uint32_t* tot = ws.tb + (size_t)chunks * RADIX;
+    hipLaunchKernelGGL(k_colscan_l2col<RADIX>, dim3(RADIX), dim3(256), 0, st, ws.tb, chunks, tot);
     LS_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_colscan_l2<16>, dim3(1), dim3(256), 0, st, ws.tb, chunks);
-    LS_TRY(hipGetLastError());
+    hipLaunchKernelGGL(k_colscan_l3<RADIX>, dim3(std::min(chunks, 1024u)), dim3(RADIX), 0, st, ws.tb, chunks,
+                       (const uint32_t*)tot);
   }
-  const int shift = lo + 4 * p;
-  const int nb = std::min(4, hi - shift);
-  RadixDigit op{(uint32_t)shift, (1u << nb) - 1u};
-  const bool fuse = p + 1 < P;
-  const int nb2 = fuse ? std::min(4, hi - shift - 4) : 1;
-  RadixDigit op_next{(uint32_t)(fuse ? shift + 4 : 0), (1u << nb2) - 1u};
+  return hipGetLastError();
+}
+
+// Sort prologue of the tile path: buffers, and (4-bit) the pass-0 counts.
+template <typename K>
+hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, int bits, hipStream_t st) {
+  const uint32_t tiles = tp_tiles<K>(n, bits);
+  const uint32_t radix = 1u << bits;
+  LS_TRY(ws.ensure_tiles((size_t)tiles * radix, ((size_t)tp_chunks(tiles, bits) + 1) * radix));
+  if (bits != 4) return hipSuccess;
+  const int nb = std::min(4, hi - lo);
+  return tiles_counts<4, K>(ws, in, n, RadixDigit{(uint32_t)lo, (1u << nb) - 1u}, tiles, ws.tc[0], ws.tc[1],
+                            tiles * 16u, st);
+}
+
+template <int BITS, typename K, typename V>
+hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout, size_t n, int p, int P,
+                      int lo, int hi, hipStream_t st) {
+  constexpr int B = tp_block(BITS);
+  const uint32_t tiles = tp_tiles<K>(n, BITS);
+  const int shift = lo + BITS * p;
+  const int nb = std::min(BITS, hi - shift);
+  const RadixDigit op{(uint32_t)shift, (1u << nb) - 1u};
+  // 4-bit (fused): counts of this pass were produced by the previous pass (or
+  // the prologue) in tc[p & 1]; otherwise count this pass's input now.
+  // LIBSORT_TP_FUSE=0 turns the fusion off (A/B measurement).
+  static const bool fuse_on = [] {
+    const char* s = getenv("LIBSORT_TP_FUSE");
+    return !(s && s[0] == '0');
+  }();
+  const bool fused_counts = BITS == 4 && fuse_on;
+  uint32_t* cur = fused_counts ? ws.tc[p & 1] : ws.tc[0];
+  uint32_t* nxt = ws.tc[(p + 1) & 1];
+  if (!fused_counts && !(BITS == 4 && p == 0))
+    LS_TRY((tiles_counts<BITS, K>(ws, kin, n, op, tiles, cur, nullptr, 0, st)));
+  LS_TRY(tiles_colscan<BITS>(ws, cur, tiles, st));
+  const bool fuse = fused_counts && p + 1 < P;
+  const int nb2 = fuse ? std::min(BITS, hi - shift - BITS) : 1;
+  const RadixDigit op_next{(uint32_t)(fuse ? shift + BITS : 0), (1u << nb2) - 1u};
   ScopedTimer tm("tilepass", st, n);
   if (fuse)
-    hipLaunchKernelGGL((k_tile_pass<4, kTpBlock, tp_items<K>(), K, V, true>), dim3(tiles), dim3(kTpBlock), 0,
-                       st, kin, kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, BITS == 4>), dim3(tiles), dim3(B), 0, st, kin,
+                       kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
   else
-    hipLaunchKernelGGL((k_tile_pass<4, kTpBlock, tp_items<K>(), K, V, false>), dim3(tiles), dim3(kTpBlock), 0,
-                       st, kin, kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, false>), dim3(tiles), dim3(B), 0, st, kin, kout,
+                       vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
   return hipGetLastError();
 }
 
@@ -1386,17 +1458,18 @@ hipError_t sort_impl(Workspace& ws, const K* in, K* out, K* tmp, const V* vin, V
   ws.last_algo = algo;
   const int OS_TILE = os_block() * os_items<K>();
   const uint32_t tiles = (uint32_t)((n + OS_TILE - 1) / OS_TILE);
-  constexpr int TP_TILE = kTpBlock * tp_items<K>();
-  const uint32_t tp_tiles = (uint32_t)((n + TP_TILE - 1) / TP_TILE);
   if (os) LS_TRY(onesweep_prologue<K>(ws, in, n, lo, hi, bits, P, tiles, st));
-  if (tp) LS_TRY(tiles_prologue<K>(ws, in, n, lo, hi, tp_tiles, st));
+  if (tp) LS_TRY(tiles_prologue<K>(ws, in, n, lo, hi, bits, st));
   for (int p = 0; p < P; ++p) {
     const int shift = lo + p * bits;
     const int nb = std::min(bits, hi - shift);
     K* kdst = dst_is_out(p) ? out : tmp;
     V* vdst = dst_is_out(p) ? vout : vtmp;
     if (tp) {
-      LS_TRY((tiles_pass<K, V>(ws, ksrc, kdst, vsrc, vdst, n, p, P, lo, hi, tp_tiles, st)));
+      if (bits == 4)
+        LS_TRY((tiles_pass<4, K, V>(ws, ksrc, kdst, vsrc, vdst, n, p, P, lo, hi, st)));
+      else
+        LS_TRY((tiles_pass<8, K, V>(ws, ksrc, kdst, vsrc, vdst, n, p, P, lo, hi, st)));
     } else if (os) {
       if (bits == 8)
         LS_TRY((onesweep_pass<8, K, V>(ws, ksrc, kdst, vsrc, vdst, n, p, P, (uint32_t)shift, (uint32_t)nb, tiles, st)));
@@ -1424,7 +1497,7 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
     ScopedTimer tm("bounds", st, n);
     if (n == 0) {
       LS_TRY(hipMemsetAsync(d_bounds, 0, (size_t)ngroups * sizeof(uint32_t), st));
-    } else if (ws.last_algo == 3 && width <= 4) {
+    } else if (ws.last_algo == 3 && num_passes(width, digit_bits) == 1) {
       // tile path, single pass: chunk 0's scanned totals are the digit starts
       LS_TRY(hipMemcpyAsync(d_bounds, ws.tb, (size_t)ngroups * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
     } else if (ws.last_algo == 3) {

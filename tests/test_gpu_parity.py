@@ -27,8 +27,9 @@ def dev():
     return D
 
 
-@pytest.fixture(params=[(8, "onesweep"), (4, "onesweep"), (8, "rts"), (4, "rts"), (4, "tiles")],
-                ids=["digit8-onesweep", "digit4-onesweep", "digit8-rts", "digit4-rts", "digit4-tiles"])
+@pytest.fixture(params=[(8, "onesweep"), (4, "onesweep"), (8, "rts"), (4, "rts"), (4, "tiles"), (8, "tiles")],
+                ids=["digit8-onesweep", "digit4-onesweep", "digit8-rts", "digit4-rts", "digit4-tiles",
+                     "digit8-tiles"])
 def digit_bits(request, dev):
     """Every parity case runs under both digit widths and both pass algorithms."""
     import pylibsort

@@ -40,6 +40,7 @@ def main():
         pylibsort.setDigitBits(int(bits))
         pylibsort.setAlgorithm(algo)
         os.environ["LIBSORT_OS_BLOCK"] = blk
+        os.environ["LIBSORT_TP_BLOCK"] = blk
         os.environ["LIBSORT_DIAG_ABLATION"] = f[3] if len(f) > 3 else "0"
         return len(f) > 3 and f[3] != "0"
 

@@ -13,7 +13,7 @@ rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 run() {
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$name" -o run --output-format csv \
-    --kernel-include-regex "onesweep|downsweep|upsweep|window_hist|copy_kernel" \
+    --kernel-include-regex "onesweep|downsweep|upsweep|window_hist|copy_kernel|tile_pass|tile_counts|colscan" \
     -- python3 tools/ab_sort.py --keys-log2 "$K" --rounds 1 --reps 2 "$CFG" > "$OUT/$name.log" 2>&1
 }
 run p_fetch FETCH_SIZE
