@@ -1259,7 +1259,10 @@ int choose_algorithm(size_t n, int bits) {
   const int a = get_algorithm();
   if (n >= (1ull << 30)) return 2;  // 30-bit look-back values; 32-bit tile offsets
   if (a == 1 || a == 2 || a == 3) return a;
-  return 3;  // auto: tile offsets
+  // auto (measured on MI355X, 2^28 keys): 4-bit digits -> tile offsets with
+  // fused counts (~490 us/pass); 8-bit digits -> onesweep (~945 us/pass; the
+  // tile path needs a separate count read there, ~1080 us/pass)
+  return bits == 4 ? 3 : 1;
 }
 
 // Tile-offset path geometry.  4-bit digits: 256-thread tiles of 4096 keys and

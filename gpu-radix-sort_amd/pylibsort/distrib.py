@@ -75,19 +75,34 @@ class HipOps:
         return self.D.segment_copy_u32(src, dst, so, do, ln)
 
 
+def _host_staged(group):
+    """gloo cannot move HIP tensors: stage through host memory.  This is only
+    for rehearsing several ranks on one GPU; RCCL ("nccl") moves device
+    memory directly over xGMI."""
+    return dist.get_backend(group) == "gloo"
+
+
 def _allgather_np(vec, ref_tensor, group):
     """All-gather a small int64 numpy vector; returns [R, len] int64 numpy."""
     R = dist.get_world_size(group)
-    t = torch.as_tensor(np.ascontiguousarray(vec, dtype=np.int64), device=ref_tensor.device)
+    dev = "cpu" if _host_staged(group) else ref_tensor.device
+    t = torch.as_tensor(np.ascontiguousarray(vec, dtype=np.int64), device=dev)
     outs = [torch.empty_like(t) for _ in range(R)]
     dist.all_gather(outs, t, group=group)
     return np.stack([o.cpu().numpy() for o in outs])
 
 
 def _alltoallv(send, send_counts, recv_counts, ops, group):
+    """all_to_all_single with uneven splits (alltoallv): contiguous slices."""
     recv = ops.empty(int(np.sum(recv_counts)))
-    dist.all_to_all_single(recv, send, [int(c) for c in recv_counts], [int(c) for c in send_counts],
-                           group=group)
+    rs = [int(c) for c in recv_counts]
+    ss = [int(c) for c in send_counts]
+    if _host_staged(group) and send.is_cuda:
+        r_host = torch.empty(recv.numel(), dtype=recv.dtype)
+        dist.all_to_all_single(r_host, send.cpu(), rs, ss, group=group)
+        recv.copy_(r_host)
+    else:
+        dist.all_to_all_single(recv, send, rs, ss, group=group)
     return recv
 
 

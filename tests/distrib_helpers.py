@@ -1,0 +1,91 @@
+"""Helpers for the multi-rank tests: an oracle-backed ops backend (test
+infrastructure, CPU) with the same interface as pylibsort.distrib.HipOps, and
+the per-rank worker run under torch.multiprocessing with gloo."""
+import os
+import pathlib
+import sys
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+for p in (str(ROOT), str(ROOT / "gpu-radix-sort_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+class OracleOps:
+    """CPU restatement of the local operations (checker, never the product)."""
+
+    def __init__(self):
+        import torch
+        self.torch = torch
+        from oracle import oracle
+        self.o = oracle
+
+    def _np(self, t):
+        return t.numpy().view(np.uint32)
+
+    def _t(self, a):
+        return self.torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32).copy())
+
+    def empty(self, n):
+        return self.torch.empty(n, dtype=self.torch.int32)
+
+    def sort(self, keys, out=None):
+        return self._t(self.o.sort_u32(self._np(keys)))
+
+    def partial_sort(self, keys, offset, width, out=None):
+        d, b = self.o.partial_u32(self._np(keys), offset, width)
+        return self._t(d), np.diff(b.astype(np.int64), append=keys.numel())
+
+    def histogram(self, keys, shift, bits):
+        x = self._np(keys)
+        h = np.bincount((x >> np.uint32(shift)) & np.uint32((1 << bits) - 1), minlength=1 << bits)
+        return self.torch.from_numpy(h.astype(np.int32))
+
+    def partition(self, keys, splitters, out=None):
+        x = self._np(keys)
+        b = np.searchsorted(np.asarray(splitters, dtype=np.uint64), x.astype(np.uint64), side="right")
+        return self._t(x[np.argsort(b, kind="stable")])
+
+    def segment_copy(self, src, dst, so, do, ln):
+        s = src.numpy()
+        d = dst.numpy()
+        for a, b, c in zip(so, do, ln):
+            d[int(b):int(b + c)] = s[int(a):int(a + c)]
+        return dst
+
+
+def shard_inputs(x, R):
+    """The reference's ceil(N/R) cut of one array into R shards."""
+    N = x.size
+    S = -(-N // R)
+    return [x[min(N, r * S):min(N, (r + 1) * S)] for r in range(R)]
+
+
+def rank_worker(rank, world, port, x, schedule, outdir, use_gpu):
+    """Runs distrib_sort on this rank's shard and saves the result."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    from pylibsort import distrib
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    shard = shard_inputs(x, world)[rank]
+    if use_gpu:
+        torch.cuda.set_device(0)
+        ops = distrib.HipOps()
+        keys = torch.from_numpy(shard.view(np.int32).copy()).cuda()
+    else:
+        ops = OracleOps()
+        keys = torch.from_numpy(shard.view(np.int32).copy())
+    res = distrib.distrib_sort(keys, ops=ops, schedule=schedule)
+    np.save(os.path.join(outdir, "rank%d.npy" % rank), res.cpu().numpy().view(np.uint32))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_ranks(x, world, schedule, tmpdir, use_gpu=False, port=29611):
+    import torch.multiprocessing as mp
+    mp.spawn(rank_worker, args=(world, port, x, schedule, str(tmpdir), use_gpu), nprocs=world, join=True)
+    return [np.load(os.path.join(str(tmpdir), "rank%d.npy" % r)) for r in range(world)]

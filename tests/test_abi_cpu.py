@@ -1,0 +1,135 @@
+"""The drop-in boundary without a GPU: libsort.so loads, exports every symbol
+include/libsort.h declares, the header compiles as C (cgo, gnu99) and C++,
+host-only entry points behave like the reference, and the GPU entry points
+fail loudly (no silent CPU fallback)."""
+import ctypes
+import pathlib
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "libsort.h"
+LIB = ROOT / "gpu-radix-sort_amd" / "libsort.so"
+
+REFERENCE_ABI = ["initLibSort", "gpuPartial", "providedGpu", "providedCpu", "populateInput",
+                 "gpuPartialProfile", "providedGpuProfile"]
+
+
+def declared_symbols():
+    txt = HEADER.read_text()
+    return sorted(set(re.findall(r"LIBSORT_API\s+[\w\s\*]+?\b(\w+)\s*\(", txt)))
+
+
+def test_header_declares_reference_abi():
+    names = declared_symbols()
+    for n in REFERENCE_ABI:
+        assert n in names
+
+
+def test_library_exports_every_declared_symbol():
+    assert LIB.exists(), "build first (python __graft_entry__.py build)"
+    out = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    missing = [n for n in declared_symbols() if n not in exported]
+    assert not missing, missing
+    import pylibsort
+    assert sorted(pylibsort.EXPORTED_SYMBOLS) == sorted(declared_symbols())
+
+
+@pytest.mark.parametrize("lang,flags", [("c", ["-std=gnu99"]), ("c++", ["-std=c++14"])])
+def test_header_compiles(tmp_path, lang, flags):
+    src = tmp_path / ("t.c" if lang == "c" else "t.cpp")
+    src.write_text('#include "libsort.h"\nint main(void){ bool (*f)(uint32_t*, uint32_t*, size_t, '
+                   'uint32_t, uint32_t) = gpuPartial; return f == 0; }\n')
+    cc = "gcc" if lang == "c" else "g++"
+    subprocess.run([cc, *flags, "-Wall", "-Werror", "-fsyntax-only", "-I", str(ROOT / "include"), str(src)],
+                   check=True)
+
+
+def test_header_matches_reference_header_types():
+    # same C types as the reference libsort/libsort.h:14-32 (unsigned int* for
+    # providedGpu/providedCpu, uint32_t* for the others)
+    txt = HEADER.read_text()
+    assert re.search(r"bool providedGpu\(unsigned int\* h_in, size_t len\)", txt)
+    assert re.search(r"bool providedCpu\(unsigned int\* in, size_t len\)", txt)
+    assert re.search(r"bool gpuPartial\(uint32_t\* h_in, uint32_t\* boundaries, size_t h_in_len,\s*"
+                     r"uint32_t offset, uint32_t width\)", txt)
+    assert re.search(r"void populateInput\(uint32_t\* arr, size_t nelem\)", txt)
+
+
+def test_populate_input_matches_reference_in_fresh_process(golden):
+    g, _ = golden
+    code = ("import sys; sys.path[:0]=[%r]; import pylibsort, numpy as np; "
+            "a=np.frombuffer(pylibsort.generateInputs(8),dtype=np.uint32); "
+            "b=np.frombuffer(pylibsort.generateInputs(4),dtype=np.uint32); "
+            "print(' '.join(format(int(v),'08x') for v in np.concatenate([a,b])))"
+            % str(ROOT / "gpu-radix-sort_amd"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True).stdout
+    words = out.split()
+    assert words[:8] == g["fresh_process_first_words"]
+    assert words[8:] == g["next_call_words_after_8"]
+
+
+def test_provided_cpu_is_std_sort(oracle_mod):
+    import pylibsort
+    x = oracle_mod.pcg(4099)
+    y = x.copy()
+    assert pylibsort.lib().providedCpu(y.ctypes.data, y.size) == 1
+    np.testing.assert_array_equal(y, np.sort(x))
+
+
+def test_gpu_entry_points_fail_loudly_without_device(capfd):
+    import pylibsort
+    if pylibsort.gpu_ready():
+        pytest.skip("a GPU is present")
+    L = pylibsort.lib()
+    x = np.arange(100, dtype=np.uint32)[::-1].copy()
+    assert L.providedGpu(x.ctypes.data, x.size) == 0
+    b = (ctypes.c_uint32 * 256)()
+    assert L.gpuPartial(x.ctypes.data, ctypes.addressof(b), x.size, 0, 8) == 0
+    assert "initLibSort" in pylibsort.last_error()
+    with pytest.raises(RuntimeError):
+        pylibsort.sortFull(bytearray(x.tobytes()))
+    np.testing.assert_array_equal(x, np.arange(100, dtype=np.uint32)[::-1])  # untouched
+
+
+def test_ctypes_default_int_restype_sees_false():
+    # reference callers (faasTest/pylibsort/sort.py:101) never set restype:
+    # the bool return must be readable as a full int
+    L = ctypes.CDLL(str(LIB))
+    x = np.arange(4, dtype=np.uint32)
+    r = L.providedGpu(ctypes.c_void_p(x.ctypes.data), ctypes.c_size_t(4))
+    assert r in (0, 1)
+
+
+def test_tunables_validate():
+    import pylibsort
+    prev = pylibsort.setDigitBits(4)
+    assert pylibsort.getDigitBits() == 4
+    pylibsort.setDigitBits(prev)
+    with pytest.raises(ValueError):
+        pylibsort.setDigitBits(5)
+    assert pylibsort.lib().libsortSetAlgorithm(9) == -1
+    prev = pylibsort.setAlgorithm("tiles")
+    assert pylibsort.setAlgorithm(prev) == "tiles"
+
+
+def test_host_checkers():
+    import pylibsort
+    x = np.array([5, 1, 4, 4, 2, 0x100], dtype=np.uint32)
+    d = np.array(sorted(x, key=lambda v: v & 3), dtype=np.uint32)
+    b = [0, 2, 3, 3]  # groups: {4,4,0x100}->0 ... computed below
+    cnt = np.bincount(x & 3, minlength=4)
+    b = np.concatenate([[0], np.cumsum(cnt)[:-1]]).tolist()
+    pylibsort.checkPartial(x.tobytes(), d.tobytes(), b, 0, 2)
+    with pytest.raises(pylibsort.sortException):
+        pylibsort.checkPartial(x.tobytes(), x.tobytes(), b, 0, 2)
+    assert pylibsort.boundariesToCaps([0, 2, 5], 40).tolist() == [8, 12, 20]
+    pylibsort.checkOrder(np.sort(x))
+    with pytest.raises(pylibsort.sortResultException):
+        pylibsort.checkOrder(x)
