@@ -109,9 +109,8 @@ hipError_t sort_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t
                               uint64_t* kout, uint32_t* vout, uint64_t* ktmp, uint32_t* vtmp,
                               size_t n, int lo, int hi, int digit_bits, hipStream_t stream);
 
-// Pass algorithm: 0 = auto (tile offsets for 4-bit digits, onesweep for 8-bit,
-// reduce-then-scan when n >= 2^30), 1 = onesweep, 2 = reduce-then-scan,
-// 3 = tile offsets.  Initialised from LIBSORT_ALGO ("auto" / "onesweep" /
+// Pass algorithm: 0 = auto (tile offsets), 1 = onesweep (n < 2^30, else tile
+// offsets), 2 = reduce-then-scan, 3 = tile offsets.  Initialised from LIBSORT_ALGO ("auto" / "onesweep" /
 // "rts" / "tiles").
 int get_algorithm();
 int set_algorithm(int algo);  // returns the previous value, -1 if invalid

@@ -36,10 +36,15 @@ constexpr int kWave = 64;
 // ----------------------------------------------------------------------------
 // digit extractors
 // ----------------------------------------------------------------------------
+// Digit = bits [shift, shift + popcount(mask)) of the key; mask = 2^w - 1 with
+// w <= 8 (one digit of a pass).
 struct RadixDigit {
   uint32_t shift;
   uint32_t mask;
-  __device__ __forceinline__ uint32_t operator()(uint32_t k) const { return (k >> shift) & mask; }
+  // one v_bfe_u32 (the width is wave-uniform: s_bcnt1 of the mask, hoisted)
+  __device__ __forceinline__ uint32_t operator()(uint32_t k) const {
+    return __builtin_amdgcn_ubfe(k, shift, (uint32_t)__builtin_popcount(mask));
+  }
   __device__ __forceinline__ uint32_t operator()(uint64_t k) const {
     return (uint32_t)(k >> shift) & mask;
   }
@@ -70,49 +75,66 @@ __device__ __forceinline__ uint64_t vec_elem(const ulonglong2& v, int c) { retur
 
 __device__ __forceinline__ uint64_t umin64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
 
-// Lanes of the wave whose digit equals this lane's (wave64 "match any" from
-// BITS ballots).  Written as an OR of per-bit mismatches so that each bit costs
-// a sign-extended bit extract, one v_cmp for the ballot and one v_bitop3 per
-// 32-bit half, instead of the select/xor/and chain of `x ? m : ~m`.
-template <int BITS>
-__device__ __forceinline__ uint64_t match_peers(uint32_t d, bool ok) {
-  uint32_t mis_lo = 0u, mis_hi = 0u;
-#pragma unroll
-  for (int bit = 0; bit < BITS; ++bit) {
-    const uint32_t X = (uint32_t)((int32_t)(d << (31 - bit)) >> 31);  // 0 or ~0
-    const uint64_t m = __ballot(X != 0u);
-    mis_lo |= (uint32_t)m ^ X;
-    mis_hi |= (uint32_t)(m >> 32) ^ X;
-  }
-  const uint64_t valid = __ballot(ok);
-  return valid & ~(((uint64_t)mis_hi << 32) | mis_lo);
+// Ballot of x != 0 as one v_cmp (left to itself the compiler re-derives the
+// predicate from the digit with a shift and a signed compare).
+__device__ __forceinline__ uint64_t ballot_nz(uint32_t x) {
+  uint64_t m;
+  asm("v_cmp_ne_u32_e64 %0, 0, %1" : "=s"(m) : "v"(x));
+  return m;
 }
 
 // Stable rank of each item among this wave's items of the same digit, items
-// in order j = 0..ITEMS-1 and lanes in order within an item.  `row` is the
-// wave's zeroed per-digit counter row in LDS; the last lane of each peer group
-// advances it.  (A leader-only ds_add_rtn + ds_bpermute variant, which lets the
-// items' LDS round trips overlap, cost 20-30 VGPRs and one wave/SIMD of
-// occupancy and was slower on MI355X.)
+// in order j = 0..ITEMS-1 and lanes in order within an item.  The peers of a
+// lane (the lanes with the same digit) come from BITS ballots: per bit a
+// sign-extended extract X (0 or ~0), one v_cmp for the ballot m, and one
+// v_bitop3 per 32-bit half accumulating the mismatches (m ^ X) | mis; the last
+// bit's bitop3 yields ~mismatch = peers directly.  `row` is the wave's zeroed
+// per-digit counter row in LDS; every peer writes the same new count (no
+// branch).  FULL: every lane holds a valid key (no predicate).  (A leader-only
+// ds_add_rtn + ds_bpermute variant, which lets the items' LDS round trips
+// overlap, cost 20-30 VGPRs and one wave/SIMD of occupancy and was slower.)
+template <int BITS, bool FULL, int ITEMS, typename K, typename Op>
+__device__ __forceinline__ void rank_items_t(const K (&k)[ITEMS], uint32_t (&rk)[ITEMS], uint32_t* row,
+                                             uint32_t valid, uint32_t wbase, uint32_t lane, Op op) {
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t d = op(k[j]);
+    uint32_t lo = 0u, hi = 0u;
+#pragma unroll
+    for (int bit = 0; bit < BITS - 1; ++bit) {
+      const uint32_t X = (uint32_t)__builtin_amdgcn_sbfe(d, bit, 1);
+      const uint64_t m = ballot_nz(X);
+      lo = __builtin_amdgcn_bitop3_b32(X, lo, (uint32_t)m, 0xDE);          // (X ^ m) | lo
+      hi = __builtin_amdgcn_bitop3_b32(X, hi, (uint32_t)(m >> 32), 0xDE);
+    }
+    const uint32_t X = (uint32_t)__builtin_amdgcn_sbfe(d, BITS - 1, 1);
+    const uint64_t m = ballot_nz(X);
+    uint32_t plo = __builtin_amdgcn_bitop3_b32(X, lo, (uint32_t)m, 0x21);  // ~((X ^ m) | lo)
+    uint32_t phi = __builtin_amdgcn_bitop3_b32(X, hi, (uint32_t)(m >> 32), 0x21);
+    bool ok = true;
+    if constexpr (!FULL) {
+      ok = wbase + j * kWave + lane < valid;
+      const uint64_t vm = __ballot(ok);
+      plo &= (uint32_t)vm;
+      phi &= (uint32_t)(vm >> 32);
+    }
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi(phi, __builtin_amdgcn_mbcnt_lo(plo, 0u));
+    const uint32_t cnt = (uint32_t)(__builtin_popcount(plo) + __builtin_popcount(phi));
+    const uint32_t base = row[d];
+    rk[j] = base + below;
+    if (FULL || ok) row[d] = base + cnt;  // all peers write the same value
+  }
+}
+
 template <int BITS, int ITEMS, typename K, typename Op>
 __device__ __forceinline__ void rank_items(const K (&k)[ITEMS], uint32_t (&rk)[ITEMS], uint32_t* row,
                                            bool full, uint32_t valid, uint32_t wbase, uint32_t lane,
                                            Op op) {
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {
-    const uint32_t d = op(k[j]);
-    const bool ok = full || (wbase + j * kWave + lane < valid);
-    const uint64_t peers = match_peers<BITS>(d, ok);
-    const uint32_t below = mbcnt64(peers);
-    const uint32_t cnt = (uint32_t)__popcll(peers);
-    const uint32_t base = row[d];
-    rk[j] = base + below;
-    if (ok && below + 1u == cnt) row[d] = base + cnt;  // last peer advances the counter
-  }
+  if (full)
+    rank_items_t<BITS, true, ITEMS>(k, rk, row, valid, wbase, lane, op);
+  else
+    rank_items_t<BITS, false, ITEMS>(k, rk, row, valid, wbase, lane, op);
 }
 
 // Writes the locally sorted tile s_keys[0..valid) (and values) to global
@@ -798,12 +820,27 @@ __global__ __launch_bounds__(RADIX) void k_colscan_l3(uint32_t* __restrict__ B, 
   for (uint32_t r = blockIdx.x; r < nchunks; r += gridDim.x) B[(size_t)r * RADIX + threadIdx.x] += ds;
 }
 
+// Tile handled by block b of a launch whose tiles are independent.  Blocks
+// are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md "Workgroup
+// dispatch"; speed only, never correctness), so XCD x = b % 8 is given the
+// contiguous tile range [x*q + min(x, r), ...) of a q*8 + r grid: the lines
+// where neighbouring tiles' digit runs meet are then written through one L2
+// and merge there instead of leaving two L2s as partial lines (measured on
+// MI355X: 4-bit pass 467 -> 428 us at 2^28 keys; a 256-run scatter probe
+// 1305 -> 603 us).  A bijection for every grid size.
+__device__ __forceinline__ uint32_t xcd_tile_of_block() {
+  const uint32_t g = gridDim.x, q = g >> 3, r = g & 7u, x = blockIdx.x & 7u, i = blockIdx.x >> 3;
+  return x * q + min(x, r) + i;
+}
+
 // The pass kernel of the tile-offset path: the onesweep tile body with the
 // run offsets read from the scanned counts.  FUSE: also count the next digit
 // (op_next) of every written key per destination tile into C_next (4-bit
 // digits: a run of one digit covers at most two destination tiles, so the
-// per-tile aggregate has RADIX x 2 x RADIX entries).  The tile's row of C is
-// zeroed after use (it becomes the C_next of the pass after the next).
+// per-tile aggregate has 2 x RADIX x RADIX entries, laid out [slot][d][dn]:
+// a wave's sorted keys mostly share d and slot, so its LDS atomics spread
+// over consecutive dn banks).  The tile's row of C is zeroed after use (it
+// becomes the C_next of the pass after the next).
 template <int BITS, int BLOCK, int ITEMS, typename K, typename V, bool FUSE>
 __global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, K* __restrict__ kout,
                                                      const V* __restrict__ vin, V* __restrict__ vout,
@@ -817,24 +854,28 @@ __global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, 
   constexpr int TILE = BLOCK * ITEMS;
   constexpr int WSPAN = ITEMS * kWave;
   constexpr int CH = kColRowsPerLane * (256 / RADIX);
+  constexpr int NEXT = 2 * RADIX * RADIX;
+  constexpr int SPLIT = 2;  // store phase in two unrolled halves (register pressure)
+  constexpr int SP = ITEMS / SPLIT;
   static_assert(RADIX <= BLOCK, "one digit per thread in the block phase");
-  static_assert(!FUSE || RADIX * 2 * RADIX <= 2 * BLOCK, "fused next-count table: two entries per thread");
+  static_assert(!FUSE || (BITS == 4 && NEXT % BLOCK == 0), "fused next-pass counts: 4-bit digits");
 
   __shared__ K s_keys[TILE];
   __shared__ VS s_vals[HAS_V ? TILE : 1];
   __shared__ uint32_t s_whist[WAVES][RADIX];
-  __shared__ uint32_t s_outbase[RADIX];
+  __shared__ uint2 s_ob[RADIX];  // (run base - local start, local position where the run enters the next tile)
   __shared__ uint32_t s_tfirst[RADIX];
-  __shared__ uint32_t s_next[FUSE ? RADIX * 2 * RADIX : 1];
+  __shared__ uint32_t s_next[FUSE ? NEXT : 1];
   __shared__ uint32_t s_wsum[WAVES];
 
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int w = tid / kWave;
-  const uint32_t t = blockIdx.x;
+  const uint32_t t = xcd_tile_of_block();
   for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0u;
   if constexpr (FUSE) {
-    for (int i = tid; i < RADIX * 2 * RADIX; i += BLOCK) s_next[i] = 0u;
+#pragma unroll
+    for (int q = 0; q < NEXT / BLOCK; ++q) s_next[tid + q * BLOCK] = 0u;
   }
   // this tile's run offsets (independent of every other tile)
   uint32_t gofs = 0;
@@ -887,8 +928,9 @@ __global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, 
       s_whist[i][tid] = run;
       run += c;
     }
-    s_outbase[tid] = gofs - excl;
-    s_tfirst[tid] = gofs / TILE;  // first destination tile of this digit's run
+    const uint32_t ob = gofs - excl, tf = gofs / TILE;
+    s_ob[tid] = make_uint2(ob, (tf + 1) * TILE - ob);
+    s_tfirst[tid] = tf;
   }
   __syncthreads();
 
@@ -903,23 +945,53 @@ __global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, 
   }
   __syncthreads();
 
-  if constexpr (!FUSE) {
-    write_tile<BLOCK, ITEMS, HAS_V>(s_keys, s_vals, s_outbase, kout, vout, valid, op);
+  if (full) {
+    // unrolled halves: the LDS reads of a half issue back to back, then its
+    // global stores, then (FUSE) its next-digit LDS atomics
+#pragma unroll
+    for (int h = 0; h < SPLIT; ++h) {
+      K kk[SP];
+      uint2 ob[SP];
+#pragma unroll
+      for (int j = 0; j < SP; ++j) kk[j] = s_keys[tid + (h * SP + j) * BLOCK];
+#pragma unroll
+      for (int j = 0; j < SP; ++j) ob[j] = s_ob[op(kk[j])];
+#pragma unroll
+      for (int j = 0; j < SP; ++j) {
+        const uint32_t i = tid + (h * SP + j) * BLOCK;
+        kout[ob[j].x + i] = kk[j];
+        if constexpr (HAS_V) vout[ob[j].x + i] = s_vals[i];
+      }
+      if constexpr (FUSE) {
+#pragma unroll
+        for (int j = 0; j < SP; ++j) {
+          const uint32_t i = tid + (h * SP + j) * BLOCK;
+          const uint32_t slot = i >= ob[j].y ? (uint32_t)(RADIX * RADIX) : 0u;
+          atomicAdd(&s_next[slot + op(kk[j]) * RADIX + op_next(kk[j])], 1u);
+        }
+      }
+    }
   } else {
     for (uint32_t i = tid; i < valid; i += BLOCK) {
       const K kk = s_keys[i];
       const uint32_t d = op(kk);
-      const uint32_t o = s_outbase[d] + i;
-      kout[o] = kk;
-      if constexpr (HAS_V) vout[o] = s_vals[i];
-      const uint32_t slot = o / TILE - s_tfirst[d];  // 0 or 1
-      atomicAdd(&s_next[(d * 2 + slot) * RADIX + op_next(kk)], 1u);
+      const uint2 ob = s_ob[d];
+      kout[ob.x + i] = kk;
+      if constexpr (HAS_V) vout[ob.x + i] = s_vals[i];
+      if constexpr (FUSE) {
+        const uint32_t slot = i >= ob.y ? (uint32_t)(RADIX * RADIX) : 0u;
+        atomicAdd(&s_next[slot + d * RADIX + op_next(kk)], 1u);
+      }
     }
+  }
+  if constexpr (FUSE) {
     __syncthreads();
-    for (int e = tid; e < RADIX * 2 * RADIX; e += BLOCK) {
+#pragma unroll
+    for (int q = 0; q < NEXT / BLOCK; ++q) {
+      const uint32_t e = tid + q * BLOCK;
       const uint32_t c = s_next[e];
       if (c) {
-        const uint32_t d = e / (2 * RADIX), slot = (e / RADIX) & 1u, dn = e % RADIX;
+        const uint32_t slot = e / (RADIX * RADIX), d = (e / RADIX) % RADIX, dn = e % RADIX;
         atomicAdd(&C_next[(size_t)(s_tfirst[d] + slot) * RADIX + dn], c);
       }
     }
@@ -1241,28 +1313,23 @@ hipError_t run_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout,
 template <typename K, typename V>
 hipError_t run_digit_pass(Workspace& ws, int bits, const K* kin, K* kout, const V* vin, V* vout,
                           size_t n, uint32_t shift, uint32_t nbits, hipStream_t st) {
-  RadixDigit op{shift, (nbits >= 32) ? 0xffffffffu : ((1u << nbits) - 1u)};
+  RadixDigit op{shift, (1u << nbits) - 1u};  // nbits <= 8
   if (bits == 8) return run_pass<8>(ws, kin, kout, vin, vout, n, op, st);
   if (bits == 4) return run_pass<4>(ws, kin, kout, vin, vout, n, op, st);
   return hipErrorInvalidValue;
 }
 
-// Algorithm choice: onesweep (default) needs n < 2^30 (30-bit look-back
-// values); LIBSORT_ALGO=rts forces reduce-then-scan.
-bool use_onesweep(size_t n) {
-  if (get_algorithm() == 2) return false;
-  return n < (1ull << 30);
-}
-
 // Which pass algorithm a sort with `bits`-bit digits over n keys runs.
 int choose_algorithm(size_t n, int bits) {
   const int a = get_algorithm();
-  if (n >= (1ull << 30)) return 2;  // 30-bit look-back values; 32-bit tile offsets
-  if (a == 1 || a == 2 || a == 3) return a;
-  // auto (measured on MI355X, 2^28 keys): 4-bit digits -> tile offsets with
-  // fused counts (~490 us/pass); 8-bit digits -> onesweep (~945 us/pass; the
-  // tile path needs a separate count read there, ~1080 us/pass)
-  return bits == 4 ? 3 : 1;
+  if (a == 2) return 2;
+  if (a == 1 && n < (1ull << 30)) return 1;  // onesweep status words carry 30-bit counts
+  // auto / tiles (and onesweep beyond its range): the tile-offset path, whose
+  // 32-bit offsets cover every n < 2^32.  Measured on MI355X at 2^28 keys:
+  // 4-bit digits 3.81 ms (fused counts, 432 us/pass) vs onesweep 5.41 ms;
+  // 8-bit digits 2.94 ms (count 234 + scan 33 + pass 464 us) vs onesweep 3.60 ms.
+  (void)bits;
+  return 3;
 }
 
 // Tile-offset path geometry.  4-bit digits: 256-thread tiles of 4096 keys and
@@ -1406,7 +1473,7 @@ template <int BITS, typename K, typename V>
 hipError_t onesweep_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout, size_t n, int p,
                          int P, uint32_t shift, uint32_t nbits, uint32_t tiles, hipStream_t st) {
   constexpr int RADIX = 1 << BITS;
-  RadixDigit op{shift, (nbits >= 32) ? 0xffffffffu : ((1u << nbits) - 1u)};
+  RadixDigit op{shift, (1u << nbits) - 1u};  // nbits <= 8
   uint32_t* status = ws.os_status[p & 1];
   uint32_t* next = (p + 1 < P) ? ws.os_status[(p + 1) & 1] : nullptr;
   ScopedTimer tm("onesweep", st, n);

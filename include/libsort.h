@@ -127,11 +127,11 @@ LIBSORT_API bool libsortPopulateDevice(uint32_t* d_out, size_t n, uint64_t first
 LIBSORT_API int libsortSetDigitBits(int bits);
 LIBSORT_API int libsortGetDigitBits(void);
 
-/* Pass algorithm: 0 = auto (default: tile offsets for 4-bit digits, onesweep
- * for 8-bit digits, reduce-then-scan for n >= 2^30), 1 = onesweep (one kernel
- * per digit, decoupled look-back), 2 = reduce-then-scan (upsweep + scan +
- * downsweep), 3 = tile offsets (per-tile counts + column scan + pass kernel
- * without look-back; 4-bit digits).  Initial value from LIBSORT_ALGO
+/* Pass algorithm: 0 = auto (default: tile offsets), 1 = onesweep (one kernel
+ * per digit, decoupled look-back; n < 2^30, else tile offsets), 2 =
+ * reduce-then-scan (upsweep + scan + downsweep), 3 = tile offsets (per-tile
+ * counts + column scan + pass kernel without look-back; 4-bit digits count
+ * the next pass inside the pass kernel).  Initial value from LIBSORT_ALGO
  * ("auto" / "onesweep" / "rts" / "tiles").  Returns the previous value, or -1
  * if `algo` is invalid. */
 LIBSORT_API int libsortSetAlgorithm(int algo);

@@ -2,6 +2,7 @@
 """Turns gpurun_out/prof_TAG into committed summaries under profiles/:
   profiles/TAG_kernel_stats.csv      rocprofv3 --stats of the bench command
   profiles/TAG_bench.json            the bench line
+  profiles/TAG_bw_probe.txt          HBM ceiling probes (tools/bw_probe)
   profiles/pmc_<kernel>.json         HBM bytes per launch from FETCH_SIZE /
                                      WRITE_SIZE (read by bench.py as `traffic`)
 gfx950 correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE reports half the
@@ -24,6 +25,8 @@ if (src / "bench.json").exists():
     shutil.copy(src / "bench.json", dst / ("%s_bench.json" % tag))
 if (src / "calib.txt").exists():
     shutil.copy(src / "calib.txt", dst / ("%s_calib_copy_rocprim.txt" % tag))
+if (src / "bw_probe.txt").exists():
+    shutil.copy(src / "bw_probe.txt", dst / ("%s_bw_probe.txt" % tag))
 
 
 def per_kernel(counter):
