@@ -544,6 +544,22 @@ LIBSORT_EXPORT int libsortPartitionU32(const uint32_t* d_in, uint32_t* d_out, si
              : 0;
 }
 
+LIBSORT_EXPORT int libsortPartitionLutU32(const uint32_t* d_in, uint32_t* d_out, size_t n, const uint8_t* d_lut,
+                                          uint32_t lut_shift, uint32_t nbuckets, uint32_t* d_bounds,
+                                          void* stream) {
+  if (n > 0 && (const uint32_t*)d_out == d_in) {
+    set_error("libsortPartitionLutU32: out of place only");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(partition_lut_u32(ws, d_in, d_out, n, d_lut, (int)lut_shift, (int)nbuckets, d_bounds, st),
+                         "libsortPartitionLutU32");
+         })
+             ? 1
+             : 0;
+}
+
 LIBSORT_EXPORT int libsortSegmentCopyU32(const uint32_t* d_src, uint32_t* d_dst, size_t nseg,
                                          const uint64_t* src_off, const uint64_t* dst_off,
                                          const uint64_t* len, void* stream) {

@@ -124,6 +124,12 @@ hipError_t histogram_u32(Workspace& ws, const uint32_t* keys, size_t n, int shif
 hipError_t partition_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n,
                          const uint32_t* splitters, int nsplit, uint32_t* d_counts,
                          hipStream_t stream);
+// Stable partition of `in` into `out` (in != out) by bucket = lut[key >>
+// lut_shift] (lut: device, 1 << (32 - lut_shift) one-byte entries, 4-byte
+// aligned, 20 <= lut_shift <= 30, entries < nbuckets <= 256); d_bounds (may
+// be null) receives the nbuckets bucket starts.
+hipError_t partition_lut_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, const uint8_t* d_lut,
+                             int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t stream);
 hipError_t segment_copy_u32(Workspace& ws, const uint32_t* src, uint32_t* dst, size_t nseg,
                             const uint64_t* src_off, const uint64_t* dst_off, const uint64_t* len,
                             hipStream_t stream);

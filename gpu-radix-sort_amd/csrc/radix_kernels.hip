@@ -64,6 +64,38 @@ struct SplitDigit {
   }
 };
 
+// Bucket = lut[key >> shift] & mask: a table over the top 32 - shift bits
+// (shift >= 20: at most 4096 one-byte entries), staged into LDS by the
+// kernels that use it (bind_op).  The mask (radix - 1) keeps a bad table
+// entry from indexing outside the kernel's counters.  Used by the range
+// partition of the multi-GPU schedule (buckets = (round, destination rank)).
+struct LutDigit {
+  const uint8_t* g;  // device table, 1 << (32 - shift) entries
+  uint32_t shift;
+  uint32_t mask;
+  const uint8_t* s;  // LDS copy, set by bind_op
+  __device__ __forceinline__ uint32_t operator()(uint32_t k) const { return s[k >> shift] & mask; }
+  __device__ __forceinline__ uint32_t operator()(uint64_t k) const { return s[(uint32_t)(k >> 32) >> shift] & mask; }
+};
+constexpr int kLutMaxBytes = 4096;
+
+template <typename Op> struct OpLds { static constexpr int bytes = 1; };
+template <> struct OpLds<LutDigit> { static constexpr int bytes = kLutMaxBytes; };
+
+// Stages the op's table (if any) into `smem`; the caller puts a barrier
+// between this and the op's first use.
+template <typename Op>
+__device__ __forceinline__ Op bind_op(Op op, uint8_t* smem, uint32_t tid, uint32_t nthreads) {
+  if constexpr (std::is_same<Op, LutDigit>::value) {
+    const uint32_t words = (1u << (32 - op.shift)) / 4u;
+    for (uint32_t i = tid; i < words; i += nthreads)
+      reinterpret_cast<uint32_t*>(smem)[i] = reinterpret_cast<const uint32_t*>(op.g)[i];
+    op.s = smem;
+  }
+  (void)smem; (void)tid; (void)nthreads;
+  return op;
+}
+
 template <typename K> struct VecOf;
 template <> struct VecOf<uint32_t> { using type = uint4; static constexpr int n = 4; };
 template <> struct VecOf<uint64_t> { using type = ulonglong2; static constexpr int n = 2; };
@@ -679,15 +711,17 @@ constexpr int kColRowsPerLane = 16;
 
 // Per-tile digit counts of the first pass; also zeroes `zero_buf` (the
 // next-pass count buffer).  One block per tile.
-template <int BITS, int BLOCK, int ITEMS, typename K>
-__global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ keys, uint32_t n, RadixDigit op,
+template <int BITS, int BLOCK, int ITEMS, typename K, typename Op = RadixDigit>
+__global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ keys, uint32_t n, Op op_in,
                                                        uint32_t* __restrict__ counts,
                                                        uint32_t* __restrict__ zero_buf, uint32_t zero_words) {
   constexpr int RADIX = 1 << BITS;
   constexpr int TILE = BLOCK * ITEMS;
   constexpr int COPIES = RADIX <= 16 ? 16 : 1;  // spread same-digit LDS atomics
   __shared__ uint32_t s_h[COPIES][RADIX];
+  __shared__ __attribute__((aligned(16))) uint8_t s_lut[OpLds<Op>::bytes];
   const uint32_t tid = threadIdx.x;
+  const Op op = bind_op(op_in, s_lut, tid, BLOCK);
   for (uint32_t i = tid; i < COPIES * RADIX; i += BLOCK) (&s_h[0][0])[i] = 0u;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + tid; i < zero_words; i += (uint64_t)gridDim.x * BLOCK)
     zero_buf[i] = 0u;
@@ -841,10 +875,10 @@ __device__ __forceinline__ uint32_t xcd_tile_of_block() {
 // a wave's sorted keys mostly share d and slot, so its LDS atomics spread
 // over consecutive dn banks).  The tile's row of C is zeroed after use (it
 // becomes the C_next of the pass after the next).
-template <int BITS, int BLOCK, int ITEMS, typename K, typename V, bool FUSE>
+template <int BITS, int BLOCK, int ITEMS, typename K, typename V, bool FUSE, typename Op = RadixDigit>
 __global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, K* __restrict__ kout,
                                                      const V* __restrict__ vin, V* __restrict__ vout,
-                                                     uint32_t n, RadixDigit op, RadixDigit op_next,
+                                                     uint32_t n, Op op_in, RadixDigit op_next,
                                                      uint32_t* __restrict__ C, const uint32_t* __restrict__ B,
                                                      uint32_t* __restrict__ C_next) {
   constexpr bool HAS_V = !std::is_same<V, NoValue>::value;
@@ -867,11 +901,14 @@ __global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, 
   __shared__ uint32_t s_tfirst[RADIX];
   __shared__ uint32_t s_next[FUSE ? NEXT : 1];
   __shared__ uint32_t s_wsum[WAVES];
+  __shared__ __attribute__((aligned(16))) uint8_t s_lut[OpLds<Op>::bytes];
 
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int w = tid / kWave;
   const uint32_t t = xcd_tile_of_block();
+  const Op op = bind_op(op_in, s_lut, tid, BLOCK);
+  if constexpr (OpLds<Op>::bytes > 1) __syncthreads();
   for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0u;
   if constexpr (FUSE) {
 #pragma unroll
@@ -1349,13 +1386,13 @@ inline uint32_t tp_chunks(uint32_t tiles, int bits) {
   return (tiles + ch - 1) / ch;
 }
 
-template <int BITS, typename K>
-hipError_t tiles_counts(Workspace& ws, const K* in, size_t n, RadixDigit op, uint32_t tiles, uint32_t* C,
+template <int BITS, typename K, typename Op = RadixDigit>
+hipError_t tiles_counts(Workspace& ws, const K* in, size_t n, Op op, uint32_t tiles, uint32_t* C,
                         uint32_t* zero, uint32_t zero_words, hipStream_t st) {
   constexpr int B = tp_block(BITS);
   ScopedTimer tm("tilecounts", st, n);
-  hipLaunchKernelGGL((k_tile_counts<BITS, B, tp_items<K>(), K>), dim3(tiles), dim3(B), 0, st, in, (uint32_t)n, op,
-                     C, zero, zero_words);
+  hipLaunchKernelGGL((k_tile_counts<BITS, B, tp_items<K>(), K, Op>), dim3(tiles), dim3(B), 0, st, in, (uint32_t)n,
+                     op, C, zero, zero_words);
   return hipGetLastError();
 }
 
@@ -1659,6 +1696,44 @@ hipError_t partition_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_
     LS_TRY(hipGetLastError());
   }
   return hipSuccess;
+}
+
+namespace {
+// One tile-offset pass whose digit is a table lookup: per-tile counts, column
+// scan, pass kernel; bucket starts = row 0 of the scanned chunk totals.
+template <int BITS>
+hipError_t partition_lut_impl(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, const uint8_t* d_lut,
+                              int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st) {
+  constexpr int RADIX = 1 << BITS;
+  constexpr int B = tp_block(BITS);
+  const uint32_t tiles = tp_tiles<uint32_t>(n, BITS);
+  LS_TRY(ws.ensure_tiles((size_t)tiles * RADIX, ((size_t)tp_chunks(tiles, BITS) + 1) * RADIX));
+  const LutDigit op{d_lut, (uint32_t)lut_shift, (uint32_t)RADIX - 1u, nullptr};
+  LS_TRY((tiles_counts<BITS, uint32_t, LutDigit>(ws, in, n, op, tiles, ws.tc[0], nullptr, 0, st)));
+  LS_TRY(tiles_colscan<BITS>(ws, ws.tc[0], tiles, st));
+  {
+    ScopedTimer tm("partition", st, n);
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<uint32_t>(), uint32_t, NoValue, false, LutDigit>), dim3(tiles),
+                       dim3(B), 0, st, in, out, (const NoValue*)nullptr, (NoValue*)nullptr, (uint32_t)n, op,
+                       RadixDigit{0u, 1u}, ws.tc[0], (const uint32_t*)ws.tb, ws.tc[1]);
+    LS_TRY(hipGetLastError());
+  }
+  if (d_bounds) LS_TRY(hipMemcpyAsync(d_bounds, ws.tb, (size_t)nbuckets * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  return hipSuccess;
+}
+}  // namespace
+
+hipError_t partition_lut_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, const uint8_t* d_lut,
+                             int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st) {
+  if (n > 0xffffffffull || lut_shift < 20 || lut_shift > 30 || nbuckets < 1 || nbuckets > 256)
+    return hipErrorInvalidValue;
+  if (n == 0) {
+    if (d_bounds) LS_TRY(hipMemsetAsync(d_bounds, 0, (size_t)nbuckets * sizeof(uint32_t), st));
+    return hipSuccess;
+  }
+  if (!in || !out || !d_lut || in == out || (reinterpret_cast<uintptr_t>(d_lut) & 3u)) return hipErrorInvalidValue;
+  if (nbuckets <= 16) return partition_lut_impl<4>(ws, in, out, n, d_lut, lut_shift, nbuckets, d_bounds, st);
+  return partition_lut_impl<8>(ws, in, out, n, d_lut, lut_shift, nbuckets, d_bounds, st);
 }
 
 hipError_t segment_copy_u32(Workspace& ws, const uint32_t* src, uint32_t* dst, size_t nseg,

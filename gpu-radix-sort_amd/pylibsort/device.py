@@ -125,6 +125,22 @@ def partition_u32(keys, splitters, out=None, counts=None):
     return out, counts
 
 
+def partition_lut_u32(keys, lut, lut_shift, nbuckets, out=None, bounds=None):
+    """Stable partition by bucket = lut[key >> lut_shift] (lut: uint8 CUDA
+    tensor of 2**(32 - lut_shift) entries, each < nbuckets).  Returns (out,
+    bounds) with bounds = int32 tensor of the nbuckets bucket starts."""
+    _need(keys, _U32, "keys")
+    if lut.dtype != torch.uint8 or not lut.is_cuda or lut.numel() != 1 << (32 - lut_shift):
+        raise ValueError("lut must be a uint8 CUDA tensor of 2**(32 - lut_shift) entries")
+    lut = lut.contiguous()
+    out = torch.empty_like(keys) if out is None else out
+    _need(out, _U32, "out")
+    bounds = torch.empty(nbuckets, dtype=torch.int32, device=keys.device) if bounds is None else bounds
+    _check(_lib().libsortPartitionLutU32(_ptr(keys), _ptr(out), keys.numel(), _ptr(lut), lut_shift, nbuckets,
+                                         _ptr(bounds), _stream()), "libsortPartitionLutU32")
+    return out, bounds
+
+
 def segment_copy_u32(src, dst, src_off, dst_off, lens):
     """dst[dst_off[i] + j] = src[src_off[i] + j] for j < lens[i]."""
     _need(src, _U32, "src")

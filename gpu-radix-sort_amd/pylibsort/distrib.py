@@ -14,12 +14,18 @@ globally sorted array, S = ceil(N/R), the reference's equal re-cut):
          partial sort (gpuPartial on the device), an allgather of the per-rank
          bucket counts, one alltoallv of contiguous slices, and a segment
          gather into bucket-major / rank-minor order.  32/width exchanges.
-  "msd"  one exchange: a 12-bit histogram of the top key bits (allgather),
-         bucket ranges assigned to ranks, one stable range partition + one
-         alltoallv, a full local LSD sort, and a small alltoallv that shifts
-         the few surplus keys to the neighbour so the shards are exact.
-         Falls back to "lsd" when one top-12-bit bucket is so large that a rank
-         would receive more than `max_imbalance` x S keys.
+  "msd"  range-split rounds: a (sampled) 12-bit histogram of the top key
+         bits (allgather) assigns contiguous key ranges to (rank, round), R x K
+         groups; ONE stable table partition (libsortPartitionLutU32) lays the
+         keys out round-major / destination-minor; K alltoallv exchanges are
+         issued at once (RCCL's stream runs them back to back) and round i is
+         sorted into its final slice of the output as soon as it has arrived,
+         overlapping the exchange of the later rounds.  The rounds are
+         disjoint key ranges in increasing order, so no merge is needed.  A
+         small alltoallv then shifts the few surplus keys to the neighbours so
+         the shards are exact.  Falls back to "lsd" when one top-12-bit bucket
+         is so large that a rank would receive more than `max_imbalance` x S
+         keys.
 
 The local operations come from an `ops` backend.  The product backend is
 HipOps (libsort's HIP kernels on torch CUDA tensors).  The CPU tests pass an
@@ -71,6 +77,19 @@ class HipOps:
         out = self.empty(keys.numel()) if out is None else out
         return self.D.partition_u32(keys, splitters, out=out)[0]
 
+    def partition_lut(self, keys, lut, shift, nbuckets):
+        """(partitioned keys, bucket starts as host int64 numpy array)."""
+        t = torch.from_numpy(np.ascontiguousarray(lut, dtype=np.uint8)).to(self.device)
+        out, b = self.D.partition_lut_u32(keys, t, shift, nbuckets, out=self.empty(keys.numel()))
+        return out, b.cpu().numpy().view(np.uint32).astype(np.int64)
+
+    def sample(self, keys, stride, block=4096):
+        """Every `stride`-th block of `block` keys (all keys when few)."""
+        nb = keys.numel() // block
+        if stride <= 1 or nb < 4 * stride:
+            return keys
+        return keys[:nb * block].view(nb, block)[::stride].contiguous().view(-1)
+
     def segment_copy(self, src, dst, so, do, ln):
         return self.D.segment_copy_u32(src, dst, so, do, ln)
 
@@ -104,6 +123,19 @@ def _alltoallv(send, send_counts, recv_counts, ops, group):
     else:
         dist.all_to_all_single(recv, send, rs, ss, group=group)
     return recv
+
+
+def _alltoallv_into(recv, send, send_counts, recv_counts, group, async_op=False):
+    """all_to_all_single into `recv`; returns the async work handle (or None).
+    Host-staged (gloo) exchanges run synchronously."""
+    rs = [int(c) for c in recv_counts]
+    ss = [int(c) for c in send_counts]
+    if _host_staged(group) and send.is_cuda:
+        r_host = torch.empty(recv.numel(), dtype=recv.dtype)
+        dist.all_to_all_single(r_host, send.cpu(), rs, ss, group=group)
+        recv.copy_(r_host)
+        return None
+    return dist.all_to_all_single(recv, send, rs, ss, group=group, async_op=async_op and not _host_staged(group))
 
 
 def shard_cut(N, R):
@@ -205,25 +237,66 @@ def plan_msd(H, R, hist_bits=HIST_BITS):
     return splitters, dest, n_recv
 
 
-def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True):
-    """One-exchange schedule; see module docstring."""
+def plan_rounds(H, R, K, hist_bits=HIST_BITS):
+    """Contiguous top-bit bucket ranges for (rank, round) from the gathered
+    (possibly sampled) histograms H[R, 2^b]: R*K groups of about equal
+    estimated count, group g -> rank g // K, round g % K.  Returns (lut,
+    est_per_rank) with lut[b] = round * R + rank (the partition bucket)."""
+    G = H.sum(axis=0).astype(np.float64)
+    T = float(G.sum())
+    if T > 0:
+        mid = np.cumsum(G) - G / 2.0
+        grp = np.minimum((mid * (R * K) / T).astype(np.int64), R * K - 1)
+        grp = np.maximum.accumulate(grp)
+    else:
+        grp = np.zeros(G.size, dtype=np.int64)
+    rank, rnd = grp // K, grp % K
+    lut = (rnd * R + rank).astype(np.uint8)
+    return lut, np.bincount(rank, weights=G, minlength=R)
+
+
+def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=4, sample_stride=16):
+    """Range-split rounds schedule; see module docstring."""
     R = dist.get_world_size(group)
     r = dist.get_rank(group)
-    h = ops.histogram(keys, 32 - HIST_BITS, HIST_BITS)
-    H = _allgather_np(h.cpu().numpy().astype(np.int64), keys, group)   # [R, 4096]
-    N = int(H.sum())
+    K = max(1, min(int(rounds), 256 // R))
+    n = keys.numel()
+    h = ops.histogram(ops.sample(keys, sample_stride), 32 - HIST_BITS, HIST_BITS)
+    hv = np.concatenate([h.cpu().numpy().astype(np.int64), [n]])
+    HN = _allgather_np(hv, keys, group)                       # [R, 4096 + 1]
+    H, n_all = HN[:, :-1], HN[:, -1]
+    N = int(n_all.sum())
     S, _ = shard_cut(N, R)
-    splitters, dest, n_recv = plan_msd(H, R)
-    if N and n_recv.max() > max_imbalance * S + 4096:
+    lut, est = plan_rounds(H, R, K)
+    hs = float(H.sum())
+    if N and hs and est.max() * N / hs > max_imbalance * S + 4096:
         return sort_lsd(keys, ops, group)
-    send = np.array([H[r][dest == d].sum() for d in range(R)], dtype=np.int64)
-    recv_counts = np.array([H[s][dest == r].sum() for s in range(R)], dtype=np.int64)
-    part = ops.partition(keys, splitters) if len(splitters) else keys
-    recv = _alltoallv(part, send, recv_counts, ops, group)
-    srt = ops.sort(recv)
+    NB = R * K
+    part, b = ops.partition_lut(keys, lut, 32 - HIST_BITS, NB)
+    sizes = np.diff(np.asarray(b, dtype=np.int64), append=n)    # bucket j = round * R + dest
+    C = _allgather_np(sizes, keys, group)                      # [R, NB]
+    recv_tot = np.array([int(C[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
+    roff = np.concatenate([[0], np.cumsum(recv_tot)])
+    recv = ops.empty(int(roff[-1]))
+    out = ops.empty(int(roff[-1]))
+    works = []
+    for i in range(K):
+        if not C[:, i * R:(i + 1) * R].any():                  # identical on every rank
+            works.append(None)
+            continue
+        s0 = int(b[i * R])
+        ss = sizes[i * R:(i + 1) * R]
+        works.append(_alltoallv_into(recv[int(roff[i]):int(roff[i + 1])], part[s0:s0 + int(ss.sum())], ss,
+                                     C[:, i * R + r], group, async_op=True))
+    for i in range(K):
+        if works[i] is not None:
+            works[i].wait()                                    # stream-level: the sort waits on RCCL
+        if recv_tot[i]:
+            ops.sort(recv[int(roff[i]):int(roff[i + 1])], out=out[int(roff[i]):int(roff[i + 1])])
     if not balance:
-        return srt
-    return _rebalance(srt, n_recv, ops, group)
+        return out
+    n_recv = np.array([int(C[:, d::R].sum()) for d in range(R)], dtype=np.int64)
+    return _rebalance(out, n_recv, ops, group)
 
 
 def distrib_sort(keys, ops=None, group=None, schedule="msd", **kw):
@@ -239,4 +312,4 @@ def distrib_sort(keys, ops=None, group=None, schedule="msd", **kw):
     raise ValueError("schedule must be 'msd' or 'lsd'")
 
 
-__all__ = ["HipOps", "distrib_sort", "sort_lsd", "sort_msd", "plan_msd", "shard_cut"]
+__all__ = ["HipOps", "distrib_sort", "sort_lsd", "sort_msd", "plan_msd", "plan_rounds", "shard_cut"]

@@ -110,6 +110,17 @@ LIBSORT_API bool libsortPartitionU32(const uint32_t* d_in, uint32_t* d_out, size
                                      const uint32_t* splitters, uint32_t nsplit,
                                      uint32_t* d_counts, void* stream);
 
+/* Stable partition by table: element x goes to bucket lut[x >> lut_shift]
+ * (d_lut: device, 1 << (32 - lut_shift) one-byte entries, 4-byte aligned,
+ * 20 <= lut_shift <= 30, every entry < nbuckets <= 256).  d_out (!= d_in)
+ * receives the buckets in order; d_bounds (nullable, device, nbuckets uint32)
+ * the bucket starts.  One tile-offset pass (per-tile counts, column scan,
+ * scatter); the multi-GPU schedule partitions by (round, destination rank)
+ * with it. */
+LIBSORT_API bool libsortPartitionLutU32(const uint32_t* d_in, uint32_t* d_out, size_t n,
+                                        const uint8_t* d_lut, uint32_t lut_shift,
+                                        uint32_t nbuckets, uint32_t* d_bounds, void* stream);
+
 /* Gather-copy of nseg segments: dst[dst_off[i] + j] = src[src_off[i] + j] for
  * j < len[i].  The three tables are host arrays.  Used to put exchanged
  * buckets into bucket-major / rank-minor order between distributed rounds. */

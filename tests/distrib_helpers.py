@@ -32,7 +32,11 @@ class OracleOps:
         return self.torch.empty(n, dtype=self.torch.int32)
 
     def sort(self, keys, out=None):
-        return self._t(self.o.sort_u32(self._np(keys)))
+        res = self._t(self.o.sort_u32(self._np(keys)))
+        if out is None:
+            return res
+        out.copy_(res)
+        return out
 
     def partial_sort(self, keys, offset, width, out=None):
         d, b = self.o.partial_u32(self._np(keys), offset, width)
@@ -47,6 +51,18 @@ class OracleOps:
         x = self._np(keys)
         b = np.searchsorted(np.asarray(splitters, dtype=np.uint64), x.astype(np.uint64), side="right")
         return self._t(x[np.argsort(b, kind="stable")])
+
+    def partition_lut(self, keys, lut, shift, nbuckets):
+        x = self._np(keys)
+        b = np.asarray(lut, dtype=np.uint8)[x >> np.uint32(shift)].astype(np.int64)
+        starts = np.concatenate([[0], np.cumsum(np.bincount(b, minlength=nbuckets))[:-1]])
+        return self._t(x[np.argsort(b, kind="stable")]), starts.astype(np.int64)
+
+    def sample(self, keys, stride, block=4096):
+        nb = keys.numel() // block
+        if stride <= 1 or nb < 4 * stride:
+            return keys
+        return keys[:nb * block].view(nb, block)[::stride].contiguous().view(-1)
 
     def segment_copy(self, src, dst, so, do, ln):
         s = src.numpy()
@@ -63,7 +79,7 @@ def shard_inputs(x, R):
     return [x[min(N, r * S):min(N, (r + 1) * S)] for r in range(R)]
 
 
-def rank_worker(rank, world, port, x, schedule, outdir, use_gpu):
+def rank_worker(rank, world, port, x, schedule, outdir, use_gpu, kw=None):
     """Runs distrib_sort on this rank's shard and saves the result."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -79,13 +95,13 @@ def rank_worker(rank, world, port, x, schedule, outdir, use_gpu):
     else:
         ops = OracleOps()
         keys = torch.from_numpy(shard.view(np.int32).copy())
-    res = distrib.distrib_sort(keys, ops=ops, schedule=schedule)
+    res = distrib.distrib_sort(keys, ops=ops, schedule=schedule, **(kw or {}))
     np.save(os.path.join(outdir, "rank%d.npy" % rank), res.cpu().numpy().view(np.uint32))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def run_ranks(x, world, schedule, tmpdir, use_gpu=False, port=29611):
+def run_ranks(x, world, schedule, tmpdir, use_gpu=False, port=29611, kw=None):
     import torch.multiprocessing as mp
-    mp.spawn(rank_worker, args=(world, port, x, schedule, str(tmpdir), use_gpu), nprocs=world, join=True)
+    mp.spawn(rank_worker, args=(world, port, x, schedule, str(tmpdir), use_gpu, kw), nprocs=world, join=True)
     return [np.load(os.path.join(str(tmpdir), "rank%d.npy" % r)) for r in range(world)]

@@ -40,6 +40,55 @@ def test_distributed_sort_gloo(tmp_path, world, schedule, case):
             np.testing.assert_array_equal(s, r)
 
 
+@pytest.mark.parametrize("world,rounds", [(2, 1), (2, 3), (3, 8), (2, 128)])
+def test_msd_rounds_gloo(tmp_path, world, rounds):
+    """Range-split rounds: every round count (including rounds with no keys
+    and R*K capped at 256 buckets) gives the sorted array and equal shards."""
+    from oracle import oracle
+    x = oracle.pcg(50021, first=rounds)
+    shards = run_ranks(x, world, "msd", tmp_path, port=29700 + 7 * world + rounds % 50, kw={"rounds": rounds})
+    np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))
+    assert [s.size for s in shards] == [s.size for s in shard_inputs(x, world)]
+
+
+def test_msd_sampled_histogram_gloo(tmp_path):
+    """Large enough for the sampled top-bit histogram (every 16th 4096-key
+    block): the plan is estimated, the exchange sizes exact."""
+    from oracle import oracle
+    x = oracle.pcg(2 * 300007, first=11)
+    shards = run_ranks(x, 2, "msd", tmp_path, port=29790, kw={"rounds": 4})
+    np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))
+    assert [s.size for s in shards] == [s.size for s in shard_inputs(x, 2)]
+
+
+def test_msd_sparse_key_ranges_gloo(tmp_path):
+    """Keys in a few narrow ranges: most (rank, round) groups are empty."""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.integers(0, 1 << 22, 7000), rng.integers(0xF0000000, 0xF0400000, 9000),
+                        rng.integers(0x80000000, 0x80000100, 5000)]).astype(np.uint32)
+    rng.shuffle(x)
+    shards = run_ranks(x, 3, "msd", tmp_path, port=29795, kw={"rounds": 5, "max_imbalance": 10.0})
+    np.testing.assert_array_equal(np.concatenate(shards), np.sort(x))
+    assert [s.size for s in shards] == [s.size for s in shard_inputs(x, 3)]
+
+
+def test_plan_rounds_contiguous_and_balanced():
+    from pylibsort.distrib import plan_rounds
+    rng = np.random.default_rng(4)
+    R, K = 8, 4
+    H = np.stack([np.bincount(rng.integers(0, 4096, 200000), minlength=4096) for _ in range(R)])
+    lut, est = plan_rounds(H, R, K)
+    grp = (lut % R) * K + lut // R                 # back to key-order group index
+    assert lut.dtype == np.uint8 and lut.size == 4096
+    assert np.all(np.diff(grp.astype(np.int64)) >= 0) and grp[0] == 0 and grp[-1] == R * K - 1
+    tot = H.sum()
+    g = np.bincount(grp, weights=H.sum(axis=0), minlength=R * K)
+    assert g.max() <= tot / (R * K) + H.sum(axis=0).max() + 1
+    assert abs(est.sum() - tot) < 1e-6 and est.max() <= tot / R * 1.01 + H.sum(axis=0).max()
+    lut0, est0 = plan_rounds(np.zeros((R, 4096)), R, K)
+    assert not lut0.any() and not est0.any()
+
+
 def test_plan_msd_balances_uniform_and_flags_skew():
     from pylibsort.distrib import plan_msd, shard_cut
     rng = np.random.default_rng(3)

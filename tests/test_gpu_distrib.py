@@ -32,3 +32,16 @@ def test_distributed_skew_falls_back(tmp_path):
     x = rng.integers(0, 300, 200003, dtype=np.uint64).astype(np.uint32)  # one top bucket
     shards = run_ranks(x, 2, "msd", tmp_path, use_gpu=True, port=29790)
     np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))
+
+
+@pytest.mark.parametrize("rounds", [1, 4, 16])
+def test_msd_rounds_hip_backend(tmp_path, rounds):
+    """Range-split rounds with libsort's table partition and sorts on the GPU
+    (2 ranks sharing the GPU, gloo host-staged exchanges)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import oracle
+    x = oracle.pcg((1 << 20) + 777, first=rounds)
+    shards = run_ranks(x, 2, "msd", tmp_path, use_gpu=True, port=29820 + rounds, kw={"rounds": rounds})
+    np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))
+    assert [s.size for s in shards] == [s.size for s in shard_inputs(x, 2)]

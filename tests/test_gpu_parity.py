@@ -174,6 +174,24 @@ def test_histogram_and_partition(dev, oracle_mod):
         np.testing.assert_array_equal(cnt.cpu().numpy(), np.bincount(bucket, minlength=len(sp) + 1))
 
 
+@pytest.mark.parametrize("n", [0, 1, 4095, 4097, 200003, 1 << 20])
+@pytest.mark.parametrize("shift,nbuckets", [(20, 2), (20, 16), (24, 17), (20, 32), (28, 16), (30, 4), (20, 256)])
+def test_partition_lut(dev, oracle_mod, n, shift, nbuckets):
+    """libsortPartitionLutU32 (the multi-GPU schedule's partition) against a
+    stable numpy partition; 4-bit (<= 16 buckets) and 8-bit tile paths,
+    partial last tiles, buckets left empty."""
+    x = oracle_mod.pcg(n, first=n + shift)
+    rng = np.random.default_rng(shift * 1000 + nbuckets)
+    lut = np.sort(rng.integers(0, nbuckets, 1 << (32 - shift))).astype(np.uint8)  # contiguous ranges
+    if nbuckets == 32:
+        lut = rng.integers(0, nbuckets, 1 << (32 - shift)).astype(np.uint8)        # arbitrary table
+    out, b = dev.partition_lut_u32(_tensor(x), torch.from_numpy(lut).cuda(), shift, nbuckets)
+    bucket = lut[x >> np.uint32(shift)].astype(np.int64)
+    np.testing.assert_array_equal(_u32(out), x[np.argsort(bucket, kind="stable")])
+    starts = np.concatenate([[0], np.cumsum(np.bincount(bucket, minlength=nbuckets))[:-1]])
+    np.testing.assert_array_equal(b.cpu().numpy().astype(np.int64), starts)
+
+
 def test_segment_copy(dev):
     src = torch.arange(1000, dtype=torch.int32, device="cuda")
     dst = torch.zeros(1000, dtype=torch.int32, device="cuda")

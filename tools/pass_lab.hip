@@ -419,7 +419,13 @@ __device__ __forceinline__ uint32_t tile_of_block() {
   }
 }
 
-template <int CHAINS, bool LASTW, int SPLIT, bool ASM = true, int BLOCK = 256, bool XCD = false>
+// ABL (timing ablations, output wrong): 1 = write the sorted tile back to its
+// own tile (contiguous, copy-like addresses), 2 = no global key stores,
+// 3 = 2 + no next-pass count atomics/flush, 4 = 3 + no ballot rank
+// (identity positions), 5 = 4 + no LDS scatter/read-back (keys go straight
+// from the load registers to a dummy-conditioned store), 6 = full kernel but
+// no global flush of the next-pass counts, 7 = full kernel without counting.
+template <int CHAINS, bool LASTW, int SPLIT, bool ASM = true, int BLOCK = 256, bool XCD = false, int ABL = 0>
 __global__ __launch_bounds__(BLOCK) void k_pass_z(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout,
                                                 uint32_t shift, uint32_t nb, uint32_t* __restrict__ C,
                                                 const uint32_t* __restrict__ B, uint32_t* __restrict__ C_next) {
@@ -452,7 +458,12 @@ __global__ __launch_bounds__(BLOCK) void k_pass_z(const uint32_t* __restrict__ k
   const uint32_t* kp = kin + (uint64_t)t * TILE + w * WSPAN + lane;
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) k[j] = kp[j * kWave];
-  rank_lean4<CHAINS, LASTW, ASM>(k, rk, &s_whist[w * CHAINS * RADIX], shift, nb, &s_dummy[tid]);
+  if constexpr (ABL >= 4 && ABL < 6) {
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) rk[j] = w * WSPAN + j * kWave + lane;
+  } else {
+    rank_lean4<CHAINS, LASTW, ASM>(k, rk, &s_whist[w * CHAINS * RADIX], shift, nb, &s_dummy[tid]);
+  }
   __syncthreads();
   if (w == 0) {
     const uint32_t d = lane & (RADIX - 1);
@@ -479,9 +490,16 @@ __global__ __launch_bounds__(BLOCK) void k_pass_z(const uint32_t* __restrict__ k
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t d = __builtin_amdgcn_ubfe(k[j], shift, nb);
-    s_keys[s_whist[(w * CHAINS + j / (ITEMS / CHAINS)) * RADIX + d] + rk[j]] = k[j];
+    if constexpr (ABL == 5) {
+      if (k[j] == 0x9e3779b9u) kout[t] = rk[j];
+    } else if constexpr (ABL == 4) {
+      s_keys[rk[j]] = k[j] + d;
+    } else {
+      s_keys[s_whist[(w * CHAINS + j / (ITEMS / CHAINS)) * RADIX + d] + rk[j]] = k[j];
+    }
   }
   __syncthreads();
+  if constexpr (ABL != 5)
 #pragma unroll
   for (int h = 0; h < SPLIT; ++h) {
     uint32_t kk[SPER];
@@ -491,15 +509,22 @@ __global__ __launch_bounds__(BLOCK) void k_pass_z(const uint32_t* __restrict__ k
 #pragma unroll
     for (int j = 0; j < SPER; ++j) ob[j] = s_ob[__builtin_amdgcn_ubfe(kk[j], shift, 4)];
 #pragma unroll
-    for (int j = 0; j < SPER; ++j) kout[ob[j].x + tid + (h * SPER + j) * BLOCK] = kk[j];
+    for (int j = 0; j < SPER; ++j) {
+      if constexpr (ABL == 0 || ABL >= 6) kout[ob[j].x + tid + (h * SPER + j) * BLOCK] = kk[j];
+      if constexpr (ABL == 1) kout[(size_t)t * TILE + tid + (h * SPER + j) * BLOCK] = kk[j] + ob[j].x;
+      if constexpr (ABL >= 2 && ABL < 6) if (kk[j] == 0x9e3779b9u && ob[j].x == 7u) kout[t] = 1u;
+    }
 #pragma unroll
     for (int j = 0; j < SPER; ++j) {
-      const uint32_t slot = (uint32_t)(tid + (h * SPER + j) * BLOCK) >= ob[j].y ? 256u : 0u;
-      const uint32_t dd = __builtin_amdgcn_ubfe(kk[j], shift, 4), dn = __builtin_amdgcn_ubfe(kk[j], shift + 4, 4);
-      atomicAdd(&s_next[slot + dd * 16 + dn], 1u);
+      if constexpr (ABL < 3 || ABL == 6) {
+        const uint32_t slot = (uint32_t)(tid + (h * SPER + j) * BLOCK) >= ob[j].y ? 256u : 0u;
+        const uint32_t dd = __builtin_amdgcn_ubfe(kk[j], shift, 4), dn = __builtin_amdgcn_ubfe(kk[j], shift + 4, 4);
+        atomicAdd(&s_next[slot + dd * 16 + dn], 1u);
+      }
     }
   }
   __syncthreads();
+  if constexpr (ABL < 3)
 #pragma unroll
   for (int q = 0; q < 2 * RADIX * RADIX / BLOCK; ++q) {
     const int e = tid + q * BLOCK;
@@ -611,20 +636,37 @@ int main(int argc, char** argv) {
                          (const NoValue*)nullptr, (NoValue*)nullptr, (uint32_t)L.n, L.op, L.op_next, L.ws.tc[0], B,
                          L.ws.tc[1]);
     }});
-    V.push_back({"x chains2", [&] {
-      hipLaunchKernelGGL((k_pass_x<2, 1>), grid, blk, 0, L.st, L.in, L.out, L.op, L.op_next, L.ws.tc[0], B, L.ws.tc[1]);
-    }});
-    V.push_back({"z c1 s2", [&] {
-      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, false>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0], B,
-                         L.ws.tc[1]);
-    }});
     V.push_back({"z c1 s2 xcd", [&] {
       hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0], B,
                          L.ws.tc[1]);
     }});
-    V.push_back({"z c2 s2 xcd", [&] {
-      hipLaunchKernelGGL((k_pass_z<2, false, 2, true, 256, true>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0], B,
-                         L.ws.tc[1]);
+    V.push_back({"ABL contiguous stores", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 1>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
+                         B, L.ws.tc[1]);
+    }});
+    V.push_back({"ABL no key stores", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 2>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
+                         B, L.ws.tc[1]);
+    }});
+    V.push_back({"ABL +no counts", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 3>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
+                         B, L.ws.tc[1]);
+    }});
+    V.push_back({"ABL +no rank", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 4>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
+                         B, L.ws.tc[1]);
+    }});
+    V.push_back({"ABL stores, no flush", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 6>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
+                         B, L.ws.tc[1]);
+    }});
+    V.push_back({"ABL stores, no counting", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 7>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
+                         B, L.ws.tc[1]);
+    }});
+    V.push_back({"ABL +no lds tile", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 5>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
+                         B, L.ws.tc[1]);
     }});
   } else {
     V.push_back({"z512 c1 s2", [&] {
@@ -669,7 +711,8 @@ int main(int argc, char** argv) {
   for (auto& v : V) {
     v.us.clear();
     run_once(L, v);
-    if (std::string(v.name).find("unfused") == std::string::npos) check(L, v);
+    if (std::string(v.name).find("unfused") == std::string::npos && std::string(v.name).find("ABL") != 0)
+      check(L, v);
     v.us.clear();
   }
   for (int r = 0; r < rounds; ++r)
