@@ -475,6 +475,29 @@ LIBSORT_EXPORT int libsortSortKeysU32(const uint32_t* d_in, uint32_t* d_out, uin
              : 0;
 }
 
+LIBSORT_EXPORT int libsortSortKeysRangeU32(const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp, size_t n,
+                                           uint32_t lo, uint64_t hi, void* stream) {
+  if (hi <= (uint64_t)lo || hi > (1ull << 32)) {
+    set_error("libsortSortKeysRangeU32: need lo < hi <= 2^32");
+    return 0;
+  }
+  if (n > 0 && (!d_in || !d_out || !d_tmp || d_tmp == d_out || (const uint32_t*)d_tmp == d_in)) {
+    set_error("libsortSortKeysRangeU32: need distinct d_tmp (d_in may equal d_out)");
+    return 0;
+  }
+  // bits of the largest key - lo: keys are ordered by the low `width` bits of key - lo
+  const uint64_t span = hi - lo - 1;
+  int width = 0;
+  while (width < 32 && (span >> width) != 0) ++width;
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(sort_u32(ws, d_in, d_out, d_tmp, n, 0, width, g_digit_bits.load(), nullptr, st, lo),
+                         "libsortSortKeysRangeU32");
+         })
+             ? 1
+             : 0;
+}
+
 LIBSORT_EXPORT int libsortSortPairsU64U32(const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
                                           uint32_t* d_vout, uint64_t* d_ktmp, uint32_t* d_vtmp, size_t n,
                                           uint32_t offset, uint32_t width, void* stream) {

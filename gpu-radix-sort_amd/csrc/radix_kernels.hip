@@ -50,6 +50,28 @@ struct RadixDigit {
   }
 };
 
+// Digit of (key - bias): the keys of a range-restricted sort lie in
+// [bias, bias + 2^w) and are ordered by the low w bits of key - bias (w is
+// often a digit short of 32: the multi-GPU schedule's rounds).  A type of its
+// own so the plain sorts keep their one-instruction digit.
+struct BiasedDigit {
+  uint32_t shift;
+  uint32_t mask;
+  uint32_t bias;
+  __device__ __forceinline__ uint32_t operator()(uint32_t k) const {
+    return __builtin_amdgcn_ubfe(k - bias, shift, (uint32_t)__builtin_popcount(mask));
+  }
+  __device__ __forceinline__ uint32_t operator()(uint64_t k) const { return (uint32_t)((k - bias) >> shift) & mask; }
+};
+
+template <typename Op> Op make_digit(uint32_t shift, uint32_t mask, uint32_t bias);
+template <> inline RadixDigit make_digit<RadixDigit>(uint32_t shift, uint32_t mask, uint32_t) {
+  return RadixDigit{shift, mask};
+}
+template <> inline BiasedDigit make_digit<BiasedDigit>(uint32_t shift, uint32_t mask, uint32_t bias) {
+  return BiasedDigit{shift, mask, bias};
+}
+
 // Range partition: bucket = number of splitters <= key (splitters ascending).
 struct SplitDigit {
   uint32_t nsplit;
@@ -875,10 +897,11 @@ __device__ __forceinline__ uint32_t xcd_tile_of_block() {
 // a wave's sorted keys mostly share d and slot, so its LDS atomics spread
 // over consecutive dn banks).  The tile's row of C is zeroed after use (it
 // becomes the C_next of the pass after the next).
-template <int BITS, int BLOCK, int ITEMS, typename K, typename V, bool FUSE, typename Op = RadixDigit>
+template <int BITS, int BLOCK, int ITEMS, typename K, typename V, bool FUSE, typename Op = RadixDigit,
+          typename OpN = RadixDigit>
 __global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, K* __restrict__ kout,
                                                      const V* __restrict__ vin, V* __restrict__ vout,
-                                                     uint32_t n, Op op_in, RadixDigit op_next,
+                                                     uint32_t n, Op op_in, OpN op_next,
                                                      uint32_t* __restrict__ C, const uint32_t* __restrict__ B,
                                                      uint32_t* __restrict__ C_next) {
   constexpr bool HAS_V = !std::is_same<V, NoValue>::value;
@@ -1004,7 +1027,15 @@ __global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, 
         for (int j = 0; j < SP; ++j) {
           const uint32_t i = tid + (h * SP + j) * BLOCK;
           const uint32_t slot = i >= ob[j].y ? (uint32_t)(RADIX * RADIX) : 0u;
-          atomicAdd(&s_next[slot + op(kk[j]) * RADIX + op_next(kk[j])], 1u);
+          const uint32_t e = slot + op(kk[j]) * RADIX + op_next(kk[j]);
+          // a wave whose 64 keys share (digit, slot, next digit) -- constant
+          // high bits -- adds 64 once instead of 64 same-address LDS atomics
+          const uint32_t e0 = __builtin_amdgcn_readfirstlane(e);
+          if (__ballot(e != e0) == 0) {
+            if (lane == 0) atomicAdd(&s_next[e0], (uint32_t)kWave);
+          } else {
+            atomicAdd(&s_next[e], 1u);
+          }
         }
       }
     }
@@ -1416,25 +1447,26 @@ hipError_t tiles_colscan(Workspace& ws, uint32_t* C, uint32_t tiles, hipStream_t
 }
 
 // Sort prologue of the tile path: buffers, and (4-bit) the pass-0 counts.
-template <typename K>
-hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, int bits, hipStream_t st) {
+template <typename K, typename Op = RadixDigit>
+hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, int bits, hipStream_t st,
+                          uint32_t bias = 0) {
   const uint32_t tiles = tp_tiles<K>(n, bits);
   const uint32_t radix = 1u << bits;
   LS_TRY(ws.ensure_tiles((size_t)tiles * radix, ((size_t)tp_chunks(tiles, bits) + 1) * radix));
   if (bits != 4) return hipSuccess;
   const int nb = std::min(4, hi - lo);
-  return tiles_counts<4, K>(ws, in, n, RadixDigit{(uint32_t)lo, (1u << nb) - 1u}, tiles, ws.tc[0], ws.tc[1],
-                            tiles * 16u, st);
+  return tiles_counts<4, K, Op>(ws, in, n, make_digit<Op>((uint32_t)lo, (1u << nb) - 1u, bias), tiles, ws.tc[0],
+                                ws.tc[1], tiles * 16u, st);
 }
 
-template <int BITS, typename K, typename V>
+template <int BITS, typename K, typename V, typename Op = RadixDigit>
 hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout, size_t n, int p, int P,
-                      int lo, int hi, hipStream_t st) {
+                      int lo, int hi, hipStream_t st, uint32_t bias = 0) {
   constexpr int B = tp_block(BITS);
   const uint32_t tiles = tp_tiles<K>(n, BITS);
   const int shift = lo + BITS * p;
   const int nb = std::min(BITS, hi - shift);
-  const RadixDigit op{(uint32_t)shift, (1u << nb) - 1u};
+  const Op op = make_digit<Op>((uint32_t)shift, (1u << nb) - 1u, bias);
   // 4-bit (fused): counts of this pass were produced by the previous pass (or
   // the prologue) in tc[p & 1]; otherwise count this pass's input now.
   // LIBSORT_TP_FUSE=0 turns the fusion off (A/B measurement).
@@ -1446,18 +1478,18 @@ hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vou
   uint32_t* cur = fused_counts ? ws.tc[p & 1] : ws.tc[0];
   uint32_t* nxt = ws.tc[(p + 1) & 1];
   if (!fused_counts && !(BITS == 4 && p == 0))
-    LS_TRY((tiles_counts<BITS, K>(ws, kin, n, op, tiles, cur, nullptr, 0, st)));
+    LS_TRY((tiles_counts<BITS, K, Op>(ws, kin, n, op, tiles, cur, nullptr, 0, st)));
   LS_TRY(tiles_colscan<BITS>(ws, cur, tiles, st));
   const bool fuse = fused_counts && p + 1 < P;
   const int nb2 = fuse ? std::min(BITS, hi - shift - BITS) : 1;
-  const RadixDigit op_next{(uint32_t)(fuse ? shift + BITS : 0), (1u << nb2) - 1u};
+  const Op op_next = make_digit<Op>((uint32_t)(fuse ? shift + BITS : 0), (1u << nb2) - 1u, bias);
   ScopedTimer tm("tilepass", st, n);
   if (fuse)
-    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, BITS == 4>), dim3(tiles), dim3(B), 0, st, kin,
-                       kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, BITS == 4, Op, Op>), dim3(tiles), dim3(B), 0, st,
+                       kin, kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
   else
-    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, false>), dim3(tiles), dim3(B), 0, st, kin, kout,
-                       vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, false, Op, Op>), dim3(tiles), dim3(B), 0, st, kin,
+                       kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
   return hipGetLastError();
 }
 
@@ -1547,7 +1579,7 @@ hipError_t copy_buf(K* dst, const K* src, V* vdst, const V* vsrc, size_t n, hipS
 // LSD over bits [lo, hi) with ping-pong between out and tmp.
 template <typename K, typename V>
 hipError_t sort_impl(Workspace& ws, const K* in, K* out, K* tmp, const V* vin, V* vout, V* vtmp,
-                     size_t n, int lo, int hi, int bits, hipStream_t st) {
+                     size_t n, int lo, int hi, int bits, hipStream_t st, uint32_t bias = 0) {
   if (n == 0) return hipSuccess;
   if (n > 0xffffffffull) return hipErrorInvalidValue;
   const int width = hi - lo;
@@ -1559,20 +1591,35 @@ hipError_t sort_impl(Workspace& ws, const K* in, K* out, K* tmp, const V* vin, V
   auto dst_is_out = [&](int p) { return inplace ? (p & 1) != 0 : ((P - 1 - p) & 1) == 0; };
   const K* ksrc = in;
   const V* vsrc = vin;
-  const int algo = (bits == 4 || bits == 8) ? choose_algorithm(n, bits) : 2;
+  // a biased (range-restricted) sort always takes the tile path (onesweep's
+  // window histogram and reduce-then-scan read raw key bits)
+  constexpr bool kCanBias = std::is_same<K, uint32_t>::value && std::is_same<V, NoValue>::value;
+  if (bias && (!kCanBias || (bits != 4 && bits != 8))) return hipErrorInvalidValue;
+  const int algo = bias ? 3 : (bits == 4 || bits == 8) ? choose_algorithm(n, bits) : 2;
   const bool os = algo == 1;
   const bool tp = algo == 3;
   ws.last_algo = algo;
   const int OS_TILE = os_block() * os_items<K>();
   const uint32_t tiles = (uint32_t)((n + OS_TILE - 1) / OS_TILE);
   if (os) LS_TRY(onesweep_prologue<K>(ws, in, n, lo, hi, bits, P, tiles, st));
-  if (tp) LS_TRY(tiles_prologue<K>(ws, in, n, lo, hi, bits, st));
+  if (tp && bias) {
+    if constexpr (kCanBias) LS_TRY((tiles_prologue<K, BiasedDigit>(ws, in, n, lo, hi, bits, st, bias)));
+  } else if (tp) {
+    LS_TRY(tiles_prologue<K>(ws, in, n, lo, hi, bits, st));
+  }
   for (int p = 0; p < P; ++p) {
     const int shift = lo + p * bits;
     const int nb = std::min(bits, hi - shift);
     K* kdst = dst_is_out(p) ? out : tmp;
     V* vdst = dst_is_out(p) ? vout : vtmp;
-    if (tp) {
+    if (tp && bias) {
+      if constexpr (kCanBias) {
+        if (bits == 4)
+          LS_TRY((tiles_pass<4, K, V, BiasedDigit>(ws, ksrc, kdst, vsrc, vdst, n, p, P, lo, hi, st, bias)));
+        else
+          LS_TRY((tiles_pass<8, K, V, BiasedDigit>(ws, ksrc, kdst, vsrc, vdst, n, p, P, lo, hi, st, bias)));
+      }
+    } else if (tp) {
       if (bits == 4)
         LS_TRY((tiles_pass<4, K, V>(ws, ksrc, kdst, vsrc, vdst, n, p, P, lo, hi, st)));
       else
@@ -1595,9 +1642,10 @@ hipError_t sort_impl(Workspace& ws, const K* in, K* out, K* tmp, const V* vin, V
 }  // namespace
 
 hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n, int lo,
-                    int hi, int digit_bits, uint32_t* d_bounds, hipStream_t st) {
+                    int hi, int digit_bits, uint32_t* d_bounds, hipStream_t st, uint32_t bias) {
+  if (bias && d_bounds) return hipErrorInvalidValue;
   LS_TRY((sort_impl<uint32_t, NoValue>(ws, in, out, tmp, nullptr, nullptr, nullptr, n, lo, hi,
-                                      digit_bits, st)));
+                                      digit_bits, st, bias)));
   if (d_bounds) {
     const int width = hi - lo;
     const uint32_t ngroups = 1u << width;

@@ -41,6 +41,8 @@ _SIGS = [
     ("gpuPartialSort", ctypes.c_int, [_vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32]),
     ("libsortSortKeysU32", ctypes.c_int,
      [_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
+    ("libsortSortKeysRangeU32", ctypes.c_int,
+     [_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, _vp]),
     ("libsortSortPairsU64U32", ctypes.c_int,
      [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     ("libsortSortPairsU32U32", ctypes.c_int,

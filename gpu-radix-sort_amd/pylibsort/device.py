@@ -65,6 +65,19 @@ def sort_keys_u32(keys, out=None, tmp=None, offset=0, width=None, boundaries=Non
     return out
 
 
+def sort_keys_range_u32(keys, lo, hi, out=None, tmp=None):
+    """Full sort of uint32 keys known to lie in [lo, hi): digits of key - lo,
+    so fewer passes when the range is narrow."""
+    _need(keys, _U32, "keys")
+    out = torch.empty_like(keys) if out is None else out
+    tmp = torch.empty_like(keys) if tmp is None else tmp
+    _need(out, _U32, "out")
+    _need(tmp, _U32, "tmp")
+    _check(_lib().libsortSortKeysRangeU32(_ptr(keys), _ptr(out), _ptr(tmp), keys.numel(), int(lo), int(hi),
+                                          _stream()), "libsortSortKeysRangeU32")
+    return out
+
+
 def sort_pairs_u64_u32(keys, vals, out_keys=None, out_vals=None, tmp_keys=None, tmp_vals=None,
                        offset=0, width=None):
     """Stable sort of (uint64 key, uint32 payload) pairs by key bits."""

@@ -73,6 +73,11 @@ class HipOps:
     def histogram(self, keys, shift, bits):
         return self.D.histogram_u32(keys, shift, bits)
 
+    def sort_range(self, keys, lo, hi, out=None):
+        """Full sort of keys known to lie in [lo, hi) (fewer passes)."""
+        out = self.empty(keys.numel()) if out is None else out
+        return self.D.sort_keys_range_u32(keys, lo, hi, out=out, tmp=self._scratch(keys.numel()))
+
     def partition(self, keys, splitters, out=None):
         out = self.empty(keys.numel()) if out is None else out
         return self.D.partition_u32(keys, splitters, out=out)[0]
@@ -237,22 +242,37 @@ def plan_msd(H, R, hist_bits=HIST_BITS):
     return splitters, dest, n_recv
 
 
-def plan_rounds(H, R, K, hist_bits=HIST_BITS):
+def plan_rounds(H, R, K, hist_bits=HIST_BITS, growth=1.6):
     """Contiguous top-bit bucket ranges for (rank, round) from the gathered
-    (possibly sampled) histograms H[R, 2^b]: R*K groups of about equal
-    estimated count, group g -> rank g // K, round g % K.  Returns (lut,
-    est_per_rank) with lut[b] = round * R + rank (the partition bucket)."""
+    (possibly sampled) histograms H[R, 2^b]: each rank gets about 1/R of the
+    estimated keys, split into K rounds whose sizes grow by `growth` (a small
+    first round keeps the exchange before the first sort short; each later
+    round's exchange hides behind the previous round's sort).  Group of a
+    bucket: rank g // K, round g % K.  Returns (lut, est_per_rank) with lut[b]
+    = round * R + rank (the partition bucket)."""
     G = H.sum(axis=0).astype(np.float64)
     T = float(G.sum())
     if T > 0:
-        mid = np.cumsum(G) - G / 2.0
-        grp = np.minimum((mid * (R * K) / T).astype(np.int64), R * K - 1)
-        grp = np.maximum.accumulate(grp)
+        x = (np.cumsum(G) - G / 2.0) / T * R                  # rank coordinate of each bucket's middle
+        rank = np.minimum(x.astype(np.int64), R - 1)
+        w = growth ** np.arange(K)
+        cw = np.cumsum(w) / w.sum()
+        rnd = np.minimum(np.searchsorted(cw, x - rank, side="right"), K - 1)
+        grp = np.maximum.accumulate(rank * K + rnd)
     else:
         grp = np.zeros(G.size, dtype=np.int64)
     rank, rnd = grp // K, grp % K
     lut = (rnd * R + rank).astype(np.uint8)
     return lut, np.bincount(rank, weights=G, minlength=R)
+
+
+def _group_range(lut, code, hist_bits=HIST_BITS):
+    """[lo, hi) key range of the contiguous buckets with lut == code (None if empty)."""
+    idx = np.nonzero(lut == code)[0]
+    if idx.size == 0:
+        return None
+    shift = 32 - hist_bits
+    return int(idx[0]) << shift, (int(idx[-1]) + 1) << shift
 
 
 def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=4, sample_stride=16):
@@ -292,7 +312,8 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=4, s
         if works[i] is not None:
             works[i].wait()                                    # stream-level: the sort waits on RCCL
         if recv_tot[i]:
-            ops.sort(recv[int(roff[i]):int(roff[i + 1])], out=out[int(roff[i]):int(roff[i + 1])])
+            lo, hi = _group_range(lut, i * R + r)              # every key of the round lies in it
+            ops.sort_range(recv[int(roff[i]):int(roff[i + 1])], lo, hi, out=out[int(roff[i]):int(roff[i + 1])])
     if not balance:
         return out
     n_recv = np.array([int(C[:, d::R].sum()) for d in range(R)], dtype=np.int64)

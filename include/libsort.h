@@ -86,6 +86,14 @@ LIBSORT_API bool libsortSortKeysU32(const uint32_t* d_in, uint32_t* d_out, uint3
                                     size_t n, uint32_t offset, uint32_t width,
                                     uint32_t* d_boundaries, void* stream);
 
+/* Full sort of keys known to lie in [lo, hi) (lo < hi <= 2^32): the digits
+ * are taken from key - lo, so ceil(log2(hi - lo) / digit bits) passes instead
+ * of 32 / digit bits (a round of the multi-GPU schedule spans about 2^27
+ * key values: 7 four-bit passes instead of 8).  Keys outside [lo, hi) give an
+ * unspecified order (no fault).  Same buffers as libsortSortKeysU32. */
+LIBSORT_API bool libsortSortKeysRangeU32(const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp,
+                                         size_t n, uint32_t lo, uint64_t hi, void* stream);
+
 /* Stable key-value sort: 64-bit keys, 32-bit payloads (BASELINE config C5). */
 LIBSORT_API bool libsortSortPairsU64U32(const uint64_t* d_kin, const uint32_t* d_vin,
                                         uint64_t* d_kout, uint32_t* d_vout,

@@ -73,18 +73,22 @@ def test_msd_sparse_key_ranges_gloo(tmp_path):
 
 
 def test_plan_rounds_contiguous_and_balanced():
-    from pylibsort.distrib import plan_rounds
+    from pylibsort.distrib import plan_rounds, _group_range
     rng = np.random.default_rng(4)
     R, K = 8, 4
     H = np.stack([np.bincount(rng.integers(0, 4096, 200000), minlength=4096) for _ in range(R)])
-    lut, est = plan_rounds(H, R, K)
+    lut, est = plan_rounds(H, R, K, growth=1.6)
     grp = (lut % R) * K + lut // R                 # back to key-order group index
     assert lut.dtype == np.uint8 and lut.size == 4096
     assert np.all(np.diff(grp.astype(np.int64)) >= 0) and grp[0] == 0 and grp[-1] == R * K - 1
-    tot = H.sum()
-    g = np.bincount(grp, weights=H.sum(axis=0), minlength=R * K)
-    assert g.max() <= tot / (R * K) + H.sum(axis=0).max() + 1
-    assert abs(est.sum() - tot) < 1e-6 and est.max() <= tot / R * 1.01 + H.sum(axis=0).max()
+    tot, bmax = H.sum(), H.sum(axis=0).max()
+    assert abs(est.sum() - tot) < 1e-6 and np.all(np.abs(est - tot / R) <= bmax + 1)   # ranks balanced
+    g = np.bincount(grp, weights=H.sum(axis=0), minlength=R * K).reshape(R, K)
+    w = 1.6 ** np.arange(K)
+    np.testing.assert_allclose(g / g.sum(axis=1, keepdims=True), np.tile(w / w.sum(), (R, 1)), atol=0.02)
+    lo, hi = _group_range(lut, 0 * R + 0)          # first round of rank 0 starts at key 0
+    assert lo == 0 and hi > 0
+    assert _group_range(lut, (K - 1) * R + R - 1)[1] == 1 << 32
     lut0, est0 = plan_rounds(np.zeros((R, 4096)), R, K)
     assert not lut0.any() and not est0.any()
 

@@ -126,6 +126,18 @@ def test_edge_distributions(dev, oracle_mod, digit_bits, kind):
     np.testing.assert_array_equal(_u32(b), bb)
 
 
+@pytest.mark.parametrize("lo,hi", [(0, 1 << 32), (0, 1 << 27), (0x12300000, 0x12300000 + (1 << 27)),
+                                   (0xF0000000, 1 << 32), (0x80000001, 0x80000001 + 3000), (777, 778)])
+@pytest.mark.parametrize("n", [1, 4097, 300001])
+def test_sort_keys_range(dev, oracle_mod, digit_bits, lo, hi, n):
+    """libsortSortKeysRangeU32 (digits of key - lo, ceil(log2(hi - lo) / bits)
+    passes) == a full sort, for keys inside [lo, hi)."""
+    x = oracle_mod.pcg(n, first=lo % 1000 + n)
+    x = (np.uint64(lo) + x.astype(np.uint64) % np.uint64(hi - lo)).astype(np.uint32)
+    got = dev.sort_keys_range_u32(_tensor(x), lo, hi)
+    np.testing.assert_array_equal(_u32(got), np.sort(x))
+
+
 def test_in_place_device_sort(dev, oracle_mod, digit_bits):
     x = oracle_mod.pcg(77777, first=5)
     t = _tensor(x)

@@ -58,6 +58,16 @@ def main():
             for i in range(K):
                 D.sort_keys_u32(keys[i * m:(i + 1) * m], out=out[i * m:(i + 1) * m], tmp=tmp[:m])
         res["sort_%d_rounds_ms" % K] = timed(rounds, reps=5)
+    lo = 1 << 28                             # a round's range at R*K = 32: [lo, lo + 2^27)
+    narrow = ((keys >> 5) & ((1 << 27) - 1)) + lo
+    for K in (1, 4, 8):
+        m = n // K
+
+        def rounds_range():
+            for i in range(K):
+                D.sort_keys_range_u32(narrow[i * m:(i + 1) * m], lo, lo + (1 << 27), out=out[i * m:(i + 1) * m],
+                                      tmp=tmp[:m])
+        res["range27_sort_%d_rounds_ms" % K] = timed(rounds_range, reps=5)
     print({k: round(v, 3) for k, v in res.items()})
 
 
