@@ -1,16 +1,22 @@
 #!/usr/bin/env python3
 """Benchmark: uint32 full sort, keys resident in HBM (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c5]
 
-N=1  : configs[1] = "256M uint32, 4-bit digits, gpuFullSort on 1 MI355X":
-       2^28 keys of the reference populateInput stream (generated on the GPU by
-       skip-ahead), one step = one full 32-bit LSD sort through the libsort C
-       ABI (libsortSortKeysU32 = the device-resident form of providedGpu).
-N>1  : launched by torch.distributed.run, one rank per GPU; rank r holds keys
-       [r*2^28, (r+1)*2^28) of the same stream (weak scaling); one step = one
-       distributed sort (pylibsort.distrib, "msd" schedule: one RCCL alltoallv)
-       ending with rank r holding keys [r*S, (r+1)*S) of the sorted array.
+c2 (default; the bench line): configs[1] = "256M uint32, 4-bit digits,
+    gpuFullSort on 1 MI355X": 2^28 keys of the reference populateInput stream
+    per GPU (generated on the GPU by skip-ahead), one step = one full 32-bit
+    LSD sort through the libsort C ABI (libsortSortKeysU32 = the
+    device-resident form of providedGpu).
+    N>1: launched by torch.distributed.run, one rank per GPU; rank r holds keys
+    [r*2^28, (r+1)*2^28) of the same stream (weak scaling); one step = one
+    distributed sort (pylibsort.distrib, "msd" schedule: one table partition,
+    range-split RCCL alltoallv rounds overlapped with the per-round sorts)
+    ending with rank r holding keys [r*S, (r+1)*S) of the sorted array.
+c3: configs[2], 2^30 keys, 8-bit digits, one GPU.
+c5: configs[4], stable (u64 key, u32 payload) sort, 2^28 pairs per GPU (2^31
+    on 8 GPUs); key = (draw 2i << 32) | draw 2i+1 of the stream, payload = the
+    global index; N>1 runs pylibsort.distrib.distrib_sort_pairs.
 
 Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 """
@@ -34,23 +40,28 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--keys-log2", type=int, default=28, help="keys per GPU = 2^k")
-    ap.add_argument("--digit-bits", type=int, default=4, help="configs[1] names 4-bit digits")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"])
+    ap.add_argument("--keys-log2", type=int, default=None, help="keys (pairs) per GPU = 2^k")
+    ap.add_argument("--digit-bits", type=int, default=None, help="configs[1] names 4-bit digits")
     ap.add_argument("--schedule", default="msd", choices=["msd", "lsd"])
+    ap.add_argument("--rounds", type=int, default=4, help="msd exchange rounds")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=26)
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--algo", default=None, choices=["auto", "tiles", "onesweep", "rts"],
                     help="force the pass algorithm (LIBSORT_ALGO)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    defaults = {"c2": (28, 4), "c3": (30, 8), "c5": (28, 8)}[a.workload]
+    a.keys_log2 = defaults[0] if a.keys_log2 is None else a.keys_log2
+    a.digit_bits = defaults[1] if a.digit_bits is None else a.digit_bits
+    return a
 
 
 def main():
     args = parse()
     if args.algo:
         os.environ["LIBSORT_ALGO"] = args.algo
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -60,6 +71,8 @@ def main():
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         if world == 1:
             raise SystemExit("--gpus %d needs torch.distributed.run with %d processes" % (args.gpus, args.gpus))
+    if args.workload == "c3" and world > 1:
+        raise SystemExit("c3 is a single-GPU configuration")
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -71,17 +84,33 @@ def main():
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
     pylibsort.setDigitBits(args.digit_bits)
+    pairs = args.workload == "c5"
 
     n = 1 << args.keys_log2
-    keys = D.populate_u32(n, first=rank * n)
+    vals = None
+    if pairs:
+        w = D.populate_u32(2 * n, first=rank * 2 * n).view(n, 2).to(torch.int64)
+        keys = (w[:, 0] << 32) | (w[:, 1] & 0xFFFFFFFF)
+        vals = torch.arange(rank * n, (rank + 1) * n, dtype=torch.int64, device="cuda").to(torch.int32)
+        del w
+        out, outv = torch.empty_like(keys), torch.empty_like(vals)
+        tmp, tmpv = torch.empty_like(keys), torch.empty_like(vals)
+    else:
+        keys = D.populate_u32(n, first=rank * n)
+        out = torch.empty_like(keys)
+        tmp = torch.empty_like(keys)
     torch.cuda.synchronize()
-    out = torch.empty_like(keys)
-    tmp = torch.empty_like(keys)
     ops = distrib.HipOps() if world > 1 else None
 
     def step():
+        if pairs:
+            if world == 1:
+                return D.sort_pairs_u64_u32(keys, vals, out_keys=out, out_vals=outv, tmp_keys=tmp, tmp_vals=tmpv)
+            return distrib.distrib_sort_pairs(keys, vals, ops=ops, rounds=args.rounds)
         if world == 1:
             return D.sort_keys_u32(keys, out=out, tmp=tmp)
+        if args.schedule == "msd":
+            return distrib.distrib_sort(keys, ops=ops, schedule="msd", rounds=args.rounds)
         return distrib.distrib_sort(keys, ops=ops, schedule=args.schedule)
 
     def barrier():
@@ -112,7 +141,8 @@ def main():
 
     # live per-kernel durations (hipEvents on libsort's launch stream)
     kern = {}
-    for name in ("whist", "onesweep", "upsweep", "scan", "downsweep", "tilecounts", "colscan", "tilepass", "histogram", "segcopy"):
+    for name in ("whist", "onesweep", "upsweep", "scan", "downsweep", "tilecounts", "colscan", "tilepass",
+                 "partition", "histogram", "segcopy"):
         launches, ms, kk = D.timing_query(name)
         if launches:
             kern[name] = {"launches": launches, "avg_us": 1e3 * ms / launches, "keys_per_launch": kk / launches}
@@ -120,39 +150,23 @@ def main():
     # verification outside the timed region: sorted + same multiset (checksums)
     verified = None
     if not args.no_verify:
-        r64 = res.to(torch.int64) & 0xFFFFFFFF
-        ok = bool((r64[1:] >= r64[:-1]).all().item()) if r64.numel() > 1 else True
-        k64 = keys.to(torch.int64) & 0xFFFFFFFF
-        sums = torch.stack([k64.sum(), (k64 * k64 % 1000000007).sum(), torch.tensor(k64.numel(), device=k64.device)])
-        rs = torch.stack([r64.sum(), (r64 * r64 % 1000000007).sum(), torch.tensor(r64.numel(), device=r64.device)])
-        lo_hi = torch.stack([r64[0], r64[-1]]) if r64.numel() else torch.zeros(2, dtype=torch.int64, device="cuda")
-        if world > 1:
-            dist.all_reduce(sums)
-            dist.all_reduce(rs)
-            # boundaries between neighbouring shards
-            allb = [torch.empty_like(lo_hi) for _ in range(world)]
-            dist.all_gather(allb, lo_hi)
-            edges = all(int(allb[i][1]) <= int(allb[i + 1][0]) for i in range(world - 1))
-            okt = torch.tensor([1 if ok else 0], device="cuda")
-            dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-            ok = bool(okt.item()) and edges
-        verified = ok and bool(torch.equal(sums, rs))
+        verified = verify(torch, dist, world, keys, res, vals)
 
     total_keys = n * world
     ms_per_step = 1e3 * elapsed / args.steps
     value = total_keys / (elapsed / args.steps) / 1e9
 
-    line = None
     if rank == 0:
         ds_name = next((k for k in ("tilepass", "onesweep", "downsweep") if k in kern), "downsweep")
         ds = kern.get(ds_name)
+        unit_bytes = 24.0 if pairs else 8.0  # read + write of one key (pair)
         roofline = None
         if ds:
-            bytes_per_launch = 8.0 * ds["keys_per_launch"]  # read 4 B + write 4 B per key
+            bytes_per_launch = unit_bytes * ds["keys_per_launch"]
             achieved = bytes_per_launch / (ds["avg_us"] * 1e-6) / 1e9
             traffic = None
             pmc = ROOT / "profiles" / ("pmc_%s.json" % ds_name)
-            if pmc.exists():
+            if pmc.exists() and args.workload == "c2":
                 try:
                     traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
                 except Exception:
@@ -162,7 +176,7 @@ def main():
                         "kernel": "k_%s (rank + scatter pass)" % ds_name, "algorithmic_bytes_per_launch": bytes_per_launch,
                         "avg_launch_us": round(ds["avg_us"], 2)}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not pairs:
             from oracle import oracle  # CPU baseline leg only (the checker's std::sort)
             m = 1 << args.cpu_sample_log2
             x = oracle.pcg(m)
@@ -173,7 +187,7 @@ def main():
                    "sample": "std::sort (providedCpu, invokers.cu:68-71) of the first 2^%d populateInput keys, "
                              "1 thread, %.2f s" % (args.cpu_sample_log2, c1 - c0)}
         variants = {}
-        if world == 1 and not args.no_variants:
+        if world == 1 and not args.no_variants and args.workload == "c2":
             ref_out = out.clone()
             prev = pylibsort.setDigitBits(8)
             for _ in range(2):
@@ -192,10 +206,22 @@ def main():
             variants["digit8"] = {"ms_per_step": round(ms8, 4), "value": round(n / (ms8 * 1e-3) / 1e9, 3),
                                   "note": "same sort with 8-bit digits (4 passes, configs[2] digit width); output "
                                           "checked equal to the 4-bit sort"}
+        sched = ""
+        if world > 1:
+            sched = (", msd schedule, %d rounds, over %d GPUs (RCCL alltoallv)" % (args.rounds, world)
+                     if pairs or args.schedule == "msd" else ", lsd schedule over %d GPUs (RCCL alltoallv)" % world)
+        if pairs:
+            metric, unit, dtype = "Gpairs/sec (u64 key, u32 payload) stable sort", "Gpairs/s", "u64+u32"
+            workload = "configs[4]: 2^%d (u64 key, u32 payload) pairs per GPU, %d-bit digits, stable sort%s" % (
+                args.keys_log2, args.digit_bits, sched)
+        else:
+            metric, unit, dtype = "Gkeys/sec uint32 full sort", "Gkeys/s", "u32"
+            workload = "configs[%d]: 2^%d uint32 keys per GPU, %d-bit digits, full sort%s" % (
+                1 if args.workload == "c2" else 2, args.keys_log2, args.digit_bits, sched)
         line = {
-            "metric": "Gkeys/sec uint32 full sort",
+            "metric": metric,
             "value": round(value, 3),
-            "unit": "Gkeys/s",
+            "unit": unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -203,13 +229,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u32",
+            "dtype": dtype,
             "data": "synthetic: reference populateInput PCG32 stream, generated on device",
-            "config": {"workload": "configs[1]: 2^%d uint32 keys per GPU, %d-bit digits, full sort%s"
-                       % (args.keys_log2, args.digit_bits,
-                          "" if world == 1 else ", %s schedule over %d GPUs (RCCL alltoallv)" % (args.schedule, world)),
-                       "keys_per_gpu": n, "digit_bits": args.digit_bits, "global_keys": total_keys,
-                       "parallelism": "shards%d" % world},
+            "config": {"workload": workload, "keys_per_gpu": n, "digit_bits": args.digit_bits,
+                       "global_keys": total_keys, "parallelism": "shards%d" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "kernels": kern,
@@ -220,6 +243,57 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def verify(torch, dist, world, keys, res, vals=None):
+    """Sorted (unsigned order) on every rank and across shard edges, same
+    multiset as the input (checksums); pairs: payloads increase within equal
+    keys (stability; payload = global input index) and move with their keys."""
+    if vals is None:
+        r = res.to(torch.int64) & 0xFFFFFFFF
+        k = keys.to(torch.int64) & 0xFFFFFFFF
+        ok = bool((r[1:] >= r[:-1]).all().item()) if r.numel() > 1 else True
+        sums = torch.stack([k.sum(), (k * k % 1000000007).sum(), torch.tensor(k.numel(), device=k.device)])
+        rs = torch.stack([r.sum(), (r * r % 1000000007).sum(), torch.tensor(r.numel(), device=r.device)])
+        z = torch.zeros(2, dtype=torch.int64, device="cuda")
+        lo_hi = torch.stack([r[0], r[-1]]) if r.numel() else z
+        first_last = lo_hi
+    else:
+        rk, rv = res
+        flip = torch.tensor(-(1 << 63), dtype=torch.int64, device=rk.device)
+        s = torch.bitwise_xor(rk, flip)                       # uint64 order -> int64 order
+        v = rv.to(torch.int64) & 0xFFFFFFFF
+        ok = True
+        if s.numel() > 1:
+            ok = bool((s[1:] >= s[:-1]).all().item())
+            eq = s[1:] == s[:-1]
+            ok = ok and bool((v[1:][eq] > v[:-1][eq]).all().item())
+
+        def mix(kk, vv):  # keys and payloads moved together
+            return ((kk & 0xFFFFFF) * 1000003 + (kk >> 40) * 7 + vv) % 1000000007
+        v0 = vals.to(torch.int64) & 0xFFFFFFFF
+        sums = torch.stack([mix(keys, v0).sum(), v0.sum(), torch.tensor(keys.numel(), device=keys.device)])
+        rs = torch.stack([mix(rk, v).sum(), v.sum(), torch.tensor(rk.numel(), device=rk.device)])
+        z = torch.zeros(2, dtype=torch.int64, device="cuda")
+        lo_hi = torch.stack([s[0], s[-1]]) if s.numel() else z
+        first_last = torch.stack([v[0], v[-1]]) if v.numel() else z
+    if world > 1:
+        dist.all_reduce(sums)
+        dist.all_reduce(rs)
+        edge = torch.stack([lo_hi, first_last])
+        allb = [torch.empty_like(edge) for _ in range(world)]
+        dist.all_gather(allb, edge)
+        edges = True
+        for i in range(world - 1):
+            a_hi, b_lo = int(allb[i][0][1]), int(allb[i + 1][0][0])
+            if vals is None:
+                edges = edges and a_hi <= b_lo
+            else:  # key order, and payload order between equal keys across the shard edge
+                edges = edges and (a_hi < b_lo or (a_hi == b_lo and int(allb[i][1][1]) < int(allb[i + 1][1][0])))
+        okt = torch.tensor([1 if ok else 0], device="cuda")
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item()) and edges
+    return ok and bool(torch.equal(sums, rs))
 
 
 if __name__ == "__main__":

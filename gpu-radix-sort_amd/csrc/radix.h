@@ -133,6 +133,10 @@ hipError_t partition_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_
 // be null) receives the nbuckets bucket starts.
 hipError_t partition_lut_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, const uint8_t* d_lut,
                              int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t stream);
+// The same for (u64 key, u32 value) pairs; bucket = lut[(key >> 32) >> lut_shift].
+hipError_t partition_lut_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
+                                       uint32_t* vout, size_t n, const uint8_t* d_lut, int lut_shift, int nbuckets,
+                                       uint32_t* d_bounds, hipStream_t stream);
 hipError_t segment_copy_u32(Workspace& ws, const uint32_t* src, uint32_t* dst, size_t nseg,
                             const uint64_t* src_off, const uint64_t* dst_off, const uint64_t* len,
                             hipStream_t stream);

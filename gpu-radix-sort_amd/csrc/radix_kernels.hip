@@ -1749,39 +1749,56 @@ hipError_t partition_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_
 namespace {
 // One tile-offset pass whose digit is a table lookup: per-tile counts, column
 // scan, pass kernel; bucket starts = row 0 of the scanned chunk totals.
-template <int BITS>
-hipError_t partition_lut_impl(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, const uint8_t* d_lut,
-                              int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st) {
+// u64 keys: the table indexes the top bits of the key's high word.
+template <int BITS, typename K, typename V>
+hipError_t partition_lut_impl(Workspace& ws, const K* in, K* out, const V* vin, V* vout, size_t n,
+                              const uint8_t* d_lut, int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st) {
   constexpr int RADIX = 1 << BITS;
   constexpr int B = tp_block(BITS);
-  const uint32_t tiles = tp_tiles<uint32_t>(n, BITS);
+  const uint32_t tiles = tp_tiles<K>(n, BITS);
   LS_TRY(ws.ensure_tiles((size_t)tiles * RADIX, ((size_t)tp_chunks(tiles, BITS) + 1) * RADIX));
   const LutDigit op{d_lut, (uint32_t)lut_shift, (uint32_t)RADIX - 1u, nullptr};
-  LS_TRY((tiles_counts<BITS, uint32_t, LutDigit>(ws, in, n, op, tiles, ws.tc[0], nullptr, 0, st)));
+  LS_TRY((tiles_counts<BITS, K, LutDigit>(ws, in, n, op, tiles, ws.tc[0], nullptr, 0, st)));
   LS_TRY(tiles_colscan<BITS>(ws, ws.tc[0], tiles, st));
   {
     ScopedTimer tm("partition", st, n);
-    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<uint32_t>(), uint32_t, NoValue, false, LutDigit>), dim3(tiles),
-                       dim3(B), 0, st, in, out, (const NoValue*)nullptr, (NoValue*)nullptr, (uint32_t)n, op,
-                       RadixDigit{0u, 1u}, ws.tc[0], (const uint32_t*)ws.tb, ws.tc[1]);
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, false, LutDigit>), dim3(tiles), dim3(B), 0, st, in,
+                       out, vin, vout, (uint32_t)n, op, RadixDigit{0u, 1u}, ws.tc[0], (const uint32_t*)ws.tb, ws.tc[1]);
     LS_TRY(hipGetLastError());
   }
   if (d_bounds) LS_TRY(hipMemcpyAsync(d_bounds, ws.tb, (size_t)nbuckets * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   return hipSuccess;
 }
-}  // namespace
 
-hipError_t partition_lut_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, const uint8_t* d_lut,
-                             int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st) {
+template <typename K, typename V>
+hipError_t partition_lut_any(Workspace& ws, const K* in, K* out, const V* vin, V* vout, size_t n,
+                             const uint8_t* d_lut, int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st) {
   if (n > 0xffffffffull || lut_shift < 20 || lut_shift > 30 || nbuckets < 1 || nbuckets > 256)
     return hipErrorInvalidValue;
   if (n == 0) {
     if (d_bounds) LS_TRY(hipMemsetAsync(d_bounds, 0, (size_t)nbuckets * sizeof(uint32_t), st));
     return hipSuccess;
   }
-  if (!in || !out || !d_lut || in == out || (reinterpret_cast<uintptr_t>(d_lut) & 3u)) return hipErrorInvalidValue;
-  if (nbuckets <= 16) return partition_lut_impl<4>(ws, in, out, n, d_lut, lut_shift, nbuckets, d_bounds, st);
-  return partition_lut_impl<8>(ws, in, out, n, d_lut, lut_shift, nbuckets, d_bounds, st);
+  if (!in || !out || !d_lut || (const void*)in == (const void*)out || (reinterpret_cast<uintptr_t>(d_lut) & 3u))
+    return hipErrorInvalidValue;
+  if constexpr (!std::is_same<V, NoValue>::value) {
+    if (!vin || !vout || (const void*)vin == (const void*)vout) return hipErrorInvalidValue;
+  }
+  if (nbuckets <= 16) return partition_lut_impl<4, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st);
+  return partition_lut_impl<8, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st);
+}
+}  // namespace
+
+hipError_t partition_lut_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, const uint8_t* d_lut,
+                             int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st) {
+  return partition_lut_any<uint32_t, NoValue>(ws, in, out, nullptr, nullptr, n, d_lut, lut_shift, nbuckets, d_bounds,
+                                              st);
+}
+
+hipError_t partition_lut_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
+                                       uint32_t* vout, size_t n, const uint8_t* d_lut, int lut_shift, int nbuckets,
+                                       uint32_t* d_bounds, hipStream_t st) {
+  return partition_lut_any<uint64_t, uint32_t>(ws, kin, kout, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st);
 }
 
 hipError_t segment_copy_u32(Workspace& ws, const uint32_t* src, uint32_t* dst, size_t nseg,

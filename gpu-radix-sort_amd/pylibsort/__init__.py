@@ -53,6 +53,8 @@ _SIGS = [
      [_vp, _vp, ctypes.c_size_t, _u32p, ctypes.c_uint32, _vp, _vp]),
     ("libsortPartitionLutU32", ctypes.c_int,
      [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
+    ("libsortPartitionLutU64U32", ctypes.c_int,
+     [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
     ("libsortSegmentCopyU32", ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _u64p, _u64p, _u64p, _vp]),
     ("libsortPopulateDevice", ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_uint64, _vp]),
     ("libsortSetDigitBits", ctypes.c_int, [ctypes.c_int]),

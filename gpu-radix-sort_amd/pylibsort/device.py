@@ -154,6 +154,26 @@ def partition_lut_u32(keys, lut, lut_shift, nbuckets, out=None, bounds=None):
     return out, bounds
 
 
+def partition_lut_pairs_u64_u32(keys, vals, lut, lut_shift, nbuckets, out_keys=None, out_vals=None,
+                                bounds=None):
+    """Stable partition of (uint64 key, uint32 payload) pairs by bucket =
+    lut[(key >> 32) >> lut_shift].  Returns (out_keys, out_vals, bounds)."""
+    _need(keys, _U64, "keys")
+    _need(vals, _U32, "vals")
+    if keys.numel() != vals.numel():
+        raise ValueError("keys and vals differ in length")
+    if lut.dtype != torch.uint8 or not lut.is_cuda or lut.numel() != 1 << (32 - lut_shift):
+        raise ValueError("lut must be a uint8 CUDA tensor of 2**(32 - lut_shift) entries")
+    lut = lut.contiguous()
+    ok_ = torch.empty_like(keys) if out_keys is None else out_keys
+    ov = torch.empty_like(vals) if out_vals is None else out_vals
+    bounds = torch.empty(nbuckets, dtype=torch.int32, device=keys.device) if bounds is None else bounds
+    _check(_lib().libsortPartitionLutU64U32(_ptr(keys), _ptr(vals), _ptr(ok_), _ptr(ov), keys.numel(), _ptr(lut),
+                                            lut_shift, nbuckets, _ptr(bounds), _stream()),
+           "libsortPartitionLutU64U32")
+    return ok_, ov, bounds
+
+
 def segment_copy_u32(src, dst, src_off, dst_off, lens):
     """dst[dst_off[i] + j] = src[src_off[i] + j] for j < lens[i]."""
     _need(src, _U32, "src")

@@ -52,6 +52,14 @@ class HipOps:
     def empty(self, n):
         return torch.empty(n, dtype=torch.int32, device=self.device)
 
+    def empty64(self, n):
+        return torch.empty(n, dtype=torch.int64, device=self.device)
+
+    def _scratch64(self, n):
+        if getattr(self, "_tmp64", None) is None or self._tmp64.numel() < n:
+            self._tmp64 = torch.empty(max(n, 1), dtype=torch.int64, device=self.device)
+        return self._tmp64[:n]
+
     def _scratch(self, n):
         if self._tmp is None or self._tmp.numel() < n:
             self._tmp = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
@@ -78,9 +86,29 @@ class HipOps:
         out = self.empty(keys.numel()) if out is None else out
         return self.D.sort_keys_range_u32(keys, lo, hi, out=out, tmp=self._scratch(keys.numel()))
 
+    def sort_pairs(self, keys, vals, out_keys=None, out_vals=None):
+        """Stable sort of (uint64 key, uint32 payload) pairs."""
+        n = keys.numel()
+        ok_ = self.empty64(n) if out_keys is None else out_keys
+        ov = self.empty(n) if out_vals is None else out_vals
+        return self.D.sort_pairs_u64_u32(keys, vals, out_keys=ok_, out_vals=ov, tmp_keys=self._scratch64(n),
+                                         tmp_vals=self._scratch(n))
+
     def partition(self, keys, splitters, out=None):
         out = self.empty(keys.numel()) if out is None else out
         return self.D.partition_u32(keys, splitters, out=out)[0]
+
+    def partition_lut_pairs(self, keys, vals, lut, shift, nbuckets):
+        """(keys, payloads, bucket starts as host int64) of the stable pair partition."""
+        t = torch.from_numpy(np.ascontiguousarray(lut, dtype=np.uint8)).to(self.device)
+        n = keys.numel()
+        k, v, b = self.D.partition_lut_pairs_u64_u32(keys, vals, t, shift, nbuckets, out_keys=self.empty64(n),
+                                                      out_vals=self.empty(n))
+        return k, v, b.cpu().numpy().view(np.uint32).astype(np.int64)
+
+    def sample_hi(self, keys, stride, block=4096):
+        """High 32-bit words of a block sample of uint64 keys (little endian)."""
+        return self.sample(keys, stride, block).view(torch.int32)[1::2].contiguous()
 
     def partition_lut(self, keys, lut, shift, nbuckets):
         """(partitioned keys, bucket starts as host int64 numpy array)."""
@@ -320,6 +348,73 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=4, s
     return _rebalance(out, n_recv, ops, group)
 
 
+def _rebalance_pairs(keys, vals, n_all, ops, group):
+    """_rebalance for (key, payload) pairs: both arrays take the same splits."""
+    R = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    N = int(n_all.sum())
+    S, _ = shard_cut(N, R)
+    offs = np.concatenate([[0], np.cumsum(n_all)[:-1]])
+    M = np.stack([_interval_counts(np.array([offs[s]]), np.array([n_all[s]]), S, R) for s in range(R)])
+    if np.array_equal(np.diag(M), n_all):
+        return keys, vals
+    rk = ops.empty64(int(M[:, r].sum()))
+    rv = ops.empty(int(M[:, r].sum()))
+    _alltoallv_into(rk, keys, M[r], M[:, r], group)
+    _alltoallv_into(rv, vals, M[r], M[:, r], group)
+    return rk, rv
+
+
+def distrib_sort_pairs(keys, vals, ops=None, group=None, rounds=4, sample_stride=16):
+    """Stable sort of the distributed (uint64 key, uint32 payload) array whose
+    rank-r shard is (keys, vals) -- SURVEY C5.  The "msd" range-split rounds of
+    sort_msd on the top 12 bits of the key: one stable pair partition
+    (libsortPartitionLutU64U32), per round an alltoallv of the keys and one of
+    the payloads (issued up front, RCCL runs them back to back), a stable local
+    pair sort of each round as it arrives, then the equal re-cut.  Equal keys
+    keep their original global order: the partition and the local sort are
+    stable and a round's data arrive in source-rank order.  There is no
+    skew fallback: a heavy key range concentrates work on one rank, the result
+    stays exact.  Returns this rank's (keys, vals) shard, ceil(N/R) pairs."""
+    ops = HipOps() if ops is None else ops
+    R = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    if R == 1:
+        return ops.sort_pairs(keys, vals)
+    K = max(1, min(int(rounds), 256 // R))
+    n = keys.numel()
+    h = ops.histogram(ops.sample_hi(keys, sample_stride), 32 - HIST_BITS, HIST_BITS)
+    HN = _allgather_np(np.concatenate([h.cpu().numpy().astype(np.int64), [n]]), keys, group)
+    H = HN[:, :-1]
+    lut, _ = plan_rounds(H, R, K)
+    NB = R * K
+    pk, pv, b = ops.partition_lut_pairs(keys, vals, lut, 32 - HIST_BITS, NB)
+    sizes = np.diff(np.asarray(b, dtype=np.int64), append=n)
+    C = _allgather_np(sizes, keys, group)
+    recv_tot = np.array([int(C[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
+    roff = np.concatenate([[0], np.cumsum(recv_tot)])
+    T = int(roff[-1])
+    rk, rv, ok_, ov = ops.empty64(T), ops.empty(T), ops.empty64(T), ops.empty(T)
+    works = []
+    for i in range(K):
+        if not C[:, i * R:(i + 1) * R].any():
+            works.append(())
+            continue
+        s0, ss = int(b[i * R]), sizes[i * R:(i + 1) * R]
+        a, z = int(roff[i]), int(roff[i + 1])
+        works.append((_alltoallv_into(rk[a:z], pk[s0:s0 + int(ss.sum())], ss, C[:, i * R + r], group, async_op=True),
+                      _alltoallv_into(rv[a:z], pv[s0:s0 + int(ss.sum())], ss, C[:, i * R + r], group, async_op=True)))
+    for i in range(K):
+        for w in works[i]:
+            if w is not None:
+                w.wait()
+        a, z = int(roff[i]), int(roff[i + 1])
+        if z > a:
+            ops.sort_pairs(rk[a:z], rv[a:z], out_keys=ok_[a:z], out_vals=ov[a:z])
+    n_recv = np.array([int(C[:, d::R].sum()) for d in range(R)], dtype=np.int64)
+    return _rebalance_pairs(ok_, ov, n_recv, ops, group)
+
+
 def distrib_sort(keys, ops=None, group=None, schedule="msd", **kw):
     """Sort the distributed uint32 array whose rank-r shard is `keys`.
     Returns this rank's shard of the sorted array (ceil(N/R) keys per rank)."""
@@ -333,4 +428,5 @@ def distrib_sort(keys, ops=None, group=None, schedule="msd", **kw):
     raise ValueError("schedule must be 'msd' or 'lsd'")
 
 
-__all__ = ["HipOps", "distrib_sort", "sort_lsd", "sort_msd", "plan_msd", "plan_rounds", "shard_cut"]
+__all__ = ["HipOps", "distrib_sort", "distrib_sort_pairs", "sort_lsd", "sort_msd", "plan_msd", "plan_rounds",
+           "shard_cut"]

@@ -129,6 +129,13 @@ LIBSORT_API bool libsortPartitionLutU32(const uint32_t* d_in, uint32_t* d_out, s
                                         const uint8_t* d_lut, uint32_t lut_shift,
                                         uint32_t nbuckets, uint32_t* d_bounds, void* stream);
 
+/* The same for (uint64 key, uint32 payload) pairs, bucket = lut[(key >> 32) >>
+ * lut_shift]; keys and payloads move together (out of place, stable). */
+LIBSORT_API bool libsortPartitionLutU64U32(const uint64_t* d_kin, const uint32_t* d_vin,
+                                           uint64_t* d_kout, uint32_t* d_vout, size_t n,
+                                           const uint8_t* d_lut, uint32_t lut_shift,
+                                           uint32_t nbuckets, uint32_t* d_bounds, void* stream);
+
 /* Gather-copy of nseg segments: dst[dst_off[i] + j] = src[src_off[i] + j] for
  * j < len[i].  The three tables are host arrays.  Used to put exchanged
  * buckets into bucket-major / rank-minor order between distributed rounds. */

@@ -31,6 +31,30 @@ class OracleOps:
     def empty(self, n):
         return self.torch.empty(n, dtype=self.torch.int32)
 
+    def empty64(self, n):
+        return self.torch.empty(n, dtype=self.torch.int64)
+
+    def sort_pairs(self, keys, vals, out_keys=None, out_vals=None):
+        k, v = self.o.stable_sort_kv64(keys.numpy().view(np.uint64), vals.numpy().view(np.uint32))
+        kt = self.torch.from_numpy(np.ascontiguousarray(k).view(np.int64).copy())
+        vt = self._t(v)
+        if out_keys is None:
+            return kt, vt
+        out_keys.copy_(kt)
+        out_vals.copy_(vt)
+        return out_keys, out_vals
+
+    def partition_lut_pairs(self, keys, vals, lut, shift, nbuckets):
+        k = keys.numpy().view(np.uint64)
+        b = np.asarray(lut, dtype=np.uint8)[(k >> np.uint64(32 + shift)).astype(np.int64)].astype(np.int64)
+        o = np.argsort(b, kind="stable")
+        starts = np.concatenate([[0], np.cumsum(np.bincount(b, minlength=nbuckets))[:-1]])
+        return (self.torch.from_numpy(k[o].view(np.int64).copy()), self._t(vals.numpy().view(np.uint32)[o]),
+                starts.astype(np.int64))
+
+    def sample_hi(self, keys, stride, block=4096):
+        return self.sample(keys, stride, block).view(self.torch.int32)[1::2].contiguous()
+
     def sort(self, keys, out=None):
         res = self._t(self.o.sort_u32(self._np(keys)))
         if out is None:
@@ -104,6 +128,39 @@ def rank_worker(rank, world, port, x, schedule, outdir, use_gpu, kw=None):
     np.save(os.path.join(outdir, "rank%d.npy" % rank), res.cpu().numpy().view(np.uint32))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def pairs_worker(rank, world, port, k, outdir, use_gpu, kw=None):
+    """distrib_sort_pairs on this rank's shard of (k, global index)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    from pylibsort import distrib
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    N = k.size
+    S = -(-N // world)
+    lo, hi = min(N, rank * S), min(N, (rank + 1) * S)
+    kt = torch.from_numpy(k[lo:hi].view(np.int64).copy())
+    vt = torch.from_numpy(np.arange(lo, hi, dtype=np.uint32).view(np.int32).copy())
+    if use_gpu:
+        torch.cuda.set_device(0)
+        ops = distrib.HipOps()
+        kt, vt = kt.cuda(), vt.cuda()
+    else:
+        ops = OracleOps()
+    rk, rv = distrib.distrib_sort_pairs(kt, vt, ops=ops, **(kw or {}))
+    np.save(os.path.join(outdir, "k%d.npy" % rank), rk.cpu().numpy().view(np.uint64))
+    np.save(os.path.join(outdir, "v%d.npy" % rank), rv.cpu().numpy().view(np.uint32))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def run_pair_ranks(k, world, tmpdir, use_gpu=False, port=29911, kw=None):
+    import torch.multiprocessing as mp
+    mp.spawn(pairs_worker, args=(world, port, k, str(tmpdir), use_gpu, kw), nprocs=world, join=True)
+    return ([np.load(os.path.join(str(tmpdir), "k%d.npy" % r)) for r in range(world)],
+            [np.load(os.path.join(str(tmpdir), "v%d.npy" % r)) for r in range(world)])
 
 
 def run_ranks(x, world, schedule, tmpdir, use_gpu=False, port=29611, kw=None):

@@ -72,6 +72,28 @@ def test_msd_sparse_key_ranges_gloo(tmp_path):
     assert [s.size for s in shards] == [s.size for s in shard_inputs(x, 3)]
 
 
+@pytest.mark.parametrize("world,rounds,case", [(2, 4, "dups"), (3, 3, "wide"), (2, 1, "wide"), (3, 5, "onekey")])
+def test_distrib_pairs_stable_gloo(tmp_path, world, rounds, case):
+    """C5 semantics: stable (u64 key, u32 payload) sort across ranks -- payload
+    = original global index, so equal keys must keep increasing payloads."""
+    from distrib_helpers import run_pair_ranks
+    from oracle import oracle
+    rng = np.random.default_rng(world * 100 + rounds)
+    n = 40013
+    if case == "dups":
+        k = rng.integers(0, 1 << 10, n, dtype=np.uint64) * np.uint64(0x0040000000100001)  # many equal keys
+    elif case == "wide":
+        k = rng.integers(0, 1 << 63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+    else:
+        k = np.full(n, 0x123456789ABCDEF0, dtype=np.uint64)
+    ks, vs = run_pair_ranks(k, world, tmp_path, port=29870 + 10 * world + rounds, kw={"rounds": rounds})
+    rk, rv = oracle.stable_sort_kv64(k, np.arange(n, dtype=np.uint32))
+    np.testing.assert_array_equal(np.concatenate(ks), rk)
+    np.testing.assert_array_equal(np.concatenate(vs), rv)
+    S = -(-n // world)
+    assert [x.size for x in ks] == [min(n, (r + 1) * S) - min(n, r * S) for r in range(world)]
+
+
 def test_plan_rounds_contiguous_and_balanced():
     from pylibsort.distrib import plan_rounds, _group_range
     rng = np.random.default_rng(4)

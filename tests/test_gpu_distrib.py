@@ -45,3 +45,18 @@ def test_msd_rounds_hip_backend(tmp_path, rounds):
     shards = run_ranks(x, 2, "msd", tmp_path, use_gpu=True, port=29820 + rounds, kw={"rounds": rounds})
     np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))
     assert [s.size for s in shards] == [s.size for s in shard_inputs(x, 2)]
+
+
+def test_distrib_pairs_hip_backend(tmp_path):
+    """C5 path on the GPU: stable (u64 key, u32 payload) sort over 2 ranks."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from distrib_helpers import run_pair_ranks
+    from oracle import oracle
+    rng = np.random.default_rng(9)
+    n = (1 << 19) + 333
+    k = rng.integers(0, 1 << 12, n, dtype=np.uint64) * np.uint64(0x0010000000000001)  # ties across ranks
+    ks, vs = run_pair_ranks(k, 2, tmp_path, use_gpu=True, port=29960, kw={"rounds": 4})
+    rk, rv = oracle.stable_sort_kv64(k, np.arange(n, dtype=np.uint32))
+    np.testing.assert_array_equal(np.concatenate(ks), rk)
+    np.testing.assert_array_equal(np.concatenate(vs), rv)

@@ -204,6 +204,27 @@ def test_partition_lut(dev, oracle_mod, n, shift, nbuckets):
     np.testing.assert_array_equal(b.cpu().numpy().astype(np.int64), starts)
 
 
+@pytest.mark.parametrize("n", [0, 3, 2049, 300007])
+@pytest.mark.parametrize("nbuckets", [8, 16, 64])
+def test_partition_lut_pairs(dev, n, nbuckets):
+    """libsortPartitionLutU64U32 (the C5 multi-GPU partition): stable, pairs
+    move together, bucket = lut[(key >> 32) >> 20]."""
+    rng = np.random.default_rng(n + nbuckets)
+    k = rng.integers(0, 1 << 64, n, dtype=np.uint64)
+    k[: n // 3] = k[0] if n else 0  # equal keys: stability visible in the payloads
+    v = np.arange(n, dtype=np.uint32)
+    lut = np.sort(rng.integers(0, nbuckets, 4096)).astype(np.uint8)
+    ok_, ov, b = dev.partition_lut_pairs_u64_u32(torch.from_numpy(k.view(np.int64)).cuda(),
+                                                 torch.from_numpy(v.view(np.int32)).cuda(),
+                                                 torch.from_numpy(lut).cuda(), 20, nbuckets)
+    bucket = lut[(k >> np.uint64(52)).astype(np.int64)].astype(np.int64)
+    o = np.argsort(bucket, kind="stable")
+    np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), k[o])
+    np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint32), v[o])
+    starts = np.concatenate([[0], np.cumsum(np.bincount(bucket, minlength=nbuckets))[:-1]])
+    np.testing.assert_array_equal(b.cpu().numpy().astype(np.int64), starts)
+
+
 def test_segment_copy(dev):
     src = torch.arange(1000, dtype=torch.int32, device="cuda")
     dst = torch.zeros(1000, dtype=torch.int32, device="cuda")
@@ -301,3 +322,41 @@ def test_reference_size_full_sort_sha(dev, golden, digit_bits):
     host = out.cpu().numpy().view(np.uint32)
     assert hashlib.sha256(host.tobytes()).hexdigest()[:16] == g["sha256_prefix"][str(n)]["sorted"]
     assert int(np.count_nonzero(host[1:] == host[:-1])) == g["sha256_prefix"][str(n)]["duplicate_keys"]
+
+
+def _device_sorted_and_checksums(x, out):
+    """Size-independent parity at configs too large for the host oracle:
+    out is non-decreasing as uint32 and holds the same multiset as x
+    (sum and sum of squares of the keys, mod 2^64)."""
+    flip = torch.tensor(-(1 << 31), dtype=torch.int32, device=out.device)
+    s = torch.bitwise_xor(out, flip)              # uint32 order -> int32 order
+    ok = True
+    chunk = 1 << 26
+    for i in range(0, out.numel() - 1, chunk):
+        a = s[i:i + chunk + 1]
+        ok &= bool((a[1:] >= a[:-1]).all())
+    def sums(t):
+        tot, sq = 0, 0
+        for i in range(0, t.numel(), chunk):
+            v = t[i:i + chunk].to(torch.int64) & 0xFFFFFFFF
+            tot += int(v.sum())
+            sq += int((v * v).sum())                  # int64 wrap = mod 2^64
+        return tot % (1 << 64), sq % (1 << 64)
+    return ok, sums(x) == sums(out)
+
+
+@pytest.mark.parametrize("bits", [8, 4])
+def test_config3_2pow30(dev, bits):
+    # C3: 2^30 keys of the PCG stream (device skip-ahead), full sort on one GPU
+    import pylibsort
+    prev = pylibsort.setDigitBits(bits)
+    try:
+        n = 1 << 30
+        x = dev.populate_u32(n)
+        out = dev.sort_keys_u32(x)
+        torch.cuda.synchronize()
+        assert pylibsort.lib().libsortDeviceErrors() == 0
+        ok, same = _device_sorted_and_checksums(x, out)
+        assert ok and same
+    finally:
+        pylibsort.setDigitBits(prev)
