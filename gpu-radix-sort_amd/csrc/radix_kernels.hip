@@ -1406,7 +1406,10 @@ int choose_algorithm(size_t n, int bits) {
 // per-tile count kernel per pass.
 template <typename K>
 constexpr int tp_items() { return sizeof(K) == 8 ? 8 : 16; }
-constexpr int tp_block(int bits) { return bits == 4 ? 256 : 512; }
+#ifndef LIBSORT_TP8_BLOCK
+#define LIBSORT_TP8_BLOCK 512  // threads of an 8-bit tile (16 keys each)
+#endif
+constexpr int tp_block(int bits) { return bits == 4 ? 256 : LIBSORT_TP8_BLOCK; }
 template <typename K>
 uint32_t tp_tiles(size_t n, int bits) {
   const uint64_t t = (uint64_t)tp_block(bits) * tp_items<K>();

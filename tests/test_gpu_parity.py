@@ -360,3 +360,25 @@ def test_config3_2pow30(dev, bits):
         assert ok and same
     finally:
         pylibsort.setDigitBits(prev)
+
+
+@pytest.mark.parametrize("bits", [8, 4])
+def test_maximum_size(dev, bits):
+    """n = 2^32 - 1 keys, the largest the ABI accepts: 32-bit run offsets up to
+    the last tile (whose next-tile index wraps), 2^19 / 2^20 tiles.  The keys
+    are the PCG stream; parity by sortedness + multiset checksums."""
+    import pylibsort
+    if torch.cuda.get_device_properties(0).total_memory < (80 << 30):
+        pytest.skip("needs ~64 GiB of device memory")
+    prev = pylibsort.setDigitBits(bits)
+    try:
+        n = (1 << 32) - 1
+        x = dev.populate_u32(n)
+        out = dev.sort_keys_u32(x)
+        torch.cuda.synchronize()
+        assert pylibsort.lib().libsortDeviceErrors() == 0
+        ok, same = _device_sorted_and_checksums(x, out)
+        assert ok and same
+    finally:
+        pylibsort.setDigitBits(prev)
+        torch.cuda.empty_cache()

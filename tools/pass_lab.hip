@@ -425,8 +425,9 @@ __device__ __forceinline__ uint32_t tile_of_block() {
 // (identity positions), 5 = 4 + no LDS scatter/read-back (keys go straight
 // from the load registers to a dummy-conditioned store), 6 = full kernel but
 // no global flush of the next-pass counts, 7 = full kernel without counting.
-template <int CHAINS, bool LASTW, int SPLIT, bool ASM = true, int BLOCK = 256, bool XCD = false, int ABL = 0>
-__global__ __launch_bounds__(BLOCK) void k_pass_z(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout,
+template <int CHAINS, bool LASTW, int SPLIT, bool ASM = true, int BLOCK = 256, bool XCD = false, int ABL = 0,
+          int MINB = 1, bool PACK = false>
+__global__ __launch_bounds__(BLOCK, MINB) void k_pass_z(const uint32_t* __restrict__ kin, uint32_t* __restrict__ kout,
                                                 uint32_t shift, uint32_t nb, uint32_t* __restrict__ C,
                                                 const uint32_t* __restrict__ B, uint32_t* __restrict__ C_next) {
   constexpr int ITEMS = 16, RADIX = 16;
@@ -455,6 +456,7 @@ __global__ __launch_bounds__(BLOCK) void k_pass_z(const uint32_t* __restrict__ k
     C[(size_t)t * RADIX + tid] = 0u;
   }
   uint32_t k[ITEMS], rk[ITEMS];
+  uint32_t rkp[ITEMS / 2];  // PACK: two 16-bit ranks per register across the block phase
   const uint32_t* kp = kin + (uint64_t)t * TILE + w * WSPAN + lane;
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) k[j] = kp[j * kWave];
@@ -463,6 +465,10 @@ __global__ __launch_bounds__(BLOCK) void k_pass_z(const uint32_t* __restrict__ k
     for (int j = 0; j < ITEMS; ++j) rk[j] = w * WSPAN + j * kWave + lane;
   } else {
     rank_lean4<CHAINS, LASTW, ASM>(k, rk, &s_whist[w * CHAINS * RADIX], shift, nb, &s_dummy[tid]);
+  }
+  if constexpr (PACK) {
+#pragma unroll
+    for (int j = 0; j < ITEMS / 2; ++j) rkp[j] = rk[2 * j] | (rk[2 * j + 1] << 16);
   }
   __syncthreads();
   if (w == 0) {
@@ -495,7 +501,8 @@ __global__ __launch_bounds__(BLOCK) void k_pass_z(const uint32_t* __restrict__ k
     } else if constexpr (ABL == 4) {
       s_keys[rk[j]] = k[j] + d;
     } else {
-      s_keys[s_whist[(w * CHAINS + j / (ITEMS / CHAINS)) * RADIX + d] + rk[j]] = k[j];
+      const uint32_t r = PACK ? ((j & 1) ? (rkp[j / 2] >> 16) : (rkp[j / 2] & 0xFFFFu)) : rk[j];
+      s_keys[s_whist[(w * CHAINS + j / (ITEMS / CHAINS)) * RADIX + d] + r] = k[j];
     }
   }
   __syncthreads();
@@ -639,6 +646,18 @@ int main(int argc, char** argv) {
     V.push_back({"z c1 s2 xcd", [&] {
       hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0], B,
                          L.ws.tc[1]);
+    }});
+    V.push_back({"z c1 s2 xcd pack", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 0, 1, true>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u,
+                         L.ws.tc[0], B, L.ws.tc[1]);
+    }});
+    V.push_back({"z c1 s2 xcd pack minb8", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 0, 8, true>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u,
+                         L.ws.tc[0], B, L.ws.tc[1]);
+    }});
+    V.push_back({"z c1 s2 xcd minb8", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 0, 8, false>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u,
+                         L.ws.tc[0], B, L.ws.tc[1]);
     }});
     V.push_back({"ABL contiguous stores", [&] {
       hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 1>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
