@@ -75,8 +75,9 @@ struct Workspace {
   // tile-offset path: per-tile digit counts (two buffers) and chunk totals
   uint32_t* tc[2] = {nullptr, nullptr};
   size_t tc_cap = 0;  // words per buffer
-  uint32_t* tb = nullptr;
+  uint32_t* tb = nullptr;  // chunk prefixes B[chunks][RADIX], then the digit starts D[RADIX]
   size_t tb_cap = 0;  // words
+  uint32_t* tticket = nullptr;  // last-arriver ticket of the column scan (zero between launches)
   hipError_t ensure_tiles(size_t count_words, size_t chunk_words);
 
   hipError_t ensure_counts(size_t m);

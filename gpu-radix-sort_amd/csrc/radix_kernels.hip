@@ -774,17 +774,39 @@ __global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ key
   }
 }
 
-// Level 1 of the column scan: block c owns rows [c*CH, (c+1)*CH), CH =
-// kColRowsPerLane * (256 / RADIX).  Thread (row-lane s, column d) sums its
-// kColRowsPerLane contiguous rows, the row-lanes are scanned through LDS, and
-// the rows are rewritten with the chunk-local exclusive prefix.  The chunk
-// totals go to B[c][d].
+// The column scan turns the per-tile counts C[tile][RADIX] into each tile's
+// run offsets: offset(t, d) = C'[t][d] + B[t / CH][d] + D[d] with C' the
+// chunk-local exclusive scan (chunks of CH = kColRowsPerLane * 256 / RADIX
+// rows), B the exclusive scan over chunks and D the digit starts.  The level
+// above each kernel runs in that kernel's last-arriving block (last_arriver),
+// so a 4-bit pass needs one scan kernel and an 8-bit pass two.
+
+// Last-arriver hand-off (MI355X_MICROARCH.md "Workgroup dispatch, XCD
+// placement & inter-workgroup visibility", the counter row of its table):
+// every block has published its values with sc1 (write-through) stores; each
+// wave waits for them (vmcnt(0)), the block joins a barrier, and one lane adds
+// to an agent-scope ticket.  The block whose add returned count - 1 is the
+// last: it reads everyone's values with sc1 loads (ld_agent) after a barrier.
+// Returns true in that block; it resets the ticket for the next launch.
+__device__ __forceinline__ bool last_arriver(uint32_t* ticket, uint32_t count, uint32_t* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = (t == count - 1u) ? 1u : 0u;
+  }
+  __syncthreads();
+  return *s_flag != 0u;
+}
+
+// Level 1: block c owns rows [c*CH, (c+1)*CH).  Thread (row-lane s, column d)
+// sums its kColRowsPerLane contiguous rows, the row-lanes are scanned through
+// LDS, and the rows are rewritten with the chunk-local exclusive prefix.
+// Returns the chunk total of column d (valid for s == 0).
 template <int RADIX>
-__global__ __launch_bounds__(256) void k_colscan_l1(uint32_t* __restrict__ C, uint32_t rows,
-                                                    uint32_t* __restrict__ B) {
+__device__ __forceinline__ uint32_t colscan_chunk(uint32_t* __restrict__ C, uint32_t rows, uint32_t* s_sum) {
   constexpr int L = 256 / RADIX;
   constexpr int CH = kColRowsPerLane * L;
-  __shared__ uint32_t s_sum[256];
   const uint32_t d = threadIdx.x % RADIX, s = threadIdx.x / RADIX;
   const uint64_t r0 = (uint64_t)blockIdx.x * CH + (uint64_t)s * kColRowsPerLane;
   uint32_t x[kColRowsPerLane];
@@ -807,49 +829,65 @@ __global__ __launch_bounds__(256) void k_colscan_l1(uint32_t* __restrict__ C, ui
     if (r0 + i < rows) C[(r0 + i) * RADIX + d] = run;
     run += x[i];
   }
-  if (s == 0) B[(size_t)blockIdx.x * RADIX + d] = tot;
+  return tot;
 }
 
-// Level 2 (one block): exclusive column scan of B[nchunks][RADIX] in place,
-// plus the digit starts (exclusive scan of the column totals) added in.
+// RADIX <= 16: level 1 per block; the last block scans the chunk totals
+// B[nchunks][RADIX] in place (exclusive over chunks) and writes the digit
+// starts D[RADIX].
 template <int RADIX>
-__global__ __launch_bounds__(256) void k_colscan_l2(uint32_t* __restrict__ B, uint32_t nchunks) {
+__global__ __launch_bounds__(256) void k_colscan_small(uint32_t* __restrict__ C, uint32_t rows, uint32_t* B,
+                                                       uint32_t nchunks, uint32_t* __restrict__ D, uint32_t* ticket) {
   constexpr int L = 256 / RADIX;
   __shared__ uint32_t s_sum[256];
   __shared__ uint32_t s_wsum[4];
-  __shared__ uint32_t s_dstart[RADIX];
+  __shared__ uint32_t s_flag;
   const uint32_t d = threadIdx.x % RADIX, s = threadIdx.x / RADIX;
-  const uint32_t per = (nchunks + L - 1) / L;  // rows per row-lane
+  const uint32_t tot = colscan_chunk<RADIX>(C, rows, s_sum);
+  if (s == 0) st_agent(&B[(size_t)blockIdx.x * RADIX + d], tot);
+  if (!last_arriver(ticket, gridDim.x, &s_flag)) return;
+  const uint32_t per = (nchunks + L - 1) / L;  // chunk rows per row-lane
   const uint32_t a = s * per, b = min(nchunks, a + per);
   uint32_t sum = 0;
-  for (uint32_t r = a; r < b; ++r) sum += B[(size_t)r * RADIX + d];
+  for (uint32_t r = a; r < b; ++r) sum += ld_agent(&B[(size_t)r * RADIX + d]);
   s_sum[threadIdx.x] = sum;
   __syncthreads();
-  uint32_t run = 0, tot = 0;
+  uint32_t run = 0, col = 0;
   for (uint32_t q = 0; q < (uint32_t)L; ++q) {
     const uint32_t v = s_sum[q * RADIX + d];
     run += q < s ? v : 0u;
-    tot += v;
+    col += v;
   }
-  // digit starts: exclusive scan over d of the column totals (thread d, s == 0)
   uint32_t total_unused;
-  const uint32_t ds = block_exclusive_scan<256>(s == 0 ? tot : 0u, s_wsum, total_unused);
-  if (s == 0) s_dstart[d] = ds;
-  __syncthreads();
-  run += s_dstart[d];
+  const uint32_t ds = block_exclusive_scan<256>(s == 0 ? col : 0u, s_wsum, total_unused);
+  if (s == 0) D[d] = ds;
   for (uint32_t r = a; r < b; ++r) {
-    const uint32_t v = B[(size_t)r * RADIX + d];
+    const uint32_t v = ld_agent(&B[(size_t)r * RADIX + d]);
     B[(size_t)r * RADIX + d] = run;
     run += v;
   }
+  if (threadIdx.x == 0) *ticket = 0u;
 }
 
-// Level 2 for wide digits (RADIX = 256): block d scans column d of
-// B[nchunks][RADIX] in place (exclusive) and writes the column total to tot[d].
+// RADIX = 256, level 1: chunk totals to B with plain stores (the next kernel
+// reads them).
 template <int RADIX>
-__global__ __launch_bounds__(256) void k_colscan_l2col(uint32_t* __restrict__ B, uint32_t nchunks,
-                                                       uint32_t* __restrict__ tot) {
+__global__ __launch_bounds__(256) void k_colscan_l1(uint32_t* __restrict__ C, uint32_t rows,
+                                                    uint32_t* __restrict__ B) {
+  __shared__ uint32_t s_sum[256];
+  const uint32_t tot = colscan_chunk<RADIX>(C, rows, s_sum);
+  if (threadIdx.x < (uint32_t)RADIX) B[(size_t)blockIdx.x * RADIX + threadIdx.x] = tot;
+}
+
+// RADIX = 256, level 2: block d scans column d of B[nchunks][RADIX] in place
+// (exclusive) and publishes the column total; the last block turns the totals
+// into the digit starts D.
+template <int RADIX>
+__global__ __launch_bounds__(256) void k_colscan_wide(uint32_t* __restrict__ B, uint32_t nchunks, uint32_t* D,
+                                                      uint32_t* ticket) {
+  static_assert(RADIX == 256, "one thread per digit in the last block");
   __shared__ uint32_t s_wsum[4];
+  __shared__ uint32_t s_flag;
   const uint32_t d = blockIdx.x;
   const uint32_t per = (nchunks + 255) / 256;
   const uint32_t a = threadIdx.x * per, b = min(nchunks, a + per);
@@ -862,18 +900,12 @@ __global__ __launch_bounds__(256) void k_colscan_l2col(uint32_t* __restrict__ B,
     B[(size_t)r * RADIX + d] = run;
     run += v;
   }
-  if (threadIdx.x == 0) tot[d] = total;
-}
-
-// Level 3 for wide digits: every block recomputes the digit starts (exclusive
-// scan of tot) and adds them to its rows of B.
-template <int RADIX>
-__global__ __launch_bounds__(RADIX) void k_colscan_l3(uint32_t* __restrict__ B, uint32_t nchunks,
-                                                      const uint32_t* __restrict__ tot) {
-  __shared__ uint32_t s_wsum[(RADIX + 63) / 64];
-  uint32_t total;
-  const uint32_t ds = block_exclusive_scan<RADIX>(tot[threadIdx.x], s_wsum, total);
-  for (uint32_t r = blockIdx.x; r < nchunks; r += gridDim.x) B[(size_t)r * RADIX + threadIdx.x] += ds;
+  if (threadIdx.x == 0) st_agent(&D[d], total);
+  if (!last_arriver(ticket, gridDim.x, &s_flag)) return;
+  uint32_t total_unused;
+  const uint32_t ds = block_exclusive_scan<256>(ld_agent(&D[threadIdx.x]), s_wsum, total_unused);
+  D[threadIdx.x] = ds;
+  if (threadIdx.x == 0) *ticket = 0u;
 }
 
 // Tile handled by block b of a launch whose tiles are independent.  Blocks
@@ -903,7 +935,7 @@ __global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, 
                                                      const V* __restrict__ vin, V* __restrict__ vout,
                                                      uint32_t n, Op op_in, OpN op_next,
                                                      uint32_t* __restrict__ C, const uint32_t* __restrict__ B,
-                                                     uint32_t* __restrict__ C_next) {
+                                                     const uint32_t* __restrict__ D, uint32_t* __restrict__ C_next) {
   constexpr bool HAS_V = !std::is_same<V, NoValue>::value;
   using VS = typename std::conditional<HAS_V, V, uint8_t>::type;
   constexpr int RADIX = 1 << BITS;
@@ -940,7 +972,7 @@ __global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, 
   // this tile's run offsets (independent of every other tile)
   uint32_t gofs = 0;
   if (tid < RADIX) {
-    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid];
+    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid] + D[tid];
     C[(size_t)t * RADIX + tid] = 0u;
   }
 
@@ -1283,6 +1315,11 @@ hipError_t Workspace::ensure_tiles(size_t count_words, size_t chunk_words) {
     LS_TRY(hipMalloc(&tb, chunk_words * sizeof(uint32_t)));
     tb_cap = chunk_words;
   }
+  if (!tticket) {
+    LS_TRY(hipMalloc(&tticket, 64 * sizeof(uint32_t)));
+    LS_TRY(hipMemset(tticket, 0, 64 * sizeof(uint32_t)));  // last-arriver tickets start (and end) at zero
+    LS_TRY(hipDeviceSynchronize());  // once: the sort streams are non-blocking w.r.t. the null stream
+  }
   return hipSuccess;
 }
 
@@ -1313,9 +1350,9 @@ void Workspace::release() {
                  (void*)os_small})
     if (p) (void)hipFree(p);
   os_status[0] = os_status[1] = os_small = nullptr;
-  for (auto p : {(void*)tc[0], (void*)tc[1], (void*)tb})
+  for (auto p : {(void*)tc[0], (void*)tc[1], (void*)tb, (void*)tticket})
     if (p) (void)hipFree(p);
-  tc[0] = tc[1] = tb = nullptr;
+  tc[0] = tc[1] = tb = tticket = nullptr;
   tc_cap = tb_cap = 0;
   os_status_cap = 0;
   if (seg_host) (void)hipHostFree(seg_host);
@@ -1430,21 +1467,23 @@ hipError_t tiles_counts(Workspace& ws, const K* in, size_t n, Op op, uint32_t ti
   return hipGetLastError();
 }
 
+// Digit starts of the last column scan (the tile path's bucket boundaries).
+inline uint32_t* tiles_digit_starts(Workspace& ws, uint32_t tiles, int bits) {
+  return ws.tb + (size_t)tp_chunks(tiles, bits) * (1u << bits);
+}
+
 template <int BITS>
 hipError_t tiles_colscan(Workspace& ws, uint32_t* C, uint32_t tiles, hipStream_t st) {
   constexpr int RADIX = 1 << BITS;
   const uint32_t chunks = tp_chunks(tiles, BITS);
+  uint32_t* D = tiles_digit_starts(ws, tiles, BITS);
   ScopedTimer tm("colscan", st, tiles);
-  hipLaunchKernelGGL(k_colscan_l1<RADIX>, dim3(chunks), dim3(256), 0, st, C, tiles, ws.tb);
-  LS_TRY(hipGetLastError());
   if constexpr (RADIX <= 16) {
-    hipLaunchKernelGGL(k_colscan_l2<RADIX>, dim3(1), dim3(256), 0, st, ws.tb, chunks);
+    hipLaunchKernelGGL(k_colscan_small<RADIX>, dim3(chunks), dim3(256), 0, st, C, tiles, ws.tb, chunks, D, ws.tticket);
   } else {
-    uint32_t* tot = ws.tb + (size_t)chunks * RADIX;
-    hipLaunchKernelGGL(k_colscan_l2col<RADIX>, dim3(RADIX), dim3(256), 0, st, ws.tb, chunks, tot);
+    hipLaunchKernelGGL(k_colscan_l1<RADIX>, dim3(chunks), dim3(256), 0, st, C, tiles, ws.tb);
     LS_TRY(hipGetLastError());
-    hipLaunchKernelGGL(k_colscan_l3<RADIX>, dim3(std::min(chunks, 1024u)), dim3(RADIX), 0, st, ws.tb, chunks,
-                       (const uint32_t*)tot);
+    hipLaunchKernelGGL(k_colscan_wide<RADIX>, dim3(RADIX), dim3(256), 0, st, ws.tb, chunks, D, ws.tticket);
   }
   return hipGetLastError();
 }
@@ -1489,10 +1528,12 @@ hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vou
   ScopedTimer tm("tilepass", st, n);
   if (fuse)
     hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, BITS == 4, Op, Op>), dim3(tiles), dim3(B), 0, st,
-                       kin, kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
+                       kin, kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, tiles_digit_starts(ws, tiles, BITS),
+                       nxt);
   else
     hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, false, Op, Op>), dim3(tiles), dim3(B), 0, st, kin,
-                       kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, nxt);
+                       kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, tiles_digit_starts(ws, tiles, BITS),
+                       nxt);
   return hipGetLastError();
 }
 
@@ -1656,8 +1697,9 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
     if (n == 0) {
       LS_TRY(hipMemsetAsync(d_bounds, 0, (size_t)ngroups * sizeof(uint32_t), st));
     } else if (ws.last_algo == 3 && num_passes(width, digit_bits) == 1) {
-      // tile path, single pass: chunk 0's scanned totals are the digit starts
-      LS_TRY(hipMemcpyAsync(d_bounds, ws.tb, (size_t)ngroups * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+      // tile path, single pass: the column scan's digit starts
+      LS_TRY(hipMemcpyAsync(d_bounds, tiles_digit_starts(ws, tp_tiles<uint32_t>(n, digit_bits), digit_bits),
+                            (size_t)ngroups * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
     } else if (ws.last_algo == 3) {
       const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 256) / 256, 4096);
       hipLaunchKernelGGL(k_group_bounds<uint32_t>, dim3(blocks), dim3(256), 0, st, out, (uint32_t)n,
@@ -1766,10 +1808,13 @@ hipError_t partition_lut_impl(Workspace& ws, const K* in, K* out, const V* vin, 
   {
     ScopedTimer tm("partition", st, n);
     hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, false, LutDigit>), dim3(tiles), dim3(B), 0, st, in,
-                       out, vin, vout, (uint32_t)n, op, RadixDigit{0u, 1u}, ws.tc[0], (const uint32_t*)ws.tb, ws.tc[1]);
+                       out, vin, vout, (uint32_t)n, op, RadixDigit{0u, 1u}, ws.tc[0], (const uint32_t*)ws.tb,
+                       (const uint32_t*)tiles_digit_starts(ws, tiles, BITS), ws.tc[1]);
     LS_TRY(hipGetLastError());
   }
-  if (d_bounds) LS_TRY(hipMemcpyAsync(d_bounds, ws.tb, (size_t)nbuckets * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  if (d_bounds)
+    LS_TRY(hipMemcpyAsync(d_bounds, tiles_digit_starts(ws, tiles, BITS), (size_t)nbuckets * sizeof(uint32_t),
+                          hipMemcpyDeviceToDevice, st));
   return hipSuccess;
 }
 

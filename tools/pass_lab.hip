@@ -21,6 +21,9 @@ int get_algorithm() { return 3; }
 
 using namespace lsort;
 
+// digit starts of the column scan (the lab's kernels add them like k_tile_pass)
+__device__ const uint32_t* g_lab_D;
+
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -60,7 +63,7 @@ __global__ __launch_bounds__(BLOCK) void k_pass_prof(const uint32_t* __restrict_
   for (int i = tid; i < RADIX * 2 * RADIX; i += BLOCK) s_next[i] = 0u;
   uint32_t gofs = 0;
   if (tid < RADIX) {
-    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid];
+    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid] + g_lab_D[tid];
     C[(size_t)t * RADIX + tid] = 0u;
   }
   const uint64_t tile_base = (uint64_t)t * TILE;
@@ -193,7 +196,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   for (int i = tid; i < RADIX * 2 * RADIX; i += BLOCK) s_next[i] = 0u;
   uint32_t gofs = 0;
   if (tid < RADIX) {
-    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid];
+    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid] + g_lab_D[tid];
     C[(size_t)t * RADIX + tid] = 0u;
   }
   const uint64_t tile_base = (uint64_t)t * TILE;
@@ -452,7 +455,7 @@ __global__ __launch_bounds__(BLOCK, MINB) void k_pass_z(const uint32_t* __restri
   for (int q = 0; q < 2 * RADIX * RADIX / BLOCK; ++q) s_next[tid + q * BLOCK] = 0u;
   uint32_t gofs = 0;
   if (tid < RADIX) {
-    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid];
+    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid] + g_lab_D[tid];
     C[(size_t)t * RADIX + tid] = 0u;
   }
   uint32_t k[ITEMS], rk[ITEMS];
@@ -614,6 +617,10 @@ int main(int argc, char** argv) {
     CK(hipGetLastError());
   }
   CK(tiles_colscan<4>(L.ws, L.ws.tc[0], L.tiles, L.st));
+  {
+    const uint32_t* dptr = tiles_digit_starts(L.ws, L.tiles, 4);
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_lab_D), &dptr, sizeof(dptr)));
+  }
   CK(hipMalloc(&L.C0, L.cwords * 4));
   CK(hipMemcpyAsync(L.C0, L.ws.tc[0], L.cwords * 4, hipMemcpyDeviceToDevice, L.st));
   CK(hipStreamSynchronize(L.st));
@@ -641,7 +648,7 @@ int main(int argc, char** argv) {
     V.push_back({"lib fused", [&] {
       hipLaunchKernelGGL((k_tile_pass<4, 256, 16, uint32_t, NoValue, true>), grid, blk, 0, L.st, L.in, L.out,
                          (const NoValue*)nullptr, (NoValue*)nullptr, (uint32_t)L.n, L.op, L.op_next, L.ws.tc[0], B,
-                         L.ws.tc[1]);
+                         tiles_digit_starts(L.ws, L.tiles, 4), L.ws.tc[1]);
     }});
     V.push_back({"z c1 s2 xcd", [&] {
       hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0], B,
