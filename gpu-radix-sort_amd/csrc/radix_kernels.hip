@@ -848,8 +848,16 @@ __global__ __launch_bounds__(256) void k_colscan_small(uint32_t* __restrict__ C,
   if (!last_arriver(ticket, gridDim.x, &s_flag)) return;
   const uint32_t per = (nchunks + L - 1) / L;  // chunk rows per row-lane
   const uint32_t a = s * per, b = min(nchunks, a + per);
+  // sc1 loads in unrolled batches of 8 (one L2 round trip per batch, not per row)
+  constexpr int BATCH = 8;
   uint32_t sum = 0;
-  for (uint32_t r = a; r < b; ++r) sum += ld_agent(&B[(size_t)r * RADIX + d]);
+  for (uint32_t r0 = a; r0 < b; r0 += BATCH) {
+    uint32_t v[BATCH];
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) v[i] = (r0 + i < b) ? ld_agent(&B[(size_t)(r0 + i) * RADIX + d]) : 0u;
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) sum += v[i];
+  }
   s_sum[threadIdx.x] = sum;
   __syncthreads();
   uint32_t run = 0, col = 0;
@@ -861,10 +869,15 @@ __global__ __launch_bounds__(256) void k_colscan_small(uint32_t* __restrict__ C,
   uint32_t total_unused;
   const uint32_t ds = block_exclusive_scan<256>(s == 0 ? col : 0u, s_wsum, total_unused);
   if (s == 0) D[d] = ds;
-  for (uint32_t r = a; r < b; ++r) {
-    const uint32_t v = ld_agent(&B[(size_t)r * RADIX + d]);
-    B[(size_t)r * RADIX + d] = run;
-    run += v;
+  for (uint32_t r0 = a; r0 < b; r0 += BATCH) {
+    uint32_t v[BATCH];
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) v[i] = (r0 + i < b) ? ld_agent(&B[(size_t)(r0 + i) * RADIX + d]) : 0u;
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) {
+      if (r0 + i < b) B[(size_t)(r0 + i) * RADIX + d] = run;
+      run += v[i];
+    }
   }
   if (threadIdx.x == 0) *ticket = 0u;
 }
