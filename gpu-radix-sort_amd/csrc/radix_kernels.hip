@@ -832,7 +832,7 @@ __device__ __forceinline__ uint32_t colscan_chunk(uint32_t* __restrict__ C, uint
   return tot;
 }
 
-// RADIX <= 16: level 1 per block; the last block scans the chunk totals
+// RADIX <= 32: level 1 per block; the last block scans the chunk totals
 // B[nchunks][RADIX] in place (exclusive over chunks) and writes the digit
 // starts D[RADIX].
 template <int RADIX>
@@ -1491,7 +1491,7 @@ hipError_t tiles_colscan(Workspace& ws, uint32_t* C, uint32_t tiles, hipStream_t
   const uint32_t chunks = tp_chunks(tiles, BITS);
   uint32_t* D = tiles_digit_starts(ws, tiles, BITS);
   ScopedTimer tm("colscan", st, tiles);
-  if constexpr (RADIX <= 16) {
+  if constexpr (RADIX <= 32) {
     hipLaunchKernelGGL(k_colscan_small<RADIX>, dim3(chunks), dim3(256), 0, st, C, tiles, ws.tb, chunks, D, ws.tticket);
   } else {
     hipLaunchKernelGGL(k_colscan_l1<RADIX>, dim3(chunks), dim3(256), 0, st, C, tiles, ws.tb);
@@ -1845,7 +1845,9 @@ hipError_t partition_lut_any(Workspace& ws, const K* in, K* out, const V* vin, V
   if constexpr (!std::is_same<V, NoValue>::value) {
     if (!vin || !vout || (const void*)vin == (const void*)vout) return hipErrorInvalidValue;
   }
+  // digit width by bucket count: 16 -> 4-bit tiles, 32 -> 5-bit (the 8-rank x 4-round exchange), else 8-bit
   if (nbuckets <= 16) return partition_lut_impl<4, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st);
+  if (nbuckets <= 32) return partition_lut_impl<5, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st);
   return partition_lut_impl<8, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st);
 }
 }  // namespace

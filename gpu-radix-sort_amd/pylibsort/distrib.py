@@ -160,7 +160,9 @@ def _alltoallv(send, send_counts, recv_counts, ops, group):
 
 def _alltoallv_into(recv, send, send_counts, recv_counts, group, async_op=False):
     """all_to_all_single into `recv`; returns the async work handle (or None).
-    Host-staged (gloo) exchanges run synchronously."""
+    Device tensors over gloo (the one-GPU rehearsal) are staged through host
+    memory synchronously; RCCL, and gloo on host tensors (the CPU tests), run
+    the same issue-now / wait-later path as the 8-GPU job."""
     rs = [int(c) for c in recv_counts]
     ss = [int(c) for c in send_counts]
     if _host_staged(group) and send.is_cuda:
@@ -168,7 +170,7 @@ def _alltoallv_into(recv, send, send_counts, recv_counts, group, async_op=False)
         dist.all_to_all_single(r_host, send.cpu(), rs, ss, group=group)
         recv.copy_(r_host)
         return None
-    return dist.all_to_all_single(recv, send, rs, ss, group=group, async_op=async_op and not _host_staged(group))
+    return dist.all_to_all_single(recv, send, rs, ss, group=group, async_op=async_op)
 
 
 def shard_cut(N, R):
