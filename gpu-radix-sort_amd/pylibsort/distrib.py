@@ -379,10 +379,15 @@ def distrib_sort_pairs(keys, vals, ops=None, group=None, rounds=4, sample_stride
     skew fallback: a heavy key range concentrates work on one rank, the result
     stays exact.  Returns this rank's (keys, vals) shard, ceil(N/R) pairs."""
     ops = HipOps() if ops is None else ops
+    if dist.get_world_size(group) == 1:
+        return ops.sort_pairs(keys, vals)
+    return _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride)
+
+
+def _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride):
+    """The round schedule of distrib_sort_pairs (any world size)."""
     R = dist.get_world_size(group)
     r = dist.get_rank(group)
-    if R == 1:
-        return ops.sort_pairs(keys, vals)
     K = max(1, min(int(rounds), 256 // R))
     n = keys.numel()
     h = ops.histogram(ops.sample_hi(keys, sample_stride), 32 - HIST_BITS, HIST_BITS)

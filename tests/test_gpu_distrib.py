@@ -60,3 +60,19 @@ def test_distrib_pairs_hip_backend(tmp_path):
     rk, rv = oracle.stable_sort_kv64(k, np.arange(n, dtype=np.uint32))
     np.testing.assert_array_equal(np.concatenate(ks), rk)
     np.testing.assert_array_equal(np.concatenate(vs), rv)
+
+
+def test_round_schedules_over_rccl_single_rank():
+    """The exchange path of the 8-GPU job on a real RCCL communicator (one
+    rank: RCCL refuses two ranks on one GPU): async all_to_all_single per
+    round, stream-level waits, per-round range sorts, pair rounds."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import os
+    import pathlib
+    import subprocess
+    import sys
+    worker = pathlib.Path(__file__).with_name("rccl_single_rank_worker.py")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29993")
+    r = subprocess.run([sys.executable, str(worker)], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
