@@ -116,6 +116,18 @@ class HipOps:
         out, b = self.D.partition_lut_u32(keys, t, shift, nbuckets, out=self.empty(keys.numel()))
         return out, b.cpu().numpy().view(np.uint32).astype(np.int64)
 
+    def partition_lut_t(self, keys, lut, shift, nbuckets):
+        """As partition_lut with the table and the bucket starts as device
+        tensors (no host synchronisation)."""
+        out, b = self.D.partition_lut_u32(keys, lut.contiguous(), shift, nbuckets, out=self.empty(keys.numel()))
+        return out, b.to(torch.int64) & 0xFFFFFFFF
+
+    def partition_lut_pairs_t(self, keys, vals, lut, shift, nbuckets):
+        n = keys.numel()
+        k, v, b = self.D.partition_lut_pairs_u64_u32(keys, vals, lut.contiguous(), shift, nbuckets,
+                                                      out_keys=self.empty64(n), out_vals=self.empty(n))
+        return k, v, b.to(torch.int64) & 0xFFFFFFFF
+
     def sample(self, keys, stride, block=4096):
         """Every `stride`-th block of `block` keys (all keys when few)."""
         nb = keys.numel() // block
@@ -144,6 +156,16 @@ def _allgather_np(vec, ref_tensor, group):
     return np.stack([o.cpu().numpy() for o in outs])
 
 
+def _allgather_t(t, group):
+    """All-gather a small 1-D int64 tensor without leaving its device (no
+    host synchronisation under RCCL); returns [R, len] on t's device."""
+    R = dist.get_world_size(group)
+    src = t.cpu() if (_host_staged(group) and t.is_cuda) else t
+    outs = [torch.empty_like(src) for _ in range(R)]
+    dist.all_gather(outs, src, group=group)
+    return torch.stack(outs).to(t.device)
+
+
 def _alltoallv(send, send_counts, recv_counts, ops, group):
     """all_to_all_single with uneven splits (alltoallv): contiguous slices."""
     recv = ops.empty(int(np.sum(recv_counts)))
@@ -158,11 +180,30 @@ def _alltoallv(send, send_counts, recv_counts, ops, group):
     return recv
 
 
-def _alltoallv_into(recv, send, send_counts, recv_counts, group, async_op=False):
-    """all_to_all_single into `recv`; returns the async work handle (or None).
-    Device tensors over gloo (the one-GPU rehearsal) are staged through host
-    memory synchronously; RCCL, and gloo on host tensors (the CPU tests), run
-    the same issue-now / wait-later path as the 8-GPU job."""
+class _Works:
+    """The point-to-point works of one exchange; wait() = wait for all (for
+    RCCL a stream-level dependency of the current stream)."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+
+
+def _alltoallv_into(recv, send, send_counts, recv_counts, group, async_op=False, self_local=True):
+    """alltoallv of contiguous slices into `recv` (pieces in source-rank
+    order) as one batch of point-to-point sends/receives (one RCCL group);
+    returns a handle whose wait() orders the caller after it (or None when
+    nothing was left in flight).  self_local: the rank's own piece is a local
+    device copy instead of a self send (RCCL moves ~360 GB/s even for a
+    self-copy; a plain copy is several times that).  Device tensors over gloo
+    (the one-GPU rehearsal) are staged through host memory synchronously; RCCL
+    and gloo on host tensors (the CPU tests) run the same issue-now /
+    wait-later path as the 8-GPU job."""
+    R = dist.get_world_size(group)
+    me = dist.get_rank(group)
     rs = [int(c) for c in recv_counts]
     ss = [int(c) for c in send_counts]
     if _host_staged(group) and send.is_cuda:
@@ -170,7 +211,28 @@ def _alltoallv_into(recv, send, send_counts, recv_counts, group, async_op=False)
         dist.all_to_all_single(r_host, send.cpu(), rs, ss, group=group)
         recv.copy_(r_host)
         return None
-    return dist.all_to_all_single(recv, send, rs, ss, group=group, async_op=async_op)
+    so = np.concatenate([[0], np.cumsum(ss)]).astype(np.int64)
+    ro = np.concatenate([[0], np.cumsum(rs)]).astype(np.int64)
+    peer = (lambda i: i) if group is None else (lambda i: dist.get_global_rank(group, i))
+    ops = []
+    for k in range(1, R + 1):  # receives and sends paired so every rank posts in the same order
+        i = (me + k) % R
+        j = (me - k) % R
+        if i == me and self_local:
+            if rs[me]:
+                recv[int(ro[me]):int(ro[me + 1])].copy_(send[int(so[me]):int(so[me + 1])])
+            continue
+        if ss[i]:
+            ops.append(dist.P2POp(dist.isend, send[int(so[i]):int(so[i + 1])], peer(i), group))
+        if rs[j]:
+            ops.append(dist.P2POp(dist.irecv, recv[int(ro[j]):int(ro[j + 1])], peer(j), group))
+    if not ops:
+        return None
+    works = _Works(dist.batch_isend_irecv(ops))
+    if not async_op:
+        works.wait()
+        return None
+    return works
 
 
 def shard_cut(N, R):
@@ -272,6 +334,23 @@ def plan_msd(H, R, hist_bits=HIST_BITS):
     return splitters, dest, n_recv
 
 
+def _plan_rounds_t(H, R, K, growth=1.6):
+    """plan_rounds on torch tensors, on H's device (the GPU under RCCL, so the
+    plan needs no host round trip).  Returns (lut uint8, est float64)."""
+    G = H.sum(dim=0).to(torch.float64)
+    T = G.sum().clamp(min=1.0)                                 # all-zero histograms -> one group
+    x = (torch.cumsum(G, 0) - G / 2.0) / T * R                 # rank coordinate of each bucket's middle
+    rank = torch.clamp(torch.floor(x).to(torch.int64), max=R - 1)
+    w = growth ** torch.arange(K, dtype=torch.float64, device=H.device)
+    cw = torch.cumsum(w, 0) / w.sum()
+    rnd = torch.clamp(torch.searchsorted(cw, (x - rank).contiguous(), right=True), max=K - 1)
+    grp = torch.cummax(rank * K + rnd, dim=0).values
+    rank, rnd = grp // K, grp % K
+    lut = (rnd * R + rank).to(torch.uint8)
+    est = torch.zeros(R, dtype=torch.float64, device=H.device).index_add_(0, rank, G)
+    return lut, est
+
+
 def plan_rounds(H, R, K, hist_bits=HIST_BITS, growth=1.6):
     """Contiguous top-bit bucket ranges for (rank, round) from the gathered
     (possibly sampled) histograms H[R, 2^b]: each rank gets about 1/R of the
@@ -279,21 +358,10 @@ def plan_rounds(H, R, K, hist_bits=HIST_BITS, growth=1.6):
     first round keeps the exchange before the first sort short; each later
     round's exchange hides behind the previous round's sort).  Group of a
     bucket: rank g // K, round g % K.  Returns (lut, est_per_rank) with lut[b]
-    = round * R + rank (the partition bucket)."""
-    G = H.sum(axis=0).astype(np.float64)
-    T = float(G.sum())
-    if T > 0:
-        x = (np.cumsum(G) - G / 2.0) / T * R                  # rank coordinate of each bucket's middle
-        rank = np.minimum(x.astype(np.int64), R - 1)
-        w = growth ** np.arange(K)
-        cw = np.cumsum(w) / w.sum()
-        rnd = np.minimum(np.searchsorted(cw, x - rank, side="right"), K - 1)
-        grp = np.maximum.accumulate(rank * K + rnd)
-    else:
-        grp = np.zeros(G.size, dtype=np.int64)
-    rank, rnd = grp // K, grp % K
-    lut = (rnd * R + rank).astype(np.uint8)
-    return lut, np.bincount(rank, weights=G, minlength=R)
+    = round * R + rank (the partition bucket).  numpy wrapper of
+    _plan_rounds_t, which sort_msd runs on the device."""
+    lut, est = _plan_rounds_t(torch.as_tensor(np.asarray(H, dtype=np.int64)), R, K, growth)
+    return lut.numpy(), est.numpy()
 
 
 def _group_range(lut, code, hist_bits=HIST_BITS):
@@ -305,26 +373,48 @@ def _group_range(lut, code, hist_bits=HIST_BITS):
     return int(idx[0]) << shift, (int(idx[-1]) + 1) << shift
 
 
-def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=4, sample_stride=16):
-    """Range-split rounds schedule; see module docstring."""
+def _mark(trace, label):
+    """Diagnostics: with a trace list, synchronise and record a timestamp."""
+    if trace is not None:
+        import time
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        trace.append((label, time.perf_counter()))
+
+
+def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=4, sample_stride=16, self_local=True,
+             trace=None):
+    """Range-split rounds schedule; see module docstring.  `trace` (a list)
+    records synchronised timestamps of the steps (diagnostics only)."""
     R = dist.get_world_size(group)
     r = dist.get_rank(group)
+    _mark(trace, "start")
     K = max(1, min(int(rounds), 256 // R))
     n = keys.numel()
+    NB = R * K
+    # histogram -> allgather -> plan -> partition -> allgather of the exact
+    # sizes, all on the device; ONE host transfer afterwards
     h = ops.histogram(ops.sample(keys, sample_stride), 32 - HIST_BITS, HIST_BITS)
-    hv = np.concatenate([h.cpu().numpy().astype(np.int64), [n]])
-    HN = _allgather_np(hv, keys, group)                       # [R, 4096 + 1]
-    H, n_all = HN[:, :-1], HN[:, -1]
+    dev = h.device
+    HN = _allgather_t(torch.cat([h.to(torch.int64), torch.tensor([n], dtype=torch.int64, device=dev)]), group)
+    lut_t, est_t = _plan_rounds_t(HN[:, :-1], R, K)
+    _mark(trace, "histogram+allgather+plan")
+    part, b_t = ops.partition_lut_t(keys, lut_t, 32 - HIST_BITS, NB)
+    sizes_t = torch.diff(b_t, append=torch.tensor([n], dtype=torch.int64, device=b_t.device))
+    C_t = _allgather_t(sizes_t, group)                         # [R, NB], bucket j = round * R + dest
+    host = torch.cat([C_t.flatten(), HN[:, -1], est_t.round().to(torch.int64), lut_t.to(torch.int64)]).cpu().numpy()
+    _mark(trace, "partition+allgather sizes")
+    C = host[:R * NB].reshape(R, NB)
+    n_all = host[R * NB:R * NB + R]
+    est = host[R * NB + R:R * NB + 2 * R]
+    lut = host[R * NB + 2 * R:].astype(np.uint8)
     N = int(n_all.sum())
     S, _ = shard_cut(N, R)
-    lut, est = plan_rounds(H, R, K)
-    hs = float(H.sum())
+    hs = float(est.sum())
     if N and hs and est.max() * N / hs > max_imbalance * S + 4096:
-        return sort_lsd(keys, ops, group)
-    NB = R * K
-    part, b = ops.partition_lut(keys, lut, 32 - HIST_BITS, NB)
-    sizes = np.diff(np.asarray(b, dtype=np.int64), append=n)    # bucket j = round * R + dest
-    C = _allgather_np(sizes, keys, group)                      # [R, NB]
+        return sort_lsd(keys, ops, group)                      # identical decision on every rank
+    sizes = C[r]
+    b = np.concatenate([[0], np.cumsum(sizes)[:-1]])
     recv_tot = np.array([int(C[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
     roff = np.concatenate([[0], np.cumsum(recv_tot)])
     recv = ops.empty(int(roff[-1]))
@@ -337,17 +427,20 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=4, s
         s0 = int(b[i * R])
         ss = sizes[i * R:(i + 1) * R]
         works.append(_alltoallv_into(recv[int(roff[i]):int(roff[i + 1])], part[s0:s0 + int(ss.sum())], ss,
-                                     C[:, i * R + r], group, async_op=True))
+                                     C[:, i * R + r], group, async_op=True, self_local=self_local))
     for i in range(K):
         if works[i] is not None:
             works[i].wait()                                    # stream-level: the sort waits on RCCL
         if recv_tot[i]:
             lo, hi = _group_range(lut, i * R + r)              # every key of the round lies in it
             ops.sort_range(recv[int(roff[i]):int(roff[i + 1])], lo, hi, out=out[int(roff[i]):int(roff[i + 1])])
+        _mark(trace, "round %d" % i)
     if not balance:
         return out
     n_recv = np.array([int(C[:, d::R].sum()) for d in range(R)], dtype=np.int64)
-    return _rebalance(out, n_recv, ops, group)
+    res = _rebalance(out, n_recv, ops, group)
+    _mark(trace, "rebalance")
+    return res
 
 
 def _rebalance_pairs(keys, vals, n_all, ops, group):
@@ -384,20 +477,23 @@ def distrib_sort_pairs(keys, vals, ops=None, group=None, rounds=4, sample_stride
     return _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride)
 
 
-def _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride):
+def _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride, self_local=True):
     """The round schedule of distrib_sort_pairs (any world size)."""
     R = dist.get_world_size(group)
     r = dist.get_rank(group)
     K = max(1, min(int(rounds), 256 // R))
     n = keys.numel()
-    h = ops.histogram(ops.sample_hi(keys, sample_stride), 32 - HIST_BITS, HIST_BITS)
-    HN = _allgather_np(np.concatenate([h.cpu().numpy().astype(np.int64), [n]]), keys, group)
-    H = HN[:, :-1]
-    lut, _ = plan_rounds(H, R, K)
     NB = R * K
-    pk, pv, b = ops.partition_lut_pairs(keys, vals, lut, 32 - HIST_BITS, NB)
-    sizes = np.diff(np.asarray(b, dtype=np.int64), append=n)
-    C = _allgather_np(sizes, keys, group)
+    h = ops.histogram(ops.sample_hi(keys, sample_stride), 32 - HIST_BITS, HIST_BITS)
+    dev = h.device
+    HN = _allgather_t(torch.cat([h.to(torch.int64), torch.tensor([n], dtype=torch.int64, device=dev)]), group)
+    lut_t, _ = _plan_rounds_t(HN[:, :-1], R, K)
+    pk, pv, b_t = ops.partition_lut_pairs_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
+    sizes_t = torch.diff(b_t, append=torch.tensor([n], dtype=torch.int64, device=b_t.device))
+    C_t = _allgather_t(sizes_t, group)
+    C = C_t.cpu().numpy()                                      # the one host transfer
+    sizes = C[r]
+    b = np.concatenate([[0], np.cumsum(sizes)[:-1]])
     recv_tot = np.array([int(C[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
     roff = np.concatenate([[0], np.cumsum(recv_tot)])
     T = int(roff[-1])
@@ -409,8 +505,10 @@ def _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride):
             continue
         s0, ss = int(b[i * R]), sizes[i * R:(i + 1) * R]
         a, z = int(roff[i]), int(roff[i + 1])
-        works.append((_alltoallv_into(rk[a:z], pk[s0:s0 + int(ss.sum())], ss, C[:, i * R + r], group, async_op=True),
-                      _alltoallv_into(rv[a:z], pv[s0:s0 + int(ss.sum())], ss, C[:, i * R + r], group, async_op=True)))
+        works.append((_alltoallv_into(rk[a:z], pk[s0:s0 + int(ss.sum())], ss, C[:, i * R + r], group, async_op=True,
+                                      self_local=self_local),
+                      _alltoallv_into(rv[a:z], pv[s0:s0 + int(ss.sum())], ss, C[:, i * R + r], group, async_op=True,
+                                      self_local=self_local)))
     for i in range(K):
         for w in works[i]:
             if w is not None:

@@ -87,6 +87,14 @@ class OracleOps:
         starts = np.concatenate([[0], np.cumsum(np.bincount(b, minlength=nbuckets))[:-1]])
         return self._t(x[np.argsort(b, kind="stable")]), starts.astype(np.int64)
 
+    def partition_lut_t(self, keys, lut, shift, nbuckets):
+        out, starts = self.partition_lut(keys, lut.numpy(), shift, nbuckets)
+        return out, self.torch.from_numpy(starts)
+
+    def partition_lut_pairs_t(self, keys, vals, lut, shift, nbuckets):
+        k, v, starts = self.partition_lut_pairs(keys, vals, lut.numpy(), shift, nbuckets)
+        return k, v, self.torch.from_numpy(starts)
+
     def sample(self, keys, stride, block=4096):
         nb = keys.numel() // block
         if stride <= 1 or nb < 4 * stride:

@@ -1,7 +1,8 @@
 """Runs the multi-GPU round schedules over a real RCCL communicator of one
-rank (RCCL refuses two ranks on one GPU): the K asynchronous
-all_to_all_single calls, their stream-level waits and the per-round sorts go
-through RCCL's kernels and stream exactly as on 8 GPUs.  Invoked by
+rank (RCCL refuses two ranks on one GPU): with self_local=False every piece
+is a send/receive through RCCL, so the K asynchronous exchanges, their
+stream-level waits and the per-round sorts go through RCCL's kernels and
+stream as on 8 GPUs.  Invoked by
 tests/test_gpu_distrib.py in a fresh process; prints OK on success."""
 import os
 import sys
@@ -27,7 +28,7 @@ def main():
     keys = D.populate_u32(n, first=99)
     ref = np.sort(keys.cpu().numpy().view(np.uint32))
     for rounds in (4, 1):
-        out = distrib.sort_msd(keys, ops, rounds=rounds)
+        out = distrib.sort_msd(keys, ops, rounds=rounds, self_local=False)  # self sends through RCCL
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy().view(np.uint32), ref), "msd rounds=%d" % rounds
     rng = np.random.default_rng(3)
@@ -36,7 +37,7 @@ def main():
     v = np.arange(m, dtype=np.uint32)
     kt = torch.from_numpy(k.view(np.int64)).cuda()
     vt = torch.from_numpy(v.view(np.int32)).cuda()
-    rk, rv = distrib._sort_pairs_rounds(kt, vt, ops, None, 4, 16)
+    rk, rv = distrib._sort_pairs_rounds(kt, vt, ops, None, 4, 16, self_local=False)
     torch.cuda.synchronize()
     o = np.argsort(k, kind="stable")
     assert np.array_equal(rk.cpu().numpy().view(np.uint64), k[o]), "pairs keys"

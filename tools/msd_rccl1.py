@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Times the msd round schedule over a one-rank RCCL communicator at 2^28
+keys (every step of the multi-GPU path except the network: sampled
+histogram, partition, RCCL self all_to_all per round, per-round range sorts)
+against the plain single-GPU sort.  python tools/msd_rccl1.py [rounds...]"""
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "gpu-radix-sort_amd")]
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29994")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    import pylibsort
+    import pylibsort.device as D
+    from pylibsort import distrib
+    pylibsort.setDigitBits(4)
+    ops = distrib.HipOps()
+    n = 1 << 28
+    keys = D.populate_u32(n)
+    out = torch.empty_like(keys)
+    tmp = torch.empty_like(keys)
+
+    def timed(fn, reps=10):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    res = {"plain_sort_ms": timed(lambda: D.sort_keys_u32(keys, out=out, tmp=tmp))}
+    for K in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
+        res["msd_rounds%d_selfcopy_ms" % K] = timed(lambda: distrib.sort_msd(keys, ops, rounds=K))
+        res["msd_rounds%d_via_rccl_ms" % K] = timed(lambda: distrib.sort_msd(keys, ops, rounds=K, self_local=False))
+    print({k: round(v, 3) for k, v in res.items()})
+    for K in (1, 4):
+        tr = []
+        distrib.sort_msd(keys, ops, rounds=K, trace=tr)
+        print("trace K=%d:" % K, ", ".join("%s %.3f ms" % (tr[i][0], 1e3 * (tr[i][1] - tr[i - 1][1]))
+                                          for i in range(1, len(tr))))
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
