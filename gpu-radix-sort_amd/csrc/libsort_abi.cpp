@@ -517,6 +517,42 @@ LIBSORT_EXPORT int libsortSortPairsU64U32(const uint64_t* d_kin, const uint32_t*
              : 0;
 }
 
+LIBSORT_EXPORT int libsortSortKeysU64(const uint64_t* d_in, uint64_t* d_out, uint64_t* d_tmp, size_t n,
+                                      uint32_t offset, uint32_t width, void* stream) {
+  if (!check_range(n, offset, width, 64)) return 0;
+  if (n > 0 && (!d_in || !d_out || !d_tmp || d_tmp == d_out || (const uint64_t*)d_tmp == d_in)) {
+    set_error("libsortSortKeysU64: need distinct d_tmp (d_in may equal d_out)");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(sort_u64(ws, d_in, d_out, d_tmp, n, (int)offset, (int)(offset + width),
+                                  g_digit_bits.load(), st),
+                         "libsortSortKeysU64");
+         })
+             ? 1
+             : 0;
+}
+
+LIBSORT_EXPORT int libsortSortPairsU64U64(const uint64_t* d_kin, const uint64_t* d_vin, uint64_t* d_kout,
+                                          uint64_t* d_vout, uint64_t* d_ktmp, uint64_t* d_vtmp, size_t n,
+                                          uint32_t offset, uint32_t width, void* stream) {
+  if (!check_range(n, offset, width, 64)) return 0;
+  if (n > 0 && (d_ktmp == d_kout || (const uint64_t*)d_ktmp == d_kin || d_vtmp == d_vout ||
+                (const uint64_t*)d_vtmp == d_vin)) {
+    set_error("libsortSortPairsU64U64: scratch buffers must not alias input/output");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(sort_pairs_u64_u64(ws, d_kin, d_vin, d_kout, d_vout, d_ktmp, d_vtmp, n,
+                                            (int)offset, (int)(offset + width), g_digit_bits.load(), st),
+                         "libsortSortPairsU64U64");
+         })
+             ? 1
+             : 0;
+}
+
 LIBSORT_EXPORT int libsortSortPairsU32U32(const uint32_t* d_kin, const uint32_t* d_vin, uint32_t* d_kout,
                                           uint32_t* d_vout, uint32_t* d_ktmp, uint32_t* d_vtmp, size_t n,
                                           uint32_t offset, uint32_t width, void* stream) {

@@ -109,6 +109,11 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
 hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t* vin,
                               uint32_t* kout, uint32_t* vout, uint32_t* ktmp, uint32_t* vtmp,
                               size_t n, int lo, int hi, int digit_bits, hipStream_t stream);
+hipError_t sort_u64(Workspace& ws, const uint64_t* in, uint64_t* out, uint64_t* tmp, size_t n, int lo, int hi,
+                    int digit_bits, hipStream_t stream);
+hipError_t sort_pairs_u64_u64(Workspace& ws, const uint64_t* kin, const uint64_t* vin,
+                              uint64_t* kout, uint64_t* vout, uint64_t* ktmp, uint64_t* vtmp,
+                              size_t n, int lo, int hi, int digit_bits, hipStream_t stream);
 hipError_t sort_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin,
                               uint64_t* kout, uint32_t* vout, uint64_t* ktmp, uint32_t* vtmp,
                               size_t n, int lo, int hi, int digit_bits, hipStream_t stream);

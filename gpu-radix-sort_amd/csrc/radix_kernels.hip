@@ -1752,6 +1752,17 @@ hipError_t sort_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t
   return sort_impl<uint64_t, uint32_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, lo, hi, digit_bits, st);
 }
 
+hipError_t sort_u64(Workspace& ws, const uint64_t* in, uint64_t* out, uint64_t* tmp, size_t n, int lo, int hi,
+                    int digit_bits, hipStream_t st) {
+  return sort_impl<uint64_t, NoValue>(ws, in, out, tmp, nullptr, nullptr, nullptr, n, lo, hi, digit_bits, st);
+}
+
+hipError_t sort_pairs_u64_u64(Workspace& ws, const uint64_t* kin, const uint64_t* vin, uint64_t* kout,
+                              uint64_t* vout, uint64_t* ktmp, uint64_t* vtmp, size_t n, int lo, int hi,
+                              int digit_bits, hipStream_t st) {
+  return sort_impl<uint64_t, uint64_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, lo, hi, digit_bits, st);
+}
+
 hipError_t histogram_u32(Workspace& ws, const uint32_t* keys, size_t n, int shift, int bits,
                          uint32_t* d_hist, hipStream_t st) {
   if (bits < 1 || bits > 16 || shift < 0 || shift + bits > 32 || n > 0xffffffffull)

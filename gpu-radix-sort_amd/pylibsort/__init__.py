@@ -4,7 +4,9 @@ Mirrors the reference binding faasTest/pylibsort (__init__.py:5-26, sort.py,
 data.py:313-317): the same module-level functions (sortFull, sortPartial,
 generateInputs, checkPartial, ...) over the same C ABI, loaded with ctypes.
 On top of that it exposes the device-resident entry points for torch tensors
-(pylibsort.device) and the multi-GPU driver (pylibsort.distrib).
+(pylibsort.device), the multi-GPU driver (pylibsort.distrib), the file
+distributed arrays of data.py (pylibsort.data) and the FaaS worker of
+faasTest/f.py (pylibsort.faas).
 
 Library lookup order: $LIBSORT_PATH, the in-tree build
 (gpu-radix-sort_amd/libsort.so), then the reference's own lookup,
@@ -44,6 +46,10 @@ _SIGS = [
     ("libsortSortKeysRangeU32", ctypes.c_int,
      [_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, _vp]),
     ("libsortSortPairsU64U32", ctypes.c_int,
+     [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp]),
+    ("libsortSortKeysU64", ctypes.c_int,
+     [_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp]),
+    ("libsortSortPairsU64U64", ctypes.c_int,
      [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     ("libsortSortPairsU32U32", ctypes.c_int,
      [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp]),
@@ -122,4 +128,5 @@ def require_gpu():
         raise RuntimeError("libsort: no HIP device (initLibSort failed: %s)" % last_error())
 
 
+from .data import *  # noqa: E402,F401,F403
 from .sort import *  # noqa: E402,F401,F403

@@ -97,6 +97,40 @@ def sort_pairs_u64_u32(keys, vals, out_keys=None, out_vals=None, tmp_keys=None, 
     return ok_, ov
 
 
+def sort_keys_u64(keys, out=None, tmp=None, offset=0, width=None):
+    """Stable LSD sort of bits [offset, offset+width) of uint64 keys (int64
+    carrier).  Returns `out`."""
+    _need(keys, _U64, "keys")
+    if width is None:
+        width = 64 - offset
+    out = torch.empty_like(keys) if out is None else out
+    tmp = torch.empty_like(keys) if tmp is None else tmp
+    _need(out, _U64, "out")
+    _need(tmp, _U64, "tmp")
+    _check(_lib().libsortSortKeysU64(_ptr(keys), _ptr(out), _ptr(tmp), keys.numel(), offset, width, _stream()),
+           "libsortSortKeysU64")
+    return out
+
+
+def sort_pairs_u64_u64(keys, vals, out_keys=None, out_vals=None, tmp_keys=None, tmp_vals=None,
+                       offset=0, width=None):
+    """Stable sort of (uint64 key, uint64 payload) pairs by key bits."""
+    _need(keys, _U64, "keys")
+    _need(vals, _U64, "vals")
+    if keys.numel() != vals.numel():
+        raise ValueError("keys and vals differ in length")
+    if width is None:
+        width = 64 - offset
+    ok_ = torch.empty_like(keys) if out_keys is None else out_keys
+    ov = torch.empty_like(vals) if out_vals is None else out_vals
+    tk = torch.empty_like(keys) if tmp_keys is None else tmp_keys
+    tv = torch.empty_like(vals) if tmp_vals is None else tmp_vals
+    _check(_lib().libsortSortPairsU64U64(_ptr(keys), _ptr(vals), _ptr(ok_), _ptr(ov), _ptr(tk),
+                                         _ptr(tv), keys.numel(), offset, width, _stream()),
+           "libsortSortPairsU64U64")
+    return ok_, ov
+
+
 def sort_pairs_u32_u32(keys, vals, out_keys=None, out_vals=None, tmp_keys=None, tmp_vals=None,
                        offset=0, width=None):
     """Stable sort of (uint32 key, uint32 payload) pairs by key bits."""

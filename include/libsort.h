@@ -100,6 +100,19 @@ LIBSORT_API bool libsortSortPairsU64U32(const uint64_t* d_kin, const uint32_t* d
                                         uint64_t* d_ktmp, uint32_t* d_vtmp, size_t n,
                                         uint32_t offset, uint32_t width, void* stream);
 
+/* Sort of 64-bit keys by bits [offset, offset+width) (width = 64 - offset for
+ * a full sort; stable).  Same buffer rules as libsortSortKeysU32 (d_in may
+ * equal d_out, d_tmp distinct).  SURVEY.md §8(f) row 4: 64-bit keys beyond C5. */
+LIBSORT_API bool libsortSortKeysU64(const uint64_t* d_in, uint64_t* d_out, uint64_t* d_tmp,
+                                    size_t n, uint32_t offset, uint32_t width, void* stream);
+
+/* Stable key-value sort: 64-bit keys, 64-bit payloads (e.g. row ids past
+ * 2^32 or packed records). */
+LIBSORT_API bool libsortSortPairsU64U64(const uint64_t* d_kin, const uint64_t* d_vin,
+                                        uint64_t* d_kout, uint64_t* d_vout,
+                                        uint64_t* d_ktmp, uint64_t* d_vtmp, size_t n,
+                                        uint32_t offset, uint32_t width, void* stream);
+
 /* Stable key-value sort: 32-bit keys, 32-bit payloads. */
 LIBSORT_API bool libsortSortPairsU32U32(const uint32_t* d_kin, const uint32_t* d_vin,
                                         uint32_t* d_kout, uint32_t* d_vout,

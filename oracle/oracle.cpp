@@ -239,4 +239,24 @@ void oracle_stable_sort_kv32(uint32_t* k, uint32_t* v, size_t n) {
   }
 }
 
+// 64-bit keys only / with 64-bit payloads (no
+// reference function: std::sort defines the keys-only result, std::stable_sort
+// by key over the original order the pair result).
+void oracle_sort_u64(uint64_t* k, size_t n) { std::sort(k, k + n); }
+
+void oracle_stable_sort_kv64v64(uint64_t* k, uint64_t* v, size_t n) {
+  std::vector<size_t> idx(n);
+  for (size_t i = 0; i < n; ++i) idx[i] = i;
+  std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return k[x] < k[y]; });
+  std::vector<uint64_t> kk(n), vv(n);
+  for (size_t i = 0; i < n; ++i) {
+    kk[i] = k[idx[i]];
+    vv[i] = v[idx[i]];
+  }
+  if (n) {
+    memcpy(k, kk.data(), n * sizeof(uint64_t));
+    memcpy(v, vv.data(), n * sizeof(uint64_t));
+  }
+}
+
 }  // extern "C"

@@ -39,6 +39,8 @@ def lib():
         L.oracle_distrib_bsp_u32.argtypes = [_u32p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _u64p]
         L.oracle_stable_sort_kv64.argtypes = [_u64p, _u32p, ctypes.c_size_t]
         L.oracle_stable_sort_kv32.argtypes = [_u32p, _u32p, ctypes.c_size_t]
+        L.oracle_sort_u64.argtypes = [_u64p, ctypes.c_size_t]
+        L.oracle_stable_sort_kv64v64.argtypes = [_u64p, _u64p, ctypes.c_size_t]
         _lib = L
     return _lib
 
@@ -133,4 +135,17 @@ def stable_sort_kv32(k, v):
     kk = np.array(k, dtype=np.uint32, copy=True)
     vv = np.array(v, dtype=np.uint32, copy=True)
     lib().oracle_stable_sort_kv32(_p32(kk), _p32(vv), kk.size)
+    return kk, vv
+
+
+def sort_u64(k):
+    kk = np.array(k, dtype=np.uint64, copy=True)
+    lib().oracle_sort_u64(_p64(kk), kk.size)
+    return kk
+
+
+def stable_sort_kv64v64(k, v):
+    kk = np.array(k, dtype=np.uint64, copy=True)
+    vv = np.array(v, dtype=np.uint64, copy=True)
+    lib().oracle_stable_sort_kv64v64(_p64(kk), _p64(vv), kk.size)
     return kk, vv

@@ -136,3 +136,27 @@ def test_shard_cut_matches_reference():
     # distrib.go:113: maxPerWorker = ceil(N / nworker)
     assert shard_cut(1111, 2) == (556, [(0, 556), (556, 1111)])
     assert shard_cut(10, 4)[1] == [(0, 3), (3, 6), (6, 9), (9, 10)]
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_msd_bench_world_sizes_gloo(tmp_path, world):
+    """The world sizes of the driver's scaling job (4 and 8 ranks) with the
+    bench's default schedule (msd, 4 rounds -> 16 / 32 partition buckets)."""
+    from oracle import oracle
+    x = oracle.pcg(8 * 20011, first=world)
+    shards = run_ranks(x, world, "msd", tmp_path, port=29900 + world)
+    np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))
+    assert [s.size for s in shards] == [s.size for s in shard_inputs(x, world)]
+
+
+def test_distrib_pairs_eight_ranks_gloo(tmp_path):
+    """C5 at the world size it is quoted on (8 ranks, 4 rounds)."""
+    from distrib_helpers import run_pair_ranks
+    from oracle import oracle
+    rng = np.random.default_rng(88)
+    n = 8 * 5003
+    k = rng.integers(0, 1 << 12, n, dtype=np.uint64) * np.uint64(0x0010000100000001)
+    ks, vs = run_pair_ranks(k, 8, tmp_path, port=29920, kw={"rounds": 4})
+    rk, rv = oracle.stable_sort_kv64(k, np.arange(n, dtype=np.uint32))
+    np.testing.assert_array_equal(np.concatenate(ks), rk)
+    np.testing.assert_array_equal(np.concatenate(vs), rv)

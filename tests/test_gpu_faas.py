@@ -1,0 +1,86 @@
+"""The FaaS worker on the GPU: faasTest/f.py's
+request flow -- input partitions read from file arrays, gpuPartial, output
+array with one partition per radix group -- through pylibsort.faas.f (host
+ABI, as the reference) and fDevice (device-resident sort, D2H into the mapped
+output file).  The 1021-key case must reproduce, byte for byte, the array the
+reference's own data layer writes for that input (tests/golden/faas)."""
+import io
+import json
+import pathlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLD = pathlib.Path(__file__).resolve().parent / "golden" / "faas"
+
+
+@pytest.fixture
+def mount(tmp_path):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from pylibsort import data as D
+    D.SetDistribMount(tmp_path)
+    yield tmp_path
+    D.closeOpenArrays()
+
+
+def _make_inputs(D, root, x, narr, npart, prefix):
+    """x split over narr arrays of npart uniform partitions (f.py:86-107)."""
+    raw = x.tobytes()
+    per = len(raw) // (narr * npart)
+    refs = []
+    for a in range(narr):
+        name = "%s%d" % (prefix, a)
+        arr = D.fileDistribArray.Create(root / name, D.ArrayShape.fromUniform(per, npart))
+        arr.WriteAll(raw[a * npart * per:(a + 1) * npart * per])
+        arr.Close()
+        refs += [{"arrayName": name, "partID": p, "start": 0, "nbyte": -1} for p in range(npart)]
+    return refs
+
+
+@pytest.mark.parametrize("handler", ["f", "fDevice"])
+def test_worker_matches_reference_array(mount, oracle_mod, handler):
+    from pylibsort import data as D
+    from pylibsort import faas
+    x = oracle_mod.pcg(1021)
+    # 1021 keys do not split evenly: one array, one partition of the whole input
+    refs = _make_inputs(D, mount, x, 1, 1, "in")
+    req = {"offset": 0, "width": 8, "arrType": "file", "input": refs, "output": "out"}
+    assert getattr(faas, handler)(req) == {"success": True, "err": ""}
+    for f in ("meta.json", "data.dat"):
+        assert (mount / "out" / f).read_bytes() == (GOLD / "out_1021_w8" / f).read_bytes(), f
+
+
+@pytest.mark.parametrize("handler", ["f", "fDevice"])
+@pytest.mark.parametrize("offset,width", [(0, 8), (8, 8), (0, 16), (5, 3)])
+def test_worker_partial_sort(mount, oracle_mod, handler, offset, width):
+    from pylibsort import data as D
+    from pylibsort import faas
+    n = 1 << 18
+    x = oracle_mod.pcg(n, first=offset * 1000 + width)
+    refs = _make_inputs(D, mount, x, 2, 2, "a")
+    req = {"offset": offset, "width": width, "arrType": "file", "input": refs, "output": "o"}
+    assert getattr(faas, handler)(req)["success"]
+    out = D.fileDistribArray.Open(mount / "o")
+    got = np.frombuffer(out.ReadAll(), dtype=np.uint32)
+    d, b = oracle_mod.partial_u32(x, offset, width)
+    np.testing.assert_array_equal(got, d)
+    assert out.shape.caps == np.diff(b.astype(np.int64) * 4, append=4 * n).tolist()
+    assert out.shape.lens == out.shape.caps
+    out.Close()
+
+
+def test_direct_invoke(mount, oracle_mod, monkeypatch):
+    from pylibsort import data as D
+    from pylibsort import faas
+    x = oracle_mod.pcg(4096, first=3)
+    refs = _make_inputs(D, mount, x, 2, 2, "d")
+    monkeypatch.setenv("OL_SHARED_VOLUME", str(mount))
+    req = {"offset": 4, "width": 4, "arrType": "file", "input": refs, "output": "dout"}
+    out = io.StringIO()
+    assert faas.directInvoke(["--device"], stdin=io.StringIO(json.dumps(req)), stdout=out) == 0
+    assert json.loads(out.getvalue()) == {"success": True, "err": ""}
+    got = np.fromfile(mount / "dout" / "data.dat", dtype=np.uint32)
+    np.testing.assert_array_equal(got, oracle_mod.partial_u32(x, 4, 4)[0])

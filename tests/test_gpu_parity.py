@@ -161,6 +161,36 @@ def test_pairs_u64_u32_stable(dev, oracle_mod, digit_bits, n):
     np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint32), rv)
 
 
+@pytest.mark.parametrize("n", [1, 2049, 300007])
+@pytest.mark.parametrize("offset,width", [(0, 64), (0, 40), (17, 31), (32, 32)])
+def test_keys_u64(dev, oracle_mod, digit_bits, n, offset, width):
+    rng = np.random.default_rng(n + offset)
+    k = rng.integers(0, 1 << 63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+    k[: n // 3] &= np.uint64(0xFFFF0000FFFF)  # duplicates and zero digits
+    kt = torch.from_numpy(k.view(np.int64)).cuda()
+    out = dev.sort_keys_u64(kt, offset=offset, width=width)
+    if (offset, width) == (0, 64):
+        ref = oracle_mod.sort_u64(k)
+    else:  # stable by the digit field: the same permutation as a stable pair sort
+        field = (k >> np.uint64(offset)) & np.uint64((1 << width) - 1)
+        _, idx = oracle_mod.stable_sort_kv64v64(field, np.arange(n, dtype=np.uint64))
+        ref = k[idx.astype(np.int64)]
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), ref)
+
+
+@pytest.mark.parametrize("n", [1, 2049, 300007])
+def test_pairs_u64_u64_stable(dev, oracle_mod, digit_bits, n):
+    rng = np.random.default_rng(n)
+    k = rng.integers(0, 1 << 20, n, dtype=np.uint64) * np.uint64(0x100000001)  # many duplicates
+    v = rng.integers(0, 1 << 63, n, dtype=np.uint64) | (np.arange(n, dtype=np.uint64) << np.uint64(40))
+    kt = torch.from_numpy(k.view(np.int64)).cuda()
+    vt = torch.from_numpy(v.view(np.int64)).cuda()
+    ok_, ov = dev.sort_pairs_u64_u64(kt, vt)
+    rk, rv = oracle_mod.stable_sort_kv64v64(k, v)
+    np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), rk)
+    np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint64), rv)
+
+
 def test_pairs_u32_u32_stable(dev, oracle_mod, digit_bits):
     n = 123457
     rng = np.random.default_rng(1)

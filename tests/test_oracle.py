@@ -114,3 +114,14 @@ def test_kv_oracles_are_stable(oracle_mod):
     order = np.lexsort((v, k))
     np.testing.assert_array_equal(kk, k[order])
     np.testing.assert_array_equal(vv, v[order])
+
+
+def test_u64_oracles_match_numpy(oracle_mod):
+    rng = np.random.default_rng(7)
+    k = rng.integers(0, 1 << 12, 5000, dtype=np.uint64) << np.uint64(40)
+    v = rng.integers(0, 1 << 63, 5000, dtype=np.uint64)
+    np.testing.assert_array_equal(oracle_mod.sort_u64(k), np.sort(k))
+    idx = np.argsort(k, kind="stable")
+    rk, rv = oracle_mod.stable_sort_kv64v64(k, v)
+    np.testing.assert_array_equal(rk, k[idx])
+    np.testing.assert_array_equal(rv, v[idx])
