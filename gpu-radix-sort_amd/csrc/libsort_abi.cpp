@@ -283,6 +283,177 @@ static inline uint32_t rotr32(uint32_t x, uint32_t r) { return (x >> r) | (x << 
 // ---------------------------------------------------------------------------
 // host-pointer sorts
 // ---------------------------------------------------------------------------
+// Pipelined full sort of a host buffer (providedGpu).
+// The host ABI is PCIe-bound (measured on the box, tools/pcie_probe: 1 GiB
+// moves in ~19 ms each way, pageable and pinned alike, ~97 GB/s when both
+// directions run at once), so the sort itself is hidden behind the two
+// transfers:
+//   1. H2D in kPipeChunks chunks on the copy stream; chunk c is partitioned
+//      (stable, by a 12-bit top-bucket table -> kPipeGroups contiguous key
+//      ranges) on the compute stream while chunk c+1 is in flight.  The table
+//      comes from the histogram of chunk 0 (balance only; sizes are exact).
+//   2. After the last chunk: one small D2H of the chunk bucket starts, then
+//      per key range g (in key order): gather its chunk pieces into one
+//      contiguous slice at its final position (segment copy), sort the slice
+//      in place with the range-restricted sort (digits of key - lo), and D2H
+//      it on the copy stream while range g+1 is gathered and sorted.
+// Critical path: H2D + partition of the last chunk + gather/sort of range 0 +
+// D2H, instead of H2D + whole sort + D2H.  Bit-identical result (a full sort
+// is unique).
+constexpr int kPipeChunks = 8;
+constexpr int kPipeGroups = 16;
+constexpr int kPlanBits = 12;
+static_assert(kPipeChunks + kPipeGroups <= Workspace::kPipeEvents, "events");
+static_assert(3 * kPipeChunks * kPipeGroups * 2 <= 3 * 2 * 1024, "segment tables");
+
+static size_t env_pipeline_min() {
+  const char* s = getenv("LIBSORT_HOST_PIPELINE_MIN");  // keys; 0 disables the pipeline
+  if (!s) return (size_t)1 << 22;
+  const long long v = atoll(s);
+  return v <= 0 ? (size_t)-1 : (size_t)v;
+}
+
+// LIBSORT_PIPE_DEBUG=1: synchronise and check after every step (diagnostics).
+static bool pipe_checkpoint(const char* step, hipStream_t a, hipStream_t b) {
+  static const bool on = [] {
+    const char* s = getenv("LIBSORT_PIPE_DEBUG");
+    return s && s[0] == '1';
+  }();
+  if (!on) return true;
+  hipError_t e1 = hipStreamSynchronize(a), e2 = hipStreamSynchronize(b);
+  if (e1 != hipSuccess || e2 != hipSuccess) {
+    fprintf(stderr, "libsort pipeline: fault after step %s: %s\n", step,
+            hipGetErrorString(e1 != hipSuccess ? e1 : e2));
+    return false;
+  }
+  fprintf(stderr, "libsort pipeline: ok after %s\n", step);
+  return true;
+}
+
+static bool host_full_sort_pipelined(Workspace* ws, uint32_t* h, size_t len, int bits) {
+  hipStream_t st = ws->stream, cs = ws->copy_stream;
+  uint32_t* b0 = static_cast<uint32_t*>(ws->hbuf[0]);
+  uint32_t* b1 = static_cast<uint32_t*>(ws->hbuf[1]);
+  uint32_t* b2 = static_cast<uint32_t*>(ws->pbuf);
+  const size_t piece = ((len + kPipeChunks - 1) / kPipeChunks + 8191) & ~(size_t)8191;
+  const int nch = (int)((len + piece - 1) / piece);
+  // plan block layout (device and pinned mirror): hist[4096] | lut bytes[4096]
+  // | chunk bucket starts[1024] | segment tables (uint64)
+  uint32_t* d_hist = ws->plan_dev;
+  uint8_t* d_lut = reinterpret_cast<uint8_t*>(ws->plan_dev + 4096);
+  uint32_t* d_bnd = ws->plan_dev + 4096 + 1024;
+  uint64_t* d_tab = reinterpret_cast<uint64_t*>(ws->plan_dev + 4096 + 2048);
+  uint32_t* H = ws->plan_host;
+  uint8_t* lut = reinterpret_cast<uint8_t*>(H + 4096);
+  uint32_t* bnd = H + 4096 + 1024;
+  uint64_t* tab = reinterpret_cast<uint64_t*>(H + 4096 + 2048);
+  hipEvent_t* ev = ws->pipe_evt;
+  uint64_t lo[kPipeGroups], hi[kPipeGroups];
+  bool ok = true;
+  for (int c = 0; ok && c < nch; ++c) {
+    const size_t off = (size_t)c * piece, m = std::min(piece, len - off);
+    ok = hip_ok(hipMemcpyAsync(b0 + off, h + off, m * sizeof(uint32_t), hipMemcpyHostToDevice, cs), "H2D chunk") &&
+         hip_ok(hipEventRecord(ev[c], cs), "hipEventRecord") && hip_ok(hipStreamWaitEvent(st, ev[c], 0), "wait");
+    if (ok && c == 0) {
+      ok = hip_ok(histogram_u32(*ws, b0, m, 32 - kPlanBits, kPlanBits, d_hist, st), "plan histogram") &&
+           hip_ok(hipMemcpyAsync(H, d_hist, 4096 * sizeof(uint32_t), hipMemcpyDeviceToHost, st), "D2H hist") &&
+           hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+      if (!ok) break;
+      // contiguous bucket ranges of about equal (sampled) size, in key order
+      uint64_t total = 0;
+      for (int b = 0; b < 4096; ++b) total += H[b];
+      uint64_t acc = 0;
+      int prev = 0;
+      for (int g = 0; g < kPipeGroups; ++g) lo[g] = hi[g] = 0;
+      for (int b = 0; b < 4096; ++b) {
+        int g = total ? (int)((2 * acc + H[b]) * kPipeGroups / (2 * total)) : 0;
+        g = std::max(prev, std::min(g, kPipeGroups - 1));
+        if (hi[g] == 0) lo[g] = (uint64_t)b << (32 - kPlanBits);
+        hi[g] = (uint64_t)(b + 1) << (32 - kPlanBits);
+        lut[b] = (uint8_t)g;
+        prev = g;
+        acc += H[b];
+      }
+      ok = hip_ok(hipMemcpyAsync(d_lut, lut, 4096, hipMemcpyHostToDevice, st), "H2D plan") &&
+           pipe_checkpoint("plan", st, cs);
+    }
+    if (ok)
+      ok = hip_ok(partition_lut_u32(*ws, b0 + off, b1 + off, m, d_lut, 32 - kPlanBits, kPipeGroups,
+                                    d_bnd + c * kPipeGroups, st),
+                  "chunk partition") &&
+           pipe_checkpoint("chunk partition", st, cs);
+  }
+  if (ok)
+    ok = hip_ok(hipMemcpyAsync(bnd, d_bnd, (size_t)nch * kPipeGroups * sizeof(uint32_t), hipMemcpyDeviceToHost, st),
+                "D2H bucket starts") &&
+         hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+  if (!ok) {
+    (void)hipStreamSynchronize(cs);
+    (void)hipStreamSynchronize(st);
+    return false;
+  }
+  uint64_t sz[kPipeChunks][kPipeGroups], T[kPipeGroups], G[kPipeGroups], maxlen[kPipeGroups];
+  uint64_t run = 0;
+  for (int g = 0; g < kPipeGroups; ++g) {
+    T[g] = maxlen[g] = 0;
+    for (int c = 0; c < nch; ++c) {
+      const uint64_t m = std::min(piece, len - (size_t)c * piece);
+      const uint64_t end = g + 1 < kPipeGroups ? bnd[c * kPipeGroups + g + 1] : m;
+      sz[c][g] = end - bnd[c * kPipeGroups + g];
+      T[g] += sz[c][g];
+      maxlen[g] = std::max(maxlen[g], sz[c][g]);
+    }
+    G[g] = run;
+    run += T[g];
+  }
+  for (int g = 0; g < kPipeGroups; ++g) {
+    uint64_t* t = tab + (size_t)g * 3 * nch;
+    uint64_t dst = G[g];
+    for (int c = 0; c < nch; ++c) {
+      t[c] = (uint64_t)c * piece + bnd[c * kPipeGroups + g];
+      t[nch + c] = dst;
+      t[2 * nch + c] = sz[c][g];
+      dst += sz[c][g];
+      // a malformed table would fault the gather: check it on the host
+      if (t[c] + sz[c][g] > std::min<uint64_t>((uint64_t)(c + 1) * piece, len) || dst > len) {
+        set_error("pipelined sort: inconsistent chunk bucket starts");
+        return false;
+      }
+    }
+  }
+  if (run != len) {
+    set_error("pipelined sort: bucket sizes do not add up");
+    return false;
+  }
+  ok = hip_ok(hipMemcpyAsync(d_tab, tab, (size_t)kPipeGroups * 3 * nch * sizeof(uint64_t), hipMemcpyHostToDevice, st),
+              "H2D segment tables");
+  // every range's gather + sort is queued before the first D2H (a pageable
+  // D2H may hold the host thread until it is done)
+  for (int g = 0; ok && g < kPipeGroups; ++g) {
+    if (!T[g]) continue;
+    const uint64_t span = hi[g] - lo[g] - 1;
+    int width = 0;
+    while (width < 32 && (span >> width) != 0) ++width;
+    ok = hip_ok(segment_copy_dev_u32(b1, b2, d_tab + (size_t)g * 3 * nch, nch, maxlen[g], T[g], st),
+                "range gather") &&
+         pipe_checkpoint("range gather", st, cs) &&
+         hip_ok(sort_u32(*ws, b2 + G[g], b2 + G[g], b0 + G[g], T[g], 0, std::max(width, 1), bits, nullptr, st,
+                         (uint32_t)lo[g]),
+                "range sort") &&
+         pipe_checkpoint("range sort", st, cs) &&
+         hip_ok(hipEventRecord(ev[kPipeChunks + g], st), "hipEventRecord");
+  }
+  for (int g = 0; ok && g < kPipeGroups; ++g) {
+    if (!T[g]) continue;
+    ok = hip_ok(hipStreamWaitEvent(cs, ev[kPipeChunks + g], 0), "wait") &&
+         hip_ok(hipMemcpyAsync(h + G[g], b2 + G[g], T[g] * sizeof(uint32_t), hipMemcpyDeviceToHost, cs), "D2H range") &&
+         pipe_checkpoint("D2H range", st, cs);
+  }
+  const bool synced = hip_ok(hipStreamSynchronize(cs), "hipStreamSynchronize") &&
+                      hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+  return ok && synced;
+}
+
 static bool host_sort(uint32_t* h, uint32_t* bounds, size_t len, uint32_t offset, uint32_t width,
                       bool partial) {
   Reservation res;
@@ -313,6 +484,14 @@ static bool host_sort(uint32_t* h, uint32_t* bounds, size_t len, uint32_t offset
   if (!ws_acquire_stream(ws->device, st)) return false;
   const int bits = g_digit_bits.load();
   const size_t bytes = len * sizeof(uint32_t);
+  static const size_t pipe_min = env_pipeline_min();
+  if (!partial && len >= pipe_min) {
+    bool ok = hip_ok(ws->ensure_hbuf(bytes), "hipMalloc(keys)") &&
+              hip_ok(ws->ensure_pipeline(bytes), "hipMalloc(pipeline)") &&
+              host_full_sort_pipelined(ws, h, len, bits);
+    ws_release_stream(ws->device, st);
+    return ok;
+  }
   const int lo = partial ? (int)offset : 0;
   const int hi = partial ? (int)(offset + width) : 32;
   const int P = num_passes(hi - lo, bits);

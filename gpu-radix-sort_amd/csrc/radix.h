@@ -65,6 +65,19 @@ struct Workspace {
 
   hipStream_t stream = nullptr;  // used by the host-pointer ABI
 
+  // pipelined host full sort (libsort_abi.cpp host_full_sort_pipelined): a
+  // third key buffer, a copy stream, the plan block on the device (histogram,
+  // partition table, chunk bucket starts, segment tables) and its pinned mirror
+  void* pbuf = nullptr;
+  size_t pbuf_cap = 0;  // bytes
+  hipStream_t copy_stream = nullptr;
+  uint32_t* plan_dev = nullptr;
+  uint32_t* plan_host = nullptr;
+  static constexpr size_t kPlanWords = 4096 + 1024 + 1024 + 3 * 2 * 1024;  // hist | lut | bounds | seg tables (u64)
+  static constexpr int kPipeEvents = 64;
+  hipEvent_t pipe_evt[kPipeEvents] = {};
+  hipError_t ensure_pipeline(size_t bytes);
+
   // onesweep path: two look-back status buffers [tiles][RADIX] and a small
   // block: window histograms | per-pass digit bases | tile counters | error
   uint32_t* os_status[2] = {nullptr, nullptr};
@@ -143,6 +156,11 @@ hipError_t partition_lut_u32(Workspace& ws, const uint32_t* in, uint32_t* out, s
 hipError_t partition_lut_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
                                        uint32_t* vout, size_t n, const uint8_t* d_lut, int lut_shift, int nbuckets,
                                        uint32_t* d_bounds, hipStream_t stream);
+// Segment copy with the table already on the device: d_tab = [src_off[nseg] |
+// dst_off[nseg] | len[nseg]] (uint64), nseg <= 65535; maxlen = the longest
+// segment (sizes the grid), total = sum of len (timing only).
+hipError_t segment_copy_dev_u32(const uint32_t* src, uint32_t* dst, const uint64_t* d_tab, size_t nseg,
+                                uint64_t maxlen, uint64_t total, hipStream_t stream);
 hipError_t segment_copy_u32(Workspace& ws, const uint32_t* src, uint32_t* dst, size_t nseg,
                             const uint64_t* src_off, const uint64_t* dst_off, const uint64_t* len,
                             hipStream_t stream);

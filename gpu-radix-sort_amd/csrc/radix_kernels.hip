@@ -1208,6 +1208,32 @@ __global__ void k_segment_copy(const uint32_t* __restrict__ src, uint32_t* __res
   }
 }
 
+// Few large segments: block (x, y) copies elements [x*4096, (x+1)*4096) of
+// segment y (blocks past the segment's end exit).
+constexpr int kSegPiece = 4096;
+__global__ __launch_bounds__(256) void k_segment_copy2d(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                        const uint64_t* __restrict__ tab, uint32_t nseg) {
+  const uint32_t s = blockIdx.y;
+  const uint64_t len = tab[2 * nseg + s];
+  const uint64_t a = (uint64_t)blockIdx.x * kSegPiece;
+  if (a >= len) return;
+  const uint32_t* sp = src + tab[s] + a;
+  uint32_t* dp = dst + tab[nseg + s] + a;
+  // (written as a branch on the remainder: a umin64 here compiled to an
+  // s_cselect on a stale SCC, i.e. m = 4096 in the partial branch)
+  const uint64_t rem = len - a;
+  if (rem >= (uint64_t)kSegPiece) {
+    uint32_t v[kSegPiece / 256];
+#pragma unroll
+    for (int j = 0; j < kSegPiece / 256; ++j) v[j] = sp[threadIdx.x + j * 256];
+#pragma unroll
+    for (int j = 0; j < kSegPiece / 256; ++j) dp[threadIdx.x + j * 256] = v[j];
+  } else {
+    const uint32_t m = (uint32_t)rem;
+    for (uint32_t j = threadIdx.x; j < m; j += 256) dp[j] = sp[j];
+  }
+}
+
 // ----------------------------------------------------------------------------
 // PCG32 stream on the device (utils.cu:65-80 + LCG skip-ahead)
 // ----------------------------------------------------------------------------
@@ -1300,6 +1326,19 @@ hipError_t Workspace::ensure_bounds(size_t m) {
   return hipSuccess;
 }
 
+hipError_t Workspace::ensure_pipeline(size_t bytes) {
+  if (!copy_stream) LS_TRY(hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking));
+  for (auto& e : pipe_evt)
+    if (!e) LS_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  if (!plan_dev) LS_TRY(hipMalloc(&plan_dev, kPlanWords * sizeof(uint32_t)));
+  if (!plan_host) LS_TRY(hipHostMalloc(&plan_host, kPlanWords * sizeof(uint32_t), hipHostMallocDefault));
+  if (bytes <= pbuf_cap) return hipSuccess;
+  if (pbuf) { (void)hipFree(pbuf); pbuf = nullptr; }
+  pbuf_cap = 0;
+  LS_TRY(hipMalloc(&pbuf, bytes));
+  pbuf_cap = bytes;
+  return hipSuccess;
+}
 hipError_t Workspace::ensure_seg(size_t m) {
   if (!seg_evt) LS_TRY(hipEventCreateWithFlags(&seg_evt, hipEventDisableTiming));
   if (m <= seg_cap) return hipSuccess;
@@ -1369,6 +1408,13 @@ void Workspace::release() {
   tc_cap = tb_cap = 0;
   os_status_cap = 0;
   if (seg_host) (void)hipHostFree(seg_host);
+  if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+  if (pbuf) (void)hipFree(pbuf);
+  if (plan_dev) (void)hipFree(plan_dev);
+  if (plan_host) (void)hipHostFree(plan_host);
+  pbuf = nullptr;
+  plan_dev = plan_host = nullptr;
+  pbuf_cap = 0;
   counts = scan_l1 = scan_l2 = dbounds = hist_tmp = nullptr;
   hbuf[0] = hbuf[1] = nullptr;
   seg_dev = seg_host = nullptr;
@@ -1873,6 +1919,18 @@ hipError_t partition_lut_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const
                                        uint32_t* vout, size_t n, const uint8_t* d_lut, int lut_shift, int nbuckets,
                                        uint32_t* d_bounds, hipStream_t st) {
   return partition_lut_any<uint64_t, uint32_t>(ws, kin, kout, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st);
+}
+
+hipError_t segment_copy_dev_u32(const uint32_t* src, uint32_t* dst, const uint64_t* d_tab, size_t nseg,
+                                uint64_t maxlen, uint64_t total, hipStream_t st) {
+  if (nseg == 0 || maxlen == 0) return hipSuccess;
+  if (nseg > 65535) return hipErrorInvalidValue;
+  ScopedTimer tm("segcopy", st, total);
+  const uint64_t px = (maxlen + kSegPiece - 1) / kSegPiece;
+  if (px > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_segment_copy2d, dim3((uint32_t)px, (uint32_t)nseg), dim3(256), 0, st, src, dst, d_tab,
+                     (uint32_t)nseg);
+  return hipGetLastError();
 }
 
 hipError_t segment_copy_u32(Workspace& ws, const uint32_t* src, uint32_t* dst, size_t nseg,

@@ -324,6 +324,48 @@ def test_host_abi_concurrent_callers(dev, oracle_mod):
         assert all(ex.map(work, range(32)))
 
 
+@pytest.mark.parametrize("kind", ["pcg", "ragged", "equal", "narrow", "heavy_bucket", "sorted", "reverse"])
+def test_host_full_sort_pipelined(dev, oracle_mod, kind):
+    """providedGpu at >= 2^22 keys takes the pipelined path (chunked H2D with
+    per-chunk range partition, per-range gather + sort + D2H): bit-identical
+    to std::sort for every distribution, including one where all keys fall
+    in one range (no overlap possible) and ragged sizes."""
+    import pylibsort
+    rng = np.random.default_rng(len(kind))
+    n = (1 << 22) + (12345 if kind == "ragged" else 0)
+    if kind in ("pcg", "ragged", "sorted", "reverse"):
+        x = oracle_mod.pcg(n, first=17)
+        if kind == "sorted":
+            x = np.sort(x)
+        elif kind == "reverse":
+            x = np.sort(x)[::-1].copy()
+    elif kind == "equal":
+        x = np.full(n, 0xDEADBEEF, dtype=np.uint32)
+    elif kind == "narrow":
+        x = (0x7FF00000 + rng.integers(0, 1 << 19, n)).astype(np.uint32)
+    else:  # half the keys in one 12-bit top bucket, the rest uniform
+        x = oracle_mod.pcg(n, first=99)
+        x[: n // 2] = (0x12300000 + rng.integers(0, 1 << 20, n // 2)).astype(np.uint32)
+    buf = bytearray(x.tobytes())
+    pylibsort.sortFull(buf)
+    np.testing.assert_array_equal(np.frombuffer(buf, dtype=np.uint32), oracle_mod.sort_u32(x))
+
+
+def test_host_full_sort_pipelined_concurrent(dev, oracle_mod):
+    """Concurrent large providedGpu callers share the device's workspace."""
+    import concurrent.futures as cf
+    import pylibsort
+    xs = [oracle_mod.pcg((1 << 22) + 1000 * i, first=i << 24) for i in range(4)]
+
+    def work(i):
+        buf = bytearray(xs[i].tobytes())
+        pylibsort.sortFull(buf)
+        return np.array_equal(np.frombuffer(buf, dtype=np.uint32), oracle_mod.sort_u32(xs[i]))
+
+    with cf.ThreadPoolExecutor(4) as ex:
+        assert all(ex.map(work, range(4)))
+
+
 def test_reference_localtest_harness(dev):
     # The reference's own localTest runTests (tests.cpp:88-161: gpuPartial,
     # providedGpu, providedCpu, distribSort with two concurrent gpuPartial
