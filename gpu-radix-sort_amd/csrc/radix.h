@@ -165,6 +165,13 @@ hipError_t segment_copy_u32(Workspace& ws, const uint32_t* src, uint32_t* dst, s
                             const uint64_t* src_off, const uint64_t* dst_off, const uint64_t* len,
                             hipStream_t stream);
 hipError_t populate_device(uint32_t* out, size_t n, uint64_t first, hipStream_t stream);
+// Multi-GPU round plan: sampled 12-bit top-bucket histogram as an int64 row
+// with n appended (d_out: 4097 entries), and the (rank, round) table of
+// sort_msd from the gathered rows (R x ld int64).
+hipError_t plan_hist_u32(Workspace& ws, const uint32_t* keys, size_t n, int bits, uint64_t block, uint64_t stride,
+                         int64_t* d_out, hipStream_t stream);
+hipError_t plan_rounds(const int64_t* d_hist, uint32_t R, uint32_t ld, uint32_t K, double growth, uint8_t* d_lut,
+                       int64_t* d_est, hipStream_t stream);
 
 // ---- per-kernel timing (hipEvents on the launch stream) ----
 bool timing_enabled();

@@ -62,6 +62,10 @@ _SIGS = [
     ("libsortPartitionLutU64U32", ctypes.c_int,
      [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
     ("libsortSegmentCopyU32", ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _u64p, _u64p, _u64p, _vp]),
+    ("libsortPlanHistogramU32", ctypes.c_int,
+     [_vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
+    ("libsortPlanRounds", ctypes.c_int,
+     [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, _vp, _vp, _vp]),
     ("libsortPopulateDevice", ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_uint64, _vp]),
     ("libsortSetDigitBits", ctypes.c_int, [ctypes.c_int]),
     ("libsortGetDigitBits", ctypes.c_int, []),

@@ -128,6 +128,15 @@ class HipOps:
                                                       out_keys=self.empty64(n), out_vals=self.empty(n))
         return k, v, b.to(torch.int64) & 0xFFFFFFFF
 
+    def plan_row(self, keys, stride, block=4096):
+        """int64[4097] on the device: sampled top-12-bit histogram + n (one
+        libsort call instead of sample copy + histogram + cat)."""
+        return self.D.plan_histogram_u32(keys, block=block, stride=stride)
+
+    def plan(self, rows, R, K, growth=1.6):
+        """(lut uint8[4096], est int64[R]) from the gathered rows, on the device."""
+        return self.D.plan_rounds(rows.contiguous(), R, K, growth)
+
     def sample(self, keys, stride, block=4096):
         """Every `stride`-th block of `block` keys (all keys when few)."""
         nb = keys.numel() // block
@@ -334,6 +343,32 @@ def plan_msd(H, R, hist_bits=HIST_BITS):
     return splitters, dest, n_recv
 
 
+def _plan_row(ops, keys, stride):
+    """This rank's plan row: the sampled top-bit histogram and its key count
+    (int64, HIST_BITS + 1 entries) -- one libsort call on HipOps."""
+    if hasattr(ops, "plan_row"):
+        return ops.plan_row(keys, stride)
+    h = ops.histogram(ops.sample(keys, stride), 32 - HIST_BITS, HIST_BITS)
+    return torch.cat([h.to(torch.int64), torch.tensor([keys.numel()], dtype=torch.int64, device=h.device)])
+
+
+def _plan(ops, HN, R, K):
+    """(lut, est) of the round plan from the gathered rows (device kernel on
+    HipOps, the torch restatement otherwise)."""
+    if hasattr(ops, "plan"):
+        return ops.plan(HN, R, K)
+    return _plan_rounds_t(HN[:, :-1], R, K)
+
+
+def _sizes_from_starts(b_t, n):
+    """Bucket sizes (int64) from bucket starts, without a host round trip."""
+    sizes = torch.empty(b_t.numel(), dtype=torch.int64, device=b_t.device)
+    if b_t.numel():
+        sizes[:-1] = b_t[1:] - b_t[:-1]
+        sizes[-1:] = n - b_t[-1:]
+    return sizes
+
+
 def _plan_rounds_t(H, R, K, growth=1.6):
     """plan_rounds on torch tensors, on H's device (the GPU under RCCL, so the
     plan needs no host round trip).  Returns (lut uint8, est float64)."""
@@ -394,13 +429,11 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=4, s
     NB = R * K
     # histogram -> allgather -> plan -> partition -> allgather of the exact
     # sizes, all on the device; ONE host transfer afterwards
-    h = ops.histogram(ops.sample(keys, sample_stride), 32 - HIST_BITS, HIST_BITS)
-    dev = h.device
-    HN = _allgather_t(torch.cat([h.to(torch.int64), torch.tensor([n], dtype=torch.int64, device=dev)]), group)
-    lut_t, est_t = _plan_rounds_t(HN[:, :-1], R, K)
+    HN = _allgather_t(_plan_row(ops, keys, sample_stride), group)     # [R, 4097]: histogram | n
+    lut_t, est_t = _plan(ops, HN, R, K)
     _mark(trace, "histogram+allgather+plan")
     part, b_t = ops.partition_lut_t(keys, lut_t, 32 - HIST_BITS, NB)
-    sizes_t = torch.diff(b_t, append=torch.tensor([n], dtype=torch.int64, device=b_t.device))
+    sizes_t = _sizes_from_starts(b_t, n)
     C_t = _allgather_t(sizes_t, group)                         # [R, NB], bucket j = round * R + dest
     host = torch.cat([C_t.flatten(), HN[:, -1], est_t.round().to(torch.int64), lut_t.to(torch.int64)]).cpu().numpy()
     _mark(trace, "partition+allgather sizes")
@@ -484,12 +517,12 @@ def _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride, self_local
     K = max(1, min(int(rounds), 256 // R))
     n = keys.numel()
     NB = R * K
-    h = ops.histogram(ops.sample_hi(keys, sample_stride), 32 - HIST_BITS, HIST_BITS)
-    dev = h.device
-    HN = _allgather_t(torch.cat([h.to(torch.int64), torch.tensor([n], dtype=torch.int64, device=dev)]), group)
-    lut_t, _ = _plan_rounds_t(HN[:, :-1], R, K)
+    hi = ops.sample_hi(keys, sample_stride)
+    h = ops.histogram(hi, 32 - HIST_BITS, HIST_BITS)
+    HN = _allgather_t(torch.cat([h.to(torch.int64), torch.tensor([n], dtype=torch.int64, device=h.device)]), group)
+    lut_t, _ = _plan(ops, HN, R, K)
     pk, pv, b_t = ops.partition_lut_pairs_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
-    sizes_t = torch.diff(b_t, append=torch.tensor([n], dtype=torch.int64, device=b_t.device))
+    sizes_t = _sizes_from_starts(b_t, n)
     C_t = _allgather_t(sizes_t, group)
     C = C_t.cpu().numpy()                                      # the one host transfer
     sizes = C[r]
