@@ -461,8 +461,10 @@ __global__ __launch_bounds__(BLOCK, MINB) void k_pass_z(const uint32_t* __restri
   uint32_t k[ITEMS], rk[ITEMS];
   uint32_t rkp[ITEMS / 2];  // PACK: two 16-bit ranks per register across the block phase
   const uint32_t* kp = kin + (uint64_t)t * TILE + w * WSPAN + lane;
+  // ABL 8: nontemporal key stores, 9: nontemporal key loads, 10: both (exact kernels)
+  constexpr bool NTS = ABL == 8 || ABL == 10, NTL = ABL == 9 || ABL == 10;
 #pragma unroll
-  for (int j = 0; j < ITEMS; ++j) k[j] = kp[j * kWave];
+  for (int j = 0; j < ITEMS; ++j) k[j] = NTL ? __builtin_nontemporal_load(&kp[j * kWave]) : kp[j * kWave];
   if constexpr (ABL >= 4 && ABL < 6) {
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) rk[j] = w * WSPAN + j * kWave + lane;
@@ -520,13 +522,14 @@ __global__ __launch_bounds__(BLOCK, MINB) void k_pass_z(const uint32_t* __restri
     for (int j = 0; j < SPER; ++j) ob[j] = s_ob[__builtin_amdgcn_ubfe(kk[j], shift, 4)];
 #pragma unroll
     for (int j = 0; j < SPER; ++j) {
-      if constexpr (ABL == 0 || ABL >= 6) kout[ob[j].x + tid + (h * SPER + j) * BLOCK] = kk[j];
+      if constexpr (NTS) __builtin_nontemporal_store(kk[j], &kout[ob[j].x + tid + (h * SPER + j) * BLOCK]);
+      else if constexpr (ABL == 0 || ABL >= 6) kout[ob[j].x + tid + (h * SPER + j) * BLOCK] = kk[j];
       if constexpr (ABL == 1) kout[(size_t)t * TILE + tid + (h * SPER + j) * BLOCK] = kk[j] + ob[j].x;
       if constexpr (ABL >= 2 && ABL < 6) if (kk[j] == 0x9e3779b9u && ob[j].x == 7u) kout[t] = 1u;
     }
 #pragma unroll
     for (int j = 0; j < SPER; ++j) {
-      if constexpr (ABL < 3 || ABL == 6) {
+      if constexpr (ABL < 3 || ABL == 6 || ABL >= 8) {
         const uint32_t slot = (uint32_t)(tid + (h * SPER + j) * BLOCK) >= ob[j].y ? 256u : 0u;
         const uint32_t dd = __builtin_amdgcn_ubfe(kk[j], shift, 4), dn = __builtin_amdgcn_ubfe(kk[j], shift + 4, 4);
         atomicAdd(&s_next[slot + dd * 16 + dn], 1u);
@@ -534,7 +537,7 @@ __global__ __launch_bounds__(BLOCK, MINB) void k_pass_z(const uint32_t* __restri
     }
   }
   __syncthreads();
-  if constexpr (ABL < 3)
+  if constexpr (ABL < 3 || ABL >= 8)
 #pragma unroll
   for (int q = 0; q < 2 * RADIX * RADIX / BLOCK; ++q) {
     const int e = tid + q * BLOCK;
@@ -665,6 +668,18 @@ int main(int argc, char** argv) {
     V.push_back({"z c1 s2 xcd minb8", [&] {
       hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 0, 8, false>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u,
                          L.ws.tc[0], B, L.ws.tc[1]);
+    }});
+    V.push_back({"z xcd NT stores", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 8>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
+                         B, L.ws.tc[1]);
+    }});
+    V.push_back({"z xcd NT loads", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 9>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
+                         B, L.ws.tc[1]);
+    }});
+    V.push_back({"z xcd NT both", [&] {
+      hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 10>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
+                         B, L.ws.tc[1]);
     }});
     V.push_back({"ABL contiguous stores", [&] {
       hipLaunchKernelGGL((k_pass_z<1, false, 2, true, 256, true, 1>), grid, blk, 0, L.st, L.in, L.out, 0u, 4u, L.ws.tc[0],
