@@ -96,7 +96,10 @@ static bool ws_acquire_stream(int dev, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_order_mu);
   if ((size_t)dev >= g_order.size()) g_order.resize(dev + 1);
   WsOrder& o = g_order[dev];
-  if (!o.evt && !hip_ok(hipEventCreateWithFlags(&o.evt, hipEventDisableTiming), "hipEventCreate"))
+  // device-scope release: the event only orders libsort's own kernels on two
+  // streams of one device (no L2 write-back per call)
+  if (!o.evt && !hip_ok(hipEventCreateWithFlags(&o.evt, hipEventDisableTiming | hipEventReleaseToDevice),
+                        "hipEventCreate"))
     return false;
   if (o.used && o.last != st) return hip_ok(hipStreamWaitEvent(st, o.evt, 0), "hipStreamWaitEvent");
   return true;
@@ -138,7 +141,13 @@ int timing_start(const char* name, hipStream_t st, uint64_t keys) {
   TimingRec r;
   r.name = name;
   r.keys = keys;
-  if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return -1;
+  // Timestamps only: no system-scope fence at record time.  A default event
+  // writes back and invalidates L2 when it is recorded (~3 us each between the
+  // kernels of a sort, and the pass kernel's L2-merged output lines flushed
+  // early); these events are never used to order memory.
+  if (hipEventCreateWithFlags(&r.a, hipEventDisableSystemFence) != hipSuccess ||
+      hipEventCreateWithFlags(&r.b, hipEventDisableSystemFence) != hipSuccess)
+    return -1;
   if (hipEventRecord(r.a, st) != hipSuccess) return -1;
   std::lock_guard<std::mutex> lk(g_tmu);
   g_recs.push_back(r);
