@@ -133,3 +133,27 @@ def test_host_checkers():
     pylibsort.checkOrder(np.sort(x))
     with pytest.raises(pylibsort.sortResultException):
         pylibsort.checkOrder(x)
+
+
+def test_c_caller_links_against_reference_layout(tmp_path):
+    """A C caller built the way the reference's callers are (cgo flags
+    `--std=gnu99 -I../../../libsort -L../../../libsort -lsort`,
+    benchmark/pkg/sort/libsort.go:11-12) against repo:libsort/ links and runs
+    the host-only entry points (populateInput, providedCpu) without a GPU."""
+    d = ROOT / "libsort"
+    if not (d / "libsort.so").exists():
+        subprocess.run(["make", "-C", str(d)], check=True, capture_output=True)
+    src = tmp_path / "caller.c"
+    src.write_text(
+        '#include <stdio.h>\n#include "libsort.h"\n'
+        "int main(void){ uint32_t a[8]; populateInput(a, 8);\n"
+        "  if (!providedCpu(a, 8)) return 2;\n"
+        "  for (int i = 1; i < 8; ++i) if (a[i-1] > a[i]) return 3;\n"
+        "  printf(\"%08x\\n\", a[0]); return 0; }\n")
+    exe = tmp_path / "caller"
+    subprocess.run(["gcc", "--std=gnu99", "-O2", "-I", str(d), str(src), "-L", str(d), "-lsort",
+                    "-Wl,-rpath," + str(d), "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    # smallest of the first 8 reference PCG words (tests/golden/pcg_golden.json)
+    assert out.stdout.strip() == "0f55ac5f"
