@@ -122,3 +122,26 @@ def test_plan_histogram(n, stride):
     ref = np.bincount(s >> 20, minlength=4096) if n else np.zeros(4096, dtype=np.int64)
     np.testing.assert_array_equal(row[:4096], ref)
     assert row[4096] == n
+
+
+def test_bench_multi_rank_path_rehearsal():
+    """bench.py's N>1 path end to end (2 ranks, gloo, both on the one GPU of
+    the test box): timed distributed sorts, max-over-ranks timing, the
+    collective verification and the 8-bit variant all complete and verify."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import json
+    import os
+    import pathlib
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = dict(os.environ, BENCH_REHEARSAL="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29557", str(root / "bench.py"), "--gpus", "2",
+           "--steps", "2", "--warmup", "1", "--keys-log2", "20"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180, cwd=str(root))
+    assert r.returncode == 0, r.stderr[-4000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["verified"] is True and line["rehearsal"]
+    assert line["config"]["global_keys"] == 2 << 20 and line["variants"]["digit8"]["value"] > 0
