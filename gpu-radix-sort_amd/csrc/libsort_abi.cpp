@@ -820,6 +820,61 @@ LIBSORT_EXPORT int libsortPartitionLutU64U32(const uint64_t* d_kin, const uint32
              : 0;
 }
 
+LIBSORT_EXPORT int libsortPartitionLutCountU32(const uint32_t* d_in, size_t n, const uint8_t* d_lut,
+                                               uint32_t lut_shift, uint32_t nbuckets, uint32_t* d_bounds,
+                                               void* stream) {
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(partition_lut_u32(ws, d_in, nullptr, n, d_lut, (int)lut_shift, (int)nbuckets, d_bounds, st,
+                                           kPartCount),
+                         "libsortPartitionLutCountU32");
+         })
+             ? 1
+             : 0;
+}
+
+LIBSORT_EXPORT int libsortPartitionLutScatterU32(const uint32_t* d_in, uint32_t* d_out, size_t n, const uint8_t* d_lut,
+                                                 uint32_t lut_shift, uint32_t nbuckets, void* stream) {
+  if (n > 0 && (const uint32_t*)d_out == d_in) {
+    set_error("libsortPartitionLutScatterU32: out of place only");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(partition_lut_u32(ws, d_in, d_out, n, d_lut, (int)lut_shift, (int)nbuckets, nullptr, st,
+                                           kPartScatter),
+                         "libsortPartitionLutScatterU32 (needs the matching count call just before it)");
+         })
+             ? 1
+             : 0;
+}
+
+LIBSORT_EXPORT int libsortPartitionLutCountU64U32(const uint64_t* d_kin, const uint32_t* d_vin, size_t n,
+                                                  const uint8_t* d_lut, uint32_t lut_shift, uint32_t nbuckets,
+                                                  uint32_t* d_bounds, void* stream) {
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(partition_lut_pairs_u64_u32(ws, d_kin, d_vin, nullptr, nullptr, n, d_lut, (int)lut_shift,
+                                                     (int)nbuckets, d_bounds, st, kPartCount),
+                         "libsortPartitionLutCountU64U32");
+         })
+             ? 1
+             : 0;
+}
+
+LIBSORT_EXPORT int libsortPartitionLutScatterU64U32(const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
+                                                    uint32_t* d_vout, size_t n, const uint8_t* d_lut,
+                                                    uint32_t lut_shift, uint32_t nbuckets, void* stream) {
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(partition_lut_pairs_u64_u32(ws, d_kin, d_vin, d_kout, d_vout, n, d_lut, (int)lut_shift,
+                                                     (int)nbuckets, nullptr, st, kPartScatter),
+                         "libsortPartitionLutScatterU64U32 (needs the matching count call just before it)");
+         })
+             ? 1
+             : 0;
+}
+
 LIBSORT_EXPORT int libsortSegmentCopyU32(const uint32_t* d_src, uint32_t* d_dst, size_t nseg,
                                          const uint64_t* src_off, const uint64_t* dst_off,
                                          const uint64_t* len, void* stream) {

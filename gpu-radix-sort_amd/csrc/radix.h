@@ -91,6 +91,23 @@ struct Workspace {
   uint32_t* tb = nullptr;  // chunk prefixes B[chunks][RADIX], then the digit starts D[RADIX]
   size_t tb_cap = 0;  // words
   uint32_t* tticket = nullptr;  // last-arriver ticket of the column scan (zero between launches)
+  // A table partition split in two calls (count + scan, then scatter): the
+  // arguments of the count call, checked by the scatter call.  ensure_tiles()
+  // (the start of every other tile-path operation) clears it.
+  struct PartToken {
+    const void* in;
+    const void* vin;
+    size_t n;
+    const uint8_t* lut;
+    int shift, nb;
+    hipStream_t st;
+    bool valid;
+    bool operator==(const PartToken& o) const {
+      return valid && o.valid && in == o.in && vin == o.vin && n == o.n && lut == o.lut && shift == o.shift &&
+             nb == o.nb && st == o.st;
+    }
+  };
+  PartToken part_pending{nullptr, nullptr, 0, nullptr, 0, 0, nullptr, false};
   hipError_t ensure_tiles(size_t count_words, size_t chunk_words);
 
   hipError_t ensure_counts(size_t m);
@@ -150,12 +167,17 @@ hipError_t partition_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_
 // lut_shift] (lut: device, 1 << (32 - lut_shift) one-byte entries, 4-byte
 // aligned, 20 <= lut_shift <= 30, entries < nbuckets <= 256); d_bounds (may
 // be null) receives the nbuckets bucket starts.
+// phase: kPartBoth (one call), or kPartCount (counts + scan + bounds; `out`
+// unused) followed by kPartScatter (the pass, same in/lut/shift/nbuckets/
+// stream, no other tile-path call on the workspace in between; d_bounds unused).
+constexpr int kPartBoth = 0, kPartCount = 1, kPartScatter = 2;
 hipError_t partition_lut_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, const uint8_t* d_lut,
-                             int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t stream);
+                             int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t stream,
+                             int phase = kPartBoth);
 // The same for (u64 key, u32 value) pairs; bucket = lut[(key >> 32) >> lut_shift].
 hipError_t partition_lut_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
                                        uint32_t* vout, size_t n, const uint8_t* d_lut, int lut_shift, int nbuckets,
-                                       uint32_t* d_bounds, hipStream_t stream);
+                                       uint32_t* d_bounds, hipStream_t stream, int phase = kPartBoth);
 // Segment copy with the table already on the device: d_tab = [src_off[nseg] |
 // dst_off[nseg] | len[nseg]] (uint64), nseg <= 65535; maxlen = the longest
 // segment (sizes the grid), total = sum of len (timing only).

@@ -1516,6 +1516,7 @@ hipError_t Workspace::ensure_seg(size_t m) {
 }
 
 hipError_t Workspace::ensure_tiles(size_t count_words, size_t chunk_words) {
+  part_pending.valid = false;  // every tile-path user starts here: a pending partition scatter is void
   if (count_words > tc_cap) {
     for (auto& p : tc) {
       if (p) { (void)hipFree(p); p = nullptr; }
@@ -2031,14 +2032,28 @@ namespace {
 // u64 keys: the table indexes the top bits of the key's high word.
 template <int BITS, typename K, typename V>
 hipError_t partition_lut_impl(Workspace& ws, const K* in, K* out, const V* vin, V* vout, size_t n,
-                              const uint8_t* d_lut, int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st) {
+                              const uint8_t* d_lut, int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st,
+                              int phase) {
   constexpr int RADIX = 1 << BITS;
   constexpr int B = tp_block(BITS);
   const uint32_t tiles = tp_tiles<K>(n, BITS);
-  LS_TRY(ws.ensure_tiles((size_t)tiles * RADIX, ((size_t)tp_chunks(tiles, BITS) + 1) * RADIX));
   const LutDigit op{d_lut, (uint32_t)lut_shift, (uint32_t)RADIX - 1u, nullptr};
-  LS_TRY((tiles_counts<BITS, K, LutDigit>(ws, in, n, op, tiles, ws.tc[0], nullptr, 0, st)));
-  LS_TRY(tiles_colscan<BITS>(ws, ws.tc[0], tiles, st));
+  Workspace::PartToken tok{in, vin, n, d_lut, lut_shift, nbuckets, st, true};
+  if (phase != kPartScatter) {
+    LS_TRY(ws.ensure_tiles((size_t)tiles * RADIX, ((size_t)tp_chunks(tiles, BITS) + 1) * RADIX));
+    LS_TRY((tiles_counts<BITS, K, LutDigit>(ws, in, n, op, tiles, ws.tc[0], nullptr, 0, st)));
+    LS_TRY(tiles_colscan<BITS>(ws, ws.tc[0], tiles, st));
+    if (d_bounds)
+      LS_TRY(hipMemcpyAsync(d_bounds, tiles_digit_starts(ws, tiles, BITS), (size_t)nbuckets * sizeof(uint32_t),
+                            hipMemcpyDeviceToDevice, st));
+    if (phase == kPartCount) {
+      ws.part_pending = tok;  // the scanned counts stay in the workspace for the scatter call
+      return hipSuccess;
+    }
+  } else if (!(ws.part_pending == tok)) {
+    return hipErrorInvalidValue;  // no matching count call, or the workspace was used in between
+  }
+  ws.part_pending.valid = false;
   {
     ScopedTimer tm("partition", st, n);
     hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, false, LutDigit>), dim3(tiles), dim3(B), 0, st, in,
@@ -2046,43 +2061,47 @@ hipError_t partition_lut_impl(Workspace& ws, const K* in, K* out, const V* vin, 
                        (const uint32_t*)tiles_digit_starts(ws, tiles, BITS), ws.tc[1]);
     LS_TRY(hipGetLastError());
   }
-  if (d_bounds)
-    LS_TRY(hipMemcpyAsync(d_bounds, tiles_digit_starts(ws, tiles, BITS), (size_t)nbuckets * sizeof(uint32_t),
-                          hipMemcpyDeviceToDevice, st));
   return hipSuccess;
 }
 
 template <typename K, typename V>
 hipError_t partition_lut_any(Workspace& ws, const K* in, K* out, const V* vin, V* vout, size_t n,
-                             const uint8_t* d_lut, int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st) {
+                             const uint8_t* d_lut, int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st,
+                             int phase = kPartBoth) {
   if (n > 0xffffffffull || lut_shift < 20 || lut_shift > 30 || nbuckets < 1 || nbuckets > 256)
     return hipErrorInvalidValue;
   if (n == 0) {
-    if (d_bounds) LS_TRY(hipMemsetAsync(d_bounds, 0, (size_t)nbuckets * sizeof(uint32_t), st));
+    if (d_bounds && phase != kPartScatter)
+      LS_TRY(hipMemsetAsync(d_bounds, 0, (size_t)nbuckets * sizeof(uint32_t), st));
     return hipSuccess;
   }
-  if (!in || !out || !d_lut || (const void*)in == (const void*)out || (reinterpret_cast<uintptr_t>(d_lut) & 3u))
+  const bool need_out = phase != kPartCount;
+  if (!in || !d_lut || (need_out && (!out || (const void*)in == (const void*)out)) ||
+      (reinterpret_cast<uintptr_t>(d_lut) & 3u))
     return hipErrorInvalidValue;
   if constexpr (!std::is_same<V, NoValue>::value) {
-    if (!vin || !vout || (const void*)vin == (const void*)vout) return hipErrorInvalidValue;
+    if (!vin || (need_out && (!vout || (const void*)vin == (const void*)vout))) return hipErrorInvalidValue;
   }
   // digit width by bucket count: 16 -> 4-bit tiles, 32 -> 5-bit (the 8-rank x 4-round exchange), else 8-bit
-  if (nbuckets <= 16) return partition_lut_impl<4, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st);
-  if (nbuckets <= 32) return partition_lut_impl<5, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st);
-  return partition_lut_impl<8, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st);
+  if (nbuckets <= 16)
+    return partition_lut_impl<4, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st, phase);
+  if (nbuckets <= 32)
+    return partition_lut_impl<5, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st, phase);
+  return partition_lut_impl<8, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st, phase);
 }
 }  // namespace
 
 hipError_t partition_lut_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, const uint8_t* d_lut,
-                             int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st) {
+                             int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st, int phase) {
   return partition_lut_any<uint32_t, NoValue>(ws, in, out, nullptr, nullptr, n, d_lut, lut_shift, nbuckets, d_bounds,
-                                              st);
+                                              st, phase);
 }
 
 hipError_t partition_lut_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
                                        uint32_t* vout, size_t n, const uint8_t* d_lut, int lut_shift, int nbuckets,
-                                       uint32_t* d_bounds, hipStream_t st) {
-  return partition_lut_any<uint64_t, uint32_t>(ws, kin, kout, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st);
+                                       uint32_t* d_bounds, hipStream_t st, int phase) {
+  return partition_lut_any<uint64_t, uint32_t>(ws, kin, kout, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st,
+                                               phase);
 }
 
 hipError_t segment_copy_dev_u32(const uint32_t* src, uint32_t* dst, const uint64_t* d_tab, size_t nseg,

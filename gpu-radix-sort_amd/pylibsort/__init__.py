@@ -61,6 +61,14 @@ _SIGS = [
      [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
     ("libsortPartitionLutU64U32", ctypes.c_int,
      [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
+    ("libsortPartitionLutCountU32", ctypes.c_int,
+     [_vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
+    ("libsortPartitionLutScatterU32", ctypes.c_int,
+     [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp]),
+    ("libsortPartitionLutCountU64U32", ctypes.c_int,
+     [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
+    ("libsortPartitionLutScatterU64U32", ctypes.c_int,
+     [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     ("libsortSegmentCopyU32", ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _u64p, _u64p, _u64p, _vp]),
     ("libsortPlanHistogramU32", ctypes.c_int,
      [_vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),

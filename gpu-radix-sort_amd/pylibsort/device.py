@@ -208,6 +208,56 @@ def partition_lut_pairs_u64_u32(keys, vals, lut, lut_shift, nbuckets, out_keys=N
     return ok_, ov, bounds
 
 
+def _lut_check(lut, lut_shift):
+    if lut.dtype != torch.uint8 or not lut.is_cuda or lut.numel() != 1 << (32 - lut_shift):
+        raise ValueError("lut must be a uint8 CUDA tensor of 2**(32 - lut_shift) entries")
+    return lut.contiguous()
+
+
+def partition_lut_count_u32(keys, lut, lut_shift, nbuckets, bounds=None):
+    """First half of partition_lut_u32: counts + scan, bucket starts (int32
+    tensor).  partition_lut_scatter_u32 with the same arguments must follow."""
+    _need(keys, _U32, "keys")
+    lut = _lut_check(lut, lut_shift)
+    bounds = torch.empty(nbuckets, dtype=torch.int32, device=keys.device) if bounds is None else bounds
+    _check(_lib().libsortPartitionLutCountU32(_ptr(keys), keys.numel(), _ptr(lut), lut_shift, nbuckets, _ptr(bounds),
+                                              _stream()), "libsortPartitionLutCountU32")
+    return bounds
+
+
+def partition_lut_scatter_u32(keys, lut, lut_shift, nbuckets, out=None):
+    """Second half of partition_lut_u32: the data movement."""
+    _need(keys, _U32, "keys")
+    lut = _lut_check(lut, lut_shift)
+    out = torch.empty_like(keys) if out is None else out
+    _need(out, _U32, "out")
+    _check(_lib().libsortPartitionLutScatterU32(_ptr(keys), _ptr(out), keys.numel(), _ptr(lut), lut_shift, nbuckets,
+                                                _stream()), "libsortPartitionLutScatterU32")
+    return out
+
+
+def partition_lut_pairs_count_u64_u32(keys, vals, lut, lut_shift, nbuckets, bounds=None):
+    _need(keys, _U64, "keys")
+    _need(vals, _U32, "vals")
+    lut = _lut_check(lut, lut_shift)
+    bounds = torch.empty(nbuckets, dtype=torch.int32, device=keys.device) if bounds is None else bounds
+    _check(_lib().libsortPartitionLutCountU64U32(_ptr(keys), _ptr(vals), keys.numel(), _ptr(lut), lut_shift, nbuckets,
+                                                 _ptr(bounds), _stream()), "libsortPartitionLutCountU64U32")
+    return bounds
+
+
+def partition_lut_pairs_scatter_u64_u32(keys, vals, lut, lut_shift, nbuckets, out_keys=None, out_vals=None):
+    _need(keys, _U64, "keys")
+    _need(vals, _U32, "vals")
+    lut = _lut_check(lut, lut_shift)
+    ok_ = torch.empty_like(keys) if out_keys is None else out_keys
+    ov = torch.empty_like(vals) if out_vals is None else out_vals
+    _check(_lib().libsortPartitionLutScatterU64U32(_ptr(keys), _ptr(vals), _ptr(ok_), _ptr(ov), keys.numel(),
+                                                   _ptr(lut), lut_shift, nbuckets, _stream()),
+           "libsortPartitionLutScatterU64U32")
+    return ok_, ov
+
+
 def segment_copy_u32(src, dst, src_off, dst_off, lens):
     """dst[dst_off[i] + j] = src[src_off[i] + j] for j < lens[i]."""
     _need(src, _U32, "src")

@@ -122,6 +122,24 @@ class HipOps:
         out, b = self.D.partition_lut_u32(keys, lut.contiguous(), shift, nbuckets, out=self.empty(keys.numel()))
         return out, b.to(torch.int64) & 0xFFFFFFFF
 
+    def partition_lut_count_t(self, keys, lut, shift, nbuckets):
+        """Count half of the split table partition: bucket starts (int64,
+        device) while nothing has moved yet."""
+        b = self.D.partition_lut_count_u32(keys, lut.contiguous(), shift, nbuckets)
+        return b.to(torch.int64) & 0xFFFFFFFF
+
+    def partition_lut_scatter_t(self, keys, lut, shift, nbuckets):
+        return self.D.partition_lut_scatter_u32(keys, lut.contiguous(), shift, nbuckets, out=self.empty(keys.numel()))
+
+    def partition_lut_pairs_count_t(self, keys, vals, lut, shift, nbuckets):
+        b = self.D.partition_lut_pairs_count_u64_u32(keys, vals, lut.contiguous(), shift, nbuckets)
+        return b.to(torch.int64) & 0xFFFFFFFF
+
+    def partition_lut_pairs_scatter_t(self, keys, vals, lut, shift, nbuckets):
+        n = keys.numel()
+        return self.D.partition_lut_pairs_scatter_u64_u32(keys, vals, lut.contiguous(), shift, nbuckets,
+                                                          out_keys=self.empty64(n), out_vals=self.empty(n))
+
     def partition_lut_pairs_t(self, keys, vals, lut, shift, nbuckets):
         n = keys.numel()
         k, v, b = self.D.partition_lut_pairs_u64_u32(keys, vals, lut.contiguous(), shift, nbuckets,
@@ -173,6 +191,30 @@ def _allgather_t(t, group):
     outs = [torch.empty_like(src) for _ in range(R)]
     dist.all_gather(outs, src, group=group)
     return torch.stack(outs).to(t.device)
+
+
+class _HostCopy:
+    """A small device -> host copy in flight: pinned buffer + event, so later
+    GPU work can be queued before the host waits for the copy alone."""
+
+    def __init__(self, t):
+        self.t = t
+        self.ev = None
+        if t.is_cuda:
+            self.host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            self.host.copy_(t, non_blocking=True)
+            self.ev = torch.cuda.Event()
+            self.ev.record()
+
+    def wait(self):
+        if self.ev is None:
+            return self.t.numpy()
+        self.ev.synchronize()
+        return self.host.numpy()
+
+
+def _to_host_async(t):
+    return _HostCopy(t)
 
 
 def _alltoallv(send, send_counts, recv_counts, ops, group):
@@ -432,10 +474,20 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=4, s
     HN = _allgather_t(_plan_row(ops, keys, sample_stride), group)     # [R, 4097]: histogram | n
     lut_t, est_t = _plan(ops, HN, R, K)
     _mark(trace, "histogram+allgather+plan")
-    part, b_t = ops.partition_lut_t(keys, lut_t, 32 - HIST_BITS, NB)
+    split = hasattr(ops, "partition_lut_count_t")
+    if split:
+        # sizes first: counts + scan, gather, start the small D2H, and only
+        # then queue the scatter, so the host plans and issues the exchange
+        # while the data moves (the one host synchronisation waits for the sizes)
+        b_t = ops.partition_lut_count_t(keys, lut_t, 32 - HIST_BITS, NB)
+    else:
+        part, b_t = ops.partition_lut_t(keys, lut_t, 32 - HIST_BITS, NB)
     sizes_t = _sizes_from_starts(b_t, n)
     C_t = _allgather_t(sizes_t, group)                         # [R, NB], bucket j = round * R + dest
-    host = torch.cat([C_t.flatten(), HN[:, -1], est_t.round().to(torch.int64), lut_t.to(torch.int64)]).cpu().numpy()
+    pending = _to_host_async(torch.cat([C_t.flatten(), HN[:, -1], est_t.to(torch.int64), lut_t.to(torch.int64)]))
+    if split:
+        part = ops.partition_lut_scatter_t(keys, lut_t, 32 - HIST_BITS, NB)
+    host = pending.wait()
     _mark(trace, "partition+allgather sizes")
     C = host[:R * NB].reshape(R, NB)
     n_all = host[R * NB:R * NB + R]
@@ -521,10 +573,17 @@ def _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride, self_local
     h = ops.histogram(hi, 32 - HIST_BITS, HIST_BITS)
     HN = _allgather_t(torch.cat([h.to(torch.int64), torch.tensor([n], dtype=torch.int64, device=h.device)]), group)
     lut_t, _ = _plan(ops, HN, R, K)
-    pk, pv, b_t = ops.partition_lut_pairs_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
+    split = hasattr(ops, "partition_lut_pairs_count_t")
+    if split:
+        b_t = ops.partition_lut_pairs_count_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
+    else:
+        pk, pv, b_t = ops.partition_lut_pairs_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
     sizes_t = _sizes_from_starts(b_t, n)
     C_t = _allgather_t(sizes_t, group)
-    C = C_t.cpu().numpy()                                      # the one host transfer
+    pending = _to_host_async(C_t)
+    if split:
+        pk, pv = ops.partition_lut_pairs_scatter_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
+    C = pending.wait()                                         # the one host transfer
     sizes = C[r]
     b = np.concatenate([[0], np.cumsum(sizes)[:-1]])
     recv_tot = np.array([int(C[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)

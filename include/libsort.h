@@ -149,6 +149,28 @@ LIBSORT_API bool libsortPartitionLutU64U32(const uint64_t* d_kin, const uint32_t
                                            const uint8_t* d_lut, uint32_t lut_shift,
                                            uint32_t nbuckets, uint32_t* d_bounds, void* stream);
 
+/* The same partitions in two calls, so a caller can read the bucket sizes
+ * while the data moves: ...Count runs the per-tile counts and the column scan
+ * and writes the bucket starts to d_bounds (device, nbuckets uint32);
+ * ...Scatter then moves the data.  The scatter call must follow its count call
+ * with the same input, table, shift, bucket count and stream, with no other
+ * libsort sort/partition on that device's workspace in between (otherwise it
+ * returns false).  The multi-GPU schedule reads the sizes, gathers them and
+ * issues its exchange while the scatter runs. */
+LIBSORT_API bool libsortPartitionLutCountU32(const uint32_t* d_in, size_t n, const uint8_t* d_lut,
+                                             uint32_t lut_shift, uint32_t nbuckets, uint32_t* d_bounds,
+                                             void* stream);
+LIBSORT_API bool libsortPartitionLutScatterU32(const uint32_t* d_in, uint32_t* d_out, size_t n,
+                                               const uint8_t* d_lut, uint32_t lut_shift, uint32_t nbuckets,
+                                               void* stream);
+LIBSORT_API bool libsortPartitionLutCountU64U32(const uint64_t* d_kin, const uint32_t* d_vin, size_t n,
+                                                const uint8_t* d_lut, uint32_t lut_shift, uint32_t nbuckets,
+                                                uint32_t* d_bounds, void* stream);
+LIBSORT_API bool libsortPartitionLutScatterU64U32(const uint64_t* d_kin, const uint32_t* d_vin,
+                                                  uint64_t* d_kout, uint32_t* d_vout, size_t n,
+                                                  const uint8_t* d_lut, uint32_t lut_shift,
+                                                  uint32_t nbuckets, void* stream);
+
 /* Gather-copy of nseg segments: dst[dst_off[i] + j] = src[src_off[i] + j] for
  * j < len[i].  The three tables are host arrays.  Used to put exchanged
  * buckets into bucket-major / rank-minor order between distributed rounds. */

@@ -234,6 +234,38 @@ def test_partition_lut(dev, oracle_mod, n, shift, nbuckets):
     np.testing.assert_array_equal(b.cpu().numpy().astype(np.int64), starts)
 
 
+@pytest.mark.parametrize("n", [0, 4097, 1 << 20])
+@pytest.mark.parametrize("nbuckets", [16, 32, 200])
+def test_partition_lut_split(dev, oracle_mod, n, nbuckets):
+    """The two-call partition (count + scan, then scatter) gives the one-call
+    result, for keys and for (u64, u32) pairs; a scatter without its count
+    call, or after another sort used the workspace, fails loudly."""
+    x = oracle_mod.pcg(n, first=7 * n + nbuckets)
+    rng = np.random.default_rng(nbuckets)
+    lut = torch.from_numpy(np.sort(rng.integers(0, nbuckets, 4096)).astype(np.uint8)).cuda()
+    t = _tensor(x)
+    ref, rb = dev.partition_lut_u32(t, lut, 20, nbuckets)
+    b = dev.partition_lut_count_u32(t, lut, 20, nbuckets)
+    out = dev.partition_lut_scatter_u32(t, lut, 20, nbuckets)
+    torch.cuda.synchronize()
+    assert torch.equal(b, rb) and torch.equal(out, ref)
+    if n == 0:
+        return
+    with pytest.raises(RuntimeError):
+        dev.partition_lut_scatter_u32(t, lut, 20, nbuckets)       # already consumed
+    dev.partition_lut_count_u32(t, lut, 20, nbuckets)
+    dev.sort_keys_u32(t)                                           # uses the workspace in between
+    with pytest.raises(RuntimeError):
+        dev.partition_lut_scatter_u32(t, lut, 20, nbuckets)
+    k = torch.from_numpy((x.astype(np.uint64) << np.uint64(32) | np.uint64(5)).view(np.int64)).cuda()
+    v = torch.arange(n, dtype=torch.int32, device="cuda")
+    rk, rv, rb2 = dev.partition_lut_pairs_u64_u32(k, v, lut, 20, nbuckets)
+    b2 = dev.partition_lut_pairs_count_u64_u32(k, v, lut, 20, nbuckets)
+    k2, v2 = dev.partition_lut_pairs_scatter_u64_u32(k, v, lut, 20, nbuckets)
+    torch.cuda.synchronize()
+    assert torch.equal(b2, rb2) and torch.equal(k2, rk) and torch.equal(v2, rv)
+
+
 @pytest.mark.parametrize("n", [0, 3, 2049, 300007])
 @pytest.mark.parametrize("nbuckets", [8, 16, 64])
 def test_partition_lut_pairs(dev, n, nbuckets):
