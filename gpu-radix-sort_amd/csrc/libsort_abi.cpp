@@ -309,11 +309,19 @@ static inline uint32_t rotr32(uint32_t x, uint32_t r) { return (x >> r) | (x << 
 // Critical path: H2D + partition of the last chunk + gather/sort of range 0 +
 // D2H, instead of H2D + whole sort + D2H.  Bit-identical result (a full sort
 // is unique).
-constexpr int kPipeChunks = 8;
-constexpr int kPipeGroups = 16;
+constexpr int kPipeChunks = 4, kPipeChunksMax = 16;   // LIBSORT_PIPE_CHUNKS
+constexpr int kPipeGroups = 8, kPipeGroupsMax = 32;   // LIBSORT_PIPE_GROUPS (A/B knobs; tools/host_pipe_ab.py)
 constexpr int kPlanBits = 12;
-static_assert(kPipeChunks + kPipeGroups <= Workspace::kPipeEvents, "events");
-static_assert(3 * kPipeChunks * kPipeGroups * 2 <= 3 * 2 * 1024, "segment tables");
+static_assert(kPipeChunksMax + kPipeGroupsMax <= Workspace::kPipeEvents, "events");
+static_assert(3 * kPipeChunksMax * kPipeGroupsMax * 2 <= 3 * 2 * 1024, "segment tables");
+static_assert(kPipeChunksMax * kPipeGroupsMax <= 1024, "chunk bucket starts");
+
+static int env_int(const char* name, int dflt, int lo, int hi) {
+  const char* s = getenv(name);
+  if (!s) return dflt;
+  const int v = atoi(s);
+  return v < lo ? lo : v > hi ? hi : v;
+}
 
 static size_t env_pipeline_min() {
   const char* s = getenv("LIBSORT_HOST_PIPELINE_MIN");  // keys; 0 disables the pipeline
@@ -340,11 +348,13 @@ static bool pipe_checkpoint(const char* step, hipStream_t a, hipStream_t b) {
 }
 
 static bool host_full_sort_pipelined(Workspace* ws, uint32_t* h, size_t len, int bits) {
+  static const int NCH = env_int("LIBSORT_PIPE_CHUNKS", kPipeChunks, 1, kPipeChunksMax);
+  static const int NG = env_int("LIBSORT_PIPE_GROUPS", kPipeGroups, 2, kPipeGroupsMax);
   hipStream_t st = ws->stream, cs = ws->copy_stream;
   uint32_t* b0 = static_cast<uint32_t*>(ws->hbuf[0]);
   uint32_t* b1 = static_cast<uint32_t*>(ws->hbuf[1]);
   uint32_t* b2 = static_cast<uint32_t*>(ws->pbuf);
-  const size_t piece = ((len + kPipeChunks - 1) / kPipeChunks + 8191) & ~(size_t)8191;
+  const size_t piece = ((len + NCH - 1) / NCH + 8191) & ~(size_t)8191;
   const int nch = (int)((len + piece - 1) / piece);
   // plan block layout (device and pinned mirror): hist[4096] | lut bytes[4096]
   // | chunk bucket starts[1024] | segment tables (uint64)
@@ -357,7 +367,7 @@ static bool host_full_sort_pipelined(Workspace* ws, uint32_t* h, size_t len, int
   uint32_t* bnd = H + 4096 + 1024;
   uint64_t* tab = reinterpret_cast<uint64_t*>(H + 4096 + 2048);
   hipEvent_t* ev = ws->pipe_evt;
-  uint64_t lo[kPipeGroups], hi[kPipeGroups];
+  uint64_t lo[kPipeGroupsMax], hi[kPipeGroupsMax];
   bool ok = true;
   for (int c = 0; ok && c < nch; ++c) {
     const size_t off = (size_t)c * piece, m = std::min(piece, len - off);
@@ -373,10 +383,10 @@ static bool host_full_sort_pipelined(Workspace* ws, uint32_t* h, size_t len, int
       for (int b = 0; b < 4096; ++b) total += H[b];
       uint64_t acc = 0;
       int prev = 0;
-      for (int g = 0; g < kPipeGroups; ++g) lo[g] = hi[g] = 0;
+      for (int g = 0; g < NG; ++g) lo[g] = hi[g] = 0;
       for (int b = 0; b < 4096; ++b) {
-        int g = total ? (int)((2 * acc + H[b]) * kPipeGroups / (2 * total)) : 0;
-        g = std::max(prev, std::min(g, kPipeGroups - 1));
+        int g = total ? (int)((2 * acc + H[b]) * NG / (2 * total)) : 0;
+        g = std::max(prev, std::min(g, NG - 1));
         if (hi[g] == 0) lo[g] = (uint64_t)b << (32 - kPlanBits);
         hi[g] = (uint64_t)(b + 1) << (32 - kPlanBits);
         lut[b] = (uint8_t)g;
@@ -387,13 +397,13 @@ static bool host_full_sort_pipelined(Workspace* ws, uint32_t* h, size_t len, int
            pipe_checkpoint("plan", st, cs);
     }
     if (ok)
-      ok = hip_ok(partition_lut_u32(*ws, b0 + off, b1 + off, m, d_lut, 32 - kPlanBits, kPipeGroups,
-                                    d_bnd + c * kPipeGroups, st),
+      ok = hip_ok(partition_lut_u32(*ws, b0 + off, b1 + off, m, d_lut, 32 - kPlanBits, NG,
+                                    d_bnd + c * NG, st),
                   "chunk partition") &&
            pipe_checkpoint("chunk partition", st, cs);
   }
   if (ok)
-    ok = hip_ok(hipMemcpyAsync(bnd, d_bnd, (size_t)nch * kPipeGroups * sizeof(uint32_t), hipMemcpyDeviceToHost, st),
+    ok = hip_ok(hipMemcpyAsync(bnd, d_bnd, (size_t)nch * NG * sizeof(uint32_t), hipMemcpyDeviceToHost, st),
                 "D2H bucket starts") &&
          hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
   if (!ok) {
@@ -401,25 +411,25 @@ static bool host_full_sort_pipelined(Workspace* ws, uint32_t* h, size_t len, int
     (void)hipStreamSynchronize(st);
     return false;
   }
-  uint64_t sz[kPipeChunks][kPipeGroups], T[kPipeGroups], G[kPipeGroups], maxlen[kPipeGroups];
+  uint64_t sz[kPipeChunksMax][kPipeGroupsMax], T[kPipeGroupsMax], G[kPipeGroupsMax], maxlen[kPipeGroupsMax];
   uint64_t run = 0;
-  for (int g = 0; g < kPipeGroups; ++g) {
+  for (int g = 0; g < NG; ++g) {
     T[g] = maxlen[g] = 0;
     for (int c = 0; c < nch; ++c) {
       const uint64_t m = std::min(piece, len - (size_t)c * piece);
-      const uint64_t end = g + 1 < kPipeGroups ? bnd[c * kPipeGroups + g + 1] : m;
-      sz[c][g] = end - bnd[c * kPipeGroups + g];
+      const uint64_t end = g + 1 < NG ? bnd[c * NG + g + 1] : m;
+      sz[c][g] = end - bnd[c * NG + g];
       T[g] += sz[c][g];
       maxlen[g] = std::max(maxlen[g], sz[c][g]);
     }
     G[g] = run;
     run += T[g];
   }
-  for (int g = 0; g < kPipeGroups; ++g) {
+  for (int g = 0; g < NG; ++g) {
     uint64_t* t = tab + (size_t)g * 3 * nch;
     uint64_t dst = G[g];
     for (int c = 0; c < nch; ++c) {
-      t[c] = (uint64_t)c * piece + bnd[c * kPipeGroups + g];
+      t[c] = (uint64_t)c * piece + bnd[c * NG + g];
       t[nch + c] = dst;
       t[2 * nch + c] = sz[c][g];
       dst += sz[c][g];
@@ -434,11 +444,11 @@ static bool host_full_sort_pipelined(Workspace* ws, uint32_t* h, size_t len, int
     set_error("pipelined sort: bucket sizes do not add up");
     return false;
   }
-  ok = hip_ok(hipMemcpyAsync(d_tab, tab, (size_t)kPipeGroups * 3 * nch * sizeof(uint64_t), hipMemcpyHostToDevice, st),
+  ok = hip_ok(hipMemcpyAsync(d_tab, tab, (size_t)NG * 3 * nch * sizeof(uint64_t), hipMemcpyHostToDevice, st),
               "H2D segment tables");
   // every range's gather + sort is queued before the first D2H (a pageable
   // D2H may hold the host thread until it is done)
-  for (int g = 0; ok && g < kPipeGroups; ++g) {
+  for (int g = 0; ok && g < NG; ++g) {
     if (!T[g]) continue;
     const uint64_t span = hi[g] - lo[g] - 1;
     int width = 0;
@@ -450,11 +460,11 @@ static bool host_full_sort_pipelined(Workspace* ws, uint32_t* h, size_t len, int
                          (uint32_t)lo[g]),
                 "range sort") &&
          pipe_checkpoint("range sort", st, cs) &&
-         hip_ok(hipEventRecord(ev[kPipeChunks + g], st), "hipEventRecord");
+         hip_ok(hipEventRecord(ev[kPipeChunksMax + g], st), "hipEventRecord");
   }
-  for (int g = 0; ok && g < kPipeGroups; ++g) {
+  for (int g = 0; ok && g < NG; ++g) {
     if (!T[g]) continue;
-    ok = hip_ok(hipStreamWaitEvent(cs, ev[kPipeChunks + g], 0), "wait") &&
+    ok = hip_ok(hipStreamWaitEvent(cs, ev[kPipeChunksMax + g], 0), "wait") &&
          hip_ok(hipMemcpyAsync(h + G[g], b2 + G[g], T[g] * sizeof(uint32_t), hipMemcpyDeviceToHost, cs), "D2H range") &&
          pipe_checkpoint("D2H range", st, cs);
   }
