@@ -769,6 +769,10 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(const K* __restrict__ kin, K
 // at C[t][d] + B[t / kColRows][d].
 // ============================================================================
 constexpr int kColRowsPerLane = 16;
+// Rows of C per column-scan chunk.  RADIX 256 has one row-lane per column, so
+// a lane walks its chunk's rows in one sequential pass and a chunk can be long
+// (fewer chunk totals for k_colscan_wide, whose column reads are strided).
+constexpr int col_chunk_rows(int radix) { return radix >= 256 ? 64 : kColRowsPerLane * (256 / radix); }
 
 // Per-tile digit counts of the first pass; also zeroes `zero_buf` (the
 // next-pass count buffer).  One block per tile.
@@ -815,7 +819,7 @@ __global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ key
 
 // The column scan turns the per-tile counts C[tile][RADIX] into each tile's
 // run offsets: offset(t, d) = C'[t][d] + B[t / CH][d] + D[d] with C' the
-// chunk-local exclusive scan (chunks of CH = kColRowsPerLane * 256 / RADIX
+// chunk-local exclusive scan (chunks of CH = col_chunk_rows(RADIX)
 // rows), B the exclusive scan over chunks and D the digit starts.  The level
 // above each kernel runs in that kernel's last-arriving block (last_arriver),
 // so a 4-bit pass needs one scan kernel and an 8-bit pass two.
@@ -845,30 +849,50 @@ __device__ __forceinline__ bool last_arriver(uint32_t* ticket, uint32_t count, u
 template <int RADIX>
 __device__ __forceinline__ uint32_t colscan_chunk(uint32_t* __restrict__ C, uint32_t rows, uint32_t* s_sum) {
   constexpr int L = 256 / RADIX;
-  constexpr int CH = kColRowsPerLane * L;
+  constexpr int CH = col_chunk_rows(RADIX);
   const uint32_t d = threadIdx.x % RADIX, s = threadIdx.x / RADIX;
-  const uint64_t r0 = (uint64_t)blockIdx.x * CH + (uint64_t)s * kColRowsPerLane;
-  uint32_t x[kColRowsPerLane];
-  uint32_t sum = 0;
+  if constexpr (L == 1) {
+    // one row-lane: exclusive scan down the column in one pass, 16 rows per batch
+    const uint64_t r0 = (uint64_t)blockIdx.x * CH;
+    uint32_t run = 0;
 #pragma unroll
-  for (int i = 0; i < kColRowsPerLane; ++i) {
-    x[i] = (r0 + i < rows) ? C[(r0 + i) * RADIX + d] : 0u;
-    sum += x[i];
-  }
-  s_sum[threadIdx.x] = sum;
-  __syncthreads();
-  uint32_t run = 0, tot = 0;
-  for (uint32_t q = 0; q < (uint32_t)L; ++q) {
-    const uint32_t v = s_sum[q * RADIX + d];
-    run += q < s ? v : 0u;
-    tot += v;
-  }
+    for (int h = 0; h < CH; h += kColRowsPerLane) {
+      uint32_t x[kColRowsPerLane];
 #pragma unroll
-  for (int i = 0; i < kColRowsPerLane; ++i) {
-    if (r0 + i < rows) C[(r0 + i) * RADIX + d] = run;
-    run += x[i];
+      for (int i = 0; i < kColRowsPerLane; ++i) x[i] = (r0 + h + i < rows) ? C[(r0 + h + i) * RADIX + d] : 0u;
+#pragma unroll
+      for (int i = 0; i < kColRowsPerLane; ++i) {
+        if (r0 + h + i < rows) C[(r0 + h + i) * RADIX + d] = run;
+        run += x[i];
+      }
+    }
+    (void)s_sum;
+    (void)s;
+    return run;
+  } else {
+    const uint64_t r0 = (uint64_t)blockIdx.x * CH + (uint64_t)s * kColRowsPerLane;
+    uint32_t x[kColRowsPerLane];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < kColRowsPerLane; ++i) {
+      x[i] = (r0 + i < rows) ? C[(r0 + i) * RADIX + d] : 0u;
+      sum += x[i];
+    }
+    s_sum[threadIdx.x] = sum;
+    __syncthreads();
+    uint32_t run = 0, tot = 0;
+    for (uint32_t q = 0; q < (uint32_t)L; ++q) {
+      const uint32_t v = s_sum[q * RADIX + d];
+      run += q < s ? v : 0u;
+      tot += v;
+    }
+#pragma unroll
+    for (int i = 0; i < kColRowsPerLane; ++i) {
+      if (r0 + i < rows) C[(r0 + i) * RADIX + d] = run;
+      run += x[i];
+    }
+    return tot;
   }
-  return tot;
 }
 
 // RADIX <= 32: level 1 per block; the last block scans the chunk totals
@@ -994,7 +1018,7 @@ __global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, 
   constexpr int WAVES = BLOCK / kWave;
   constexpr int TILE = BLOCK * ITEMS;
   constexpr int WSPAN = ITEMS * kWave;
-  constexpr int CH = kColRowsPerLane * (256 / RADIX);
+  constexpr int CH = col_chunk_rows(RADIX);
   constexpr int NEXT = 2 * RADIX * RADIX;
   constexpr int SPLIT = 2;  // store phase in two unrolled halves (register pressure)
   constexpr int SP = ITEMS / SPLIT;
@@ -1677,7 +1701,7 @@ uint32_t tp_tiles(size_t n, int bits) {
   return (uint32_t)((n + t - 1) / t);
 }
 inline uint32_t tp_chunks(uint32_t tiles, int bits) {
-  const uint32_t ch = kColRowsPerLane * (256u >> bits);
+  const uint32_t ch = (uint32_t)col_chunk_rows(1 << bits);
   return (tiles + ch - 1) / ch;
 }
 
