@@ -772,7 +772,10 @@ constexpr int kColRowsPerLane = 16;
 // Rows of C per column-scan chunk.  RADIX 256 has one row-lane per column, so
 // a lane walks its chunk's rows in one sequential pass and a chunk can be long
 // (fewer chunk totals for k_colscan_wide, whose column reads are strided).
-constexpr int col_chunk_rows(int radix) { return radix >= 256 ? 64 : kColRowsPerLane * (256 / radix); }
+#ifndef LIBSORT_COL_ROWS256
+#define LIBSORT_COL_ROWS256 64
+#endif
+constexpr int col_chunk_rows(int radix) { return radix >= 256 ? LIBSORT_COL_ROWS256 : kColRowsPerLane * (256 / radix); }
 
 // Per-tile digit counts of the first pass; also zeroes `zero_buf` (the
 // next-pass count buffer).  One block per tile.
