@@ -486,3 +486,40 @@ def test_maximum_size(dev, bits):
     finally:
         pylibsort.setDigitBits(prev)
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("bits", [8, 4])
+def test_config5_pairs_size(dev, bits):
+    """C5's per-GPU share as one sort: 2^28 (u64 key, u32 payload) pairs with
+    the bench's keys (two consecutive PCG draws) and payload = index.  Parity
+    by properties: keys non-decreasing (uint64 order), payloads increasing
+    inside every run of equal keys (stability), and the (key, payload) pairs
+    unchanged as a multiset (checksum of a mix of both)."""
+    import pylibsort
+    prev = pylibsort.setDigitBits(bits)
+    try:
+        n = 1 << 28
+        w = dev.populate_u32(2 * n).view(n, 2).to(torch.int64)
+        keys = (w[:, 0] << 32) | (w[:, 1] & 0xFFFFFFFF)
+        del w
+        keys[: n // 64] = keys[: n // 64] & 0x7FF                  # many equal keys (stability matters)
+        vals = torch.arange(n, dtype=torch.int64, device="cuda").to(torch.int32)
+        ok_, ov = dev.sort_pairs_u64_u32(keys, vals)
+        torch.cuda.synchronize()
+        assert pylibsort.lib().libsortDeviceErrors() == 0
+        flip = torch.tensor(-(1 << 63), dtype=torch.int64, device="cuda")
+        s = torch.bitwise_xor(ok_, flip)
+        v = ov.to(torch.int64) & 0xFFFFFFFF
+        chunk = 1 << 25
+        for i in range(0, n - 1, chunk):
+            a, b = s[i:i + chunk + 1], v[i:i + chunk + 1]
+            assert bool((a[1:] >= a[:-1]).all())
+            eq = a[1:] == a[:-1]
+            assert bool((b[1:][eq] > b[:-1][eq]).all())
+
+        def mix(k, p):
+            return (((k & 0xFFFFFF) * 1000003 + (k >> 40) * 7 + p) % 1000000007).sum()
+        assert int(mix(keys, vals.to(torch.int64) & 0xFFFFFFFF)) == int(mix(ok_, v))
+    finally:
+        pylibsort.setDigitBits(prev)
+        torch.cuda.empty_cache()
