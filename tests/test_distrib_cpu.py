@@ -138,13 +138,14 @@ def test_shard_cut_matches_reference():
     assert shard_cut(10, 4)[1] == [(0, 3), (3, 6), (6, 9), (9, 10)]
 
 
-@pytest.mark.parametrize("world", [4, 8])
-def test_msd_bench_world_sizes_gloo(tmp_path, world):
+@pytest.mark.parametrize("world,schedule", [(4, "msd"), (8, "msd"), (4, "lsd")])
+def test_msd_bench_world_sizes_gloo(tmp_path, world, schedule):
     """The world sizes of the driver's scaling job (4 and 8 ranks) with the
-    bench's default schedule (msd, 4 rounds -> 16 / 32 partition buckets)."""
+    bench's default schedule (msd, 4 rounds -> 16 / 32 partition buckets), and
+    the reference-semantics lsd schedule (the skew fallback) at 4 ranks."""
     from oracle import oracle
     x = oracle.pcg(8 * 20011, first=world)
-    shards = run_ranks(x, world, "msd", tmp_path, port=29900 + world)
+    shards = run_ranks(x, world, schedule, tmp_path, port=29900 + world + 20 * (schedule == "lsd"))
     np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))
     assert [s.size for s in shards] == [s.size for s in shard_inputs(x, world)]
 
