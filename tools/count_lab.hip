@@ -100,6 +100,36 @@ __global__ __launch_bounds__(BLOCK) void k_counts_match(const uint32_t* __restri
   for (uint32_t d = tid; d < RADIX; d += BLOCK) counts[(size_t)blockIdx.x * RADIX + d] = s_h[d];
 }
 
+// TPB tiles per block: every thread issues the loads of all TPB tiles first
+// (more bytes in flight per CU), then counts tile by tile into its own LDS
+// histogram; nontemporal 16-byte loads like the library kernel.
+template <int BITS, int BLOCK, int TPB>
+__global__ __launch_bounds__(BLOCK) void k_counts_multi(const uint32_t* __restrict__ keys, RadixDigit op,
+                                                        uint32_t* __restrict__ counts) {
+  constexpr int RADIX = 1 << BITS;
+  constexpr int TILE = BLOCK * 16;
+  __shared__ uint32_t s_h[TPB][RADIX];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < TPB * RADIX; i += BLOCK) (&s_h[0][0])[i] = 0u;
+  __syncthreads();
+  typedef unsigned int nv4 __attribute__((ext_vector_type(4)));
+  const nv4* vp = reinterpret_cast<const nv4*>(keys + (uint64_t)blockIdx.x * TPB * TILE);
+  nv4 v[TPB][4];
+#pragma unroll
+  for (int t = 0; t < TPB; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[t][j] = __builtin_nontemporal_load(&vp[t * (TILE / 4) + j * BLOCK + tid]);
+#pragma unroll
+  for (int t = 0; t < TPB; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) atomicAdd(&s_h[t][op(v[t][j][q])], 1u);
+  __syncthreads();
+  for (uint32_t i = tid; i < TPB * RADIX; i += BLOCK)
+    counts[(size_t)blockIdx.x * TPB * RADIX + i] = (&s_h[0][0])[i];
+}
+
 struct Variant {
   std::string name;
   std::function<void()> launch;
@@ -135,6 +165,9 @@ int main(int argc, char** argv) {
   add("8b 4 copies", [&] { hipLaunchKernelGGL((k_counts_x<8, 512, 4, false>), dim3(t8), dim3(512), 0, st, keys, op8, c_out); });
   add("8b per-wave", [&] { hipLaunchKernelGGL((k_counts_x<8, 512, 1, true>), dim3(t8), dim3(512), 0, st, keys, op8, c_out); });
   add("8b match", [&] { hipLaunchKernelGGL((k_counts_match<8, 512>), dim3(t8), dim3(512), 0, st, keys, op8, c_out); });
+  add("8b 2 tiles/block", [&] { hipLaunchKernelGGL((k_counts_multi<8, 512, 2>), dim3(t8 / 2), dim3(512), 0, st, keys, op8, c_out); });
+  add("8b 4 tiles/block", [&] { hipLaunchKernelGGL((k_counts_multi<8, 512, 4>), dim3(t8 / 4), dim3(512), 0, st, keys, op8, c_out); });
+  add("8b 1 tile nt", [&] { hipLaunchKernelGGL((k_counts_multi<8, 512, 1>), dim3(t8), dim3(512), 0, st, keys, op8, c_out); });
   // 4-bit, 256-thread tiles (pass-0 counts of 4-bit sorts)
   add("4b lib (16 copies)", [&] {
     hipLaunchKernelGGL((k_tile_counts<4, 256, 16, uint32_t>), dim3(t4), dim3(256), 0, st, keys, (uint32_t)n, op4,
@@ -144,6 +177,8 @@ int main(int argc, char** argv) {
   add("4b 4 interleaved", [&] { hipLaunchKernelGGL((k_counts_x<4, 256, 4, false>), dim3(t4), dim3(256), 0, st, keys, op4, c_out); });
   add("4b per-wave", [&] { hipLaunchKernelGGL((k_counts_x<4, 256, 1, true>), dim3(t4), dim3(256), 0, st, keys, op4, c_out); });
   add("4b match", [&] { hipLaunchKernelGGL((k_counts_match<4, 256>), dim3(t4), dim3(256), 0, st, keys, op4, c_out); });
+  add("4b 2 tiles/block", [&] { hipLaunchKernelGGL((k_counts_multi<4, 256, 2>), dim3(t4 / 2), dim3(256), 0, st, keys, op4, c_out); });
+  add("4b 4 tiles/block", [&] { hipLaunchKernelGGL((k_counts_multi<4, 256, 4>), dim3(t4 / 4), dim3(256), 0, st, keys, op4, c_out); });
 
   // correctness: each family against its library kernel
   std::vector<uint32_t> ref, got;
