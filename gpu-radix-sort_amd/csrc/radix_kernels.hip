@@ -1697,10 +1697,16 @@ constexpr int tp_items() { return sizeof(K) == 8 ? 8 : 16; }
 #ifndef LIBSORT_TP8_BLOCK
 #define LIBSORT_TP8_BLOCK 512  // threads of an 8-bit tile (16 keys each)
 #endif
-constexpr int tp_block(int bits) { return bits == 4 ? 256 : LIBSORT_TP8_BLOCK; }
+#ifndef LIBSORT_TP8_BLOCK64
+#define LIBSORT_TP8_BLOCK64 512  // threads of an 8-bit tile of 64-bit keys (8 keys each)
+#endif
+template <typename K>
+constexpr int tp_block(int bits) {
+  return bits == 4 ? 256 : (sizeof(K) == 8 ? LIBSORT_TP8_BLOCK64 : LIBSORT_TP8_BLOCK);
+}
 template <typename K>
 uint32_t tp_tiles(size_t n, int bits) {
-  const uint64_t t = (uint64_t)tp_block(bits) * tp_items<K>();
+  const uint64_t t = (uint64_t)tp_block<K>(bits) * tp_items<K>();
   return (uint32_t)((n + t - 1) / t);
 }
 inline uint32_t tp_chunks(uint32_t tiles, int bits) {
@@ -1711,7 +1717,7 @@ inline uint32_t tp_chunks(uint32_t tiles, int bits) {
 template <int BITS, typename K, typename Op = RadixDigit>
 hipError_t tiles_counts(Workspace& ws, const K* in, size_t n, Op op, uint32_t tiles, uint32_t* C,
                         uint32_t* zero, uint32_t zero_words, hipStream_t st) {
-  constexpr int B = tp_block(BITS);
+  constexpr int B = tp_block<K>(BITS);
   ScopedTimer tm("tilecounts", st, n);
   hipLaunchKernelGGL((k_tile_counts<BITS, B, tp_items<K>(), K, Op>), dim3(tiles), dim3(B), 0, st, in, (uint32_t)n,
                      op, C, zero, zero_words);
@@ -1755,7 +1761,7 @@ hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, 
 template <int BITS, typename K, typename V, typename Op = RadixDigit>
 hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout, size_t n, int p, int P,
                       int lo, int hi, hipStream_t st, uint32_t bias = 0) {
-  constexpr int B = tp_block(BITS);
+  constexpr int B = tp_block<K>(BITS);
   const uint32_t tiles = tp_tiles<K>(n, BITS);
   const int shift = lo + BITS * p;
   const int nb = std::min(BITS, hi - shift);
@@ -2062,7 +2068,7 @@ hipError_t partition_lut_impl(Workspace& ws, const K* in, K* out, const V* vin, 
                               const uint8_t* d_lut, int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st,
                               int phase) {
   constexpr int RADIX = 1 << BITS;
-  constexpr int B = tp_block(BITS);
+  constexpr int B = tp_block<K>(BITS);
   const uint32_t tiles = tp_tiles<K>(n, BITS);
   const LutDigit op{d_lut, (uint32_t)lut_shift, (uint32_t)RADIX - 1u, nullptr};
   Workspace::PartToken tok{in, vin, n, d_lut, lut_shift, nbuckets, st, true};
