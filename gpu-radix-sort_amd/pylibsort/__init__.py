@@ -18,6 +18,7 @@ instead of silently running anything else.
 """
 import ctypes
 import ctypes.util
+import importlib.util
 import os
 import pathlib
 import types
@@ -100,8 +101,28 @@ def library_path():
     return ctypes.util._findLib_ld("sort")
 
 
+def _preload_torch_hip():
+    """torch ships its own HIP runtime (torch/lib/libamdhip64.so, soname
+    libamdhip64.so.7).  If libsort.so were loaded first it would bring in
+    /opt/rocm's copy, torch would later load its own, and with two HIP
+    runtimes in the process torch sees no GPU ("No HIP GPUs are available").
+    Loading torch's copy first (global, without importing torch) makes
+    libsort.so bind to it: one runtime, whichever of torch and pylibsort is
+    imported first.  Without torch installed this does nothing."""
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return
+    if spec is None or not spec.origin:
+        return
+    hip = pathlib.Path(spec.origin).parent / "lib" / "libamdhip64.so"
+    if hip.exists():
+        ctypes.CDLL(str(hip), mode=ctypes.RTLD_GLOBAL)
+
+
 def _setup():
     s = types.SimpleNamespace()
+    _preload_torch_hip()
     path = library_path()
     if path is None:
         raise RuntimeError("libsort could not be located: build it (python __graft_entry__.py build) "

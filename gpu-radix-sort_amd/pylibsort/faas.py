@@ -11,9 +11,9 @@ Response: {"success": bool, "err": str}.
 f() follows the reference exactly: the referenced partitions are read into one
 host buffer, partially sorted in place by gpuPartial, and written as an array
 with one partition per radix group.  fDevice() produces the same output array
-with the keys staying on the device between the sort and the file write
-(H2D once, device-resident partial sort, one D2H straight into the mapped
-data.dat).
+without host copies of the keys: each input piece goes host -> device straight
+from the memory-mapped data.dat, the partial sort runs device-resident, and
+one D2H lands in the mapped output data.dat.
 """
 import json
 import os
@@ -47,9 +47,9 @@ def fDevice(event):
     import torch
 
     from . import device as D
-    raw = data.readPartRefs(data.getPartRefs(event))
+    refs = data.getPartRefs(event)
     try:
-        keys = torch.from_numpy(np.frombuffer(raw, dtype=np.int32)).cuda()
+        keys = _gather_to_device(refs, np, torch)
         width = int(event["width"])
         bounds = torch.empty(1 << width, dtype=torch.int32, device=keys.device)
         out = D.sort_keys_u32(keys, offset=int(event["offset"]), width=width, boundaries=bounds)
@@ -57,6 +57,30 @@ def fDevice(event):
         return _fail(str(e))
     data.writeOutputDevice(event, out, bounds)
     return {"success": True, "err": ""}
+
+
+def _gather_to_device(refs, np, torch):
+    """The referenced partition bytes, concatenated, as an int32 CUDA tensor:
+    each piece is copied host -> device straight from the memory-mapped
+    data.dat (no intermediate host buffer)."""
+    total = sum(r.nbyte for r in refs)
+    if total % 4:
+        raise ValueError("input is not a whole number of uint32 keys")
+    keys = torch.empty(total // 4, dtype=torch.int32, device="cuda")
+    flat = keys.view(torch.uint8)
+    pos = 0
+    for r in refs:
+        if r.nbyte == 0:
+            continue
+        used = r.arr.shape.lens[r.partID]
+        if r.start < 0 or r.start + r.nbyte > used:
+            raise data.DistribArrayError("Read beyond end of partition {}".format(r.partID))
+        mm = np.memmap(r.arr.datPath, dtype=np.uint8, mode="c", offset=r.arr.shape.starts[r.partID] + r.start,
+                       shape=(r.nbyte,))
+        flat[pos:pos + r.nbyte].copy_(torch.from_numpy(np.asarray(mm)))
+        del mm
+        pos += r.nbyte
+    return keys
 
 
 def directInvoke(argv=None, stdin=None, stdout=None):

@@ -157,3 +157,18 @@ def test_c_caller_links_against_reference_layout(tmp_path):
     assert out.returncode == 0, out.stderr
     # smallest of the first 8 reference PCG words (tests/golden/pcg_golden.json)
     assert out.stdout.strip() == "0f55ac5f"
+
+
+@pytest.mark.parametrize("order", ["pylibsort_first", "torch_first"])
+def test_one_hip_runtime_per_process(order):
+    """torch bundles its own HIP runtime; pylibsort must bind libsort.so to it
+    whichever is imported first (two runtimes in one process leave torch
+    without a GPU)."""
+    pytest.importorskip("torch")
+    first, second = ("pylibsort", "torch") if order == "pylibsort_first" else ("torch", "pylibsort")
+    code = ("import sys; sys.path.insert(0, %r); import %s; import %s; "
+            "maps = open('/proc/self/maps').read(); "
+            "print(len({l.split()[-1] for l in maps.splitlines() if 'libamdhip64' in l}))"
+            % (str(ROOT / "gpu-radix-sort_amd"), first, second))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True).stdout
+    assert out.split()[-1] == "1"

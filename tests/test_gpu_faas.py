@@ -84,3 +84,23 @@ def test_direct_invoke(mount, oracle_mod, monkeypatch):
     assert json.loads(out.getvalue()) == {"success": True, "err": ""}
     got = np.fromfile(mount / "dout" / "data.dat", dtype=np.uint32)
     np.testing.assert_array_equal(got, oracle_mod.partial_u32(x, 4, 4)[0])
+
+
+def test_worker_device_path_when_pylibsort_is_imported_first(tmp_path):
+    """As faasTest/f.py does: import pylibsort, then the device handler needs
+    torch on the GPU (fresh process, so the import order is real)."""
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    code = ("import sys; sys.path[:0] = [%r, %r]; import pylibsort; from pylibsort import data, faas; "
+            "import numpy as np; from oracle import oracle; import pathlib; d = pathlib.Path(%r); "
+            "data.SetDistribMount(d); x = oracle.pcg(100000); "
+            "a = data.fileDistribArray.Create(d / 'in', data.ArrayShape.fromUniform(x.nbytes, 1)); "
+            "a.WriteAll(x.tobytes()); a.Close(); "
+            "r = faas.fDevice({'offset': 0, 'width': 8, 'arrType': 'file', "
+            "'input': [{'arrayName': 'in', 'partID': 0, 'start': 0, 'nbyte': -1}], 'output': 'out'}); "
+            "assert r['success'], r; "
+            "assert np.array_equal(np.fromfile(d / 'out' / 'data.dat', dtype=np.uint32), oracle.partial_u32(x, 0, 8)[0]); "
+            "print('OK')" % (str(root), str(root / "gpu-radix-sort_amd"), str(tmp_path)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])

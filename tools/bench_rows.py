@@ -86,7 +86,8 @@ def row3():
             for i in range(4):
                 req = {"offset": 0, "width": 8, "arrType": "file", "input": refs, "output": "o%d" % i}
                 t0 = time.perf_counter()
-                assert fn(req)["success"]
+                resp = fn(req)
+                assert resp["success"], resp["err"]
                 ts.append(time.perf_counter() - t0)
                 data.closeOpenArrays()
             got = np.fromfile(root / "o3" / "data.dat", dtype=np.uint32)
