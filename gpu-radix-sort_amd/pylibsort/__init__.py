@@ -108,7 +108,11 @@ def _preload_torch_hip():
     runtimes in the process torch sees no GPU ("No HIP GPUs are available").
     Loading torch's copy first (global, without importing torch) makes
     libsort.so bind to it: one runtime, whichever of torch and pylibsort is
-    imported first.  Without torch installed this does nothing."""
+    imported first.  Without torch installed this does nothing;
+    LIBSORT_HIP_RUNTIME=system keeps the image's runtime (a process that never
+    imports torch, e.g. the reference's FaaS worker flow)."""
+    if os.environ.get("LIBSORT_HIP_RUNTIME", "torch") == "system":
+        return
     try:
         spec = importlib.util.find_spec("torch")
     except (ImportError, ValueError):

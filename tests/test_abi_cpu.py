@@ -3,6 +3,7 @@ include/libsort.h declares, the header compiles as C (cgo, gnu99) and C++,
 host-only entry points behave like the reference, and the GPU entry points
 fail loudly (no silent CPU fallback)."""
 import ctypes
+import os
 import pathlib
 import re
 import subprocess
@@ -172,3 +173,17 @@ def test_one_hip_runtime_per_process(order):
             % (str(ROOT / "gpu-radix-sort_amd"), first, second))
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True).stdout
     assert out.split()[-1] == "1"
+
+
+def test_system_runtime_opt_out():
+    """LIBSORT_HIP_RUNTIME=system (a torch-free worker) keeps the image's HIP
+    runtime, which moves pageable host buffers faster than torch's."""
+    code = ("import sys; sys.path.insert(0, %r); import pylibsort; "
+            "maps = open('/proc/self/maps').read(); "
+            "print(sorted({l.split()[-1] for l in maps.splitlines() if 'libamdhip64' in l}))"
+            % str(ROOT / "gpu-radix-sort_amd"))
+    env = dict(os.environ, LIBSORT_HIP_RUNTIME="system")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True,
+                         env=env).stdout
+    libs = eval(out.strip().splitlines()[-1])
+    assert len(libs) == 1 and "torch" not in libs[0]
