@@ -1303,39 +1303,85 @@ __global__ __launch_bounds__(256) void k_segment_copy2d(const uint32_t* __restri
 // ----------------------------------------------------------------------------
 // multi-GPU round plan (pylibsort.distrib.sort_msd) on the device
 // ----------------------------------------------------------------------------
-// Sampled top-bit histogram as one int64 row: out[0..bins) = counts of
-// key >> shift over every `stride`-th block of `block` keys (all keys when
-// n < 4 * stride * block, as HipOps.sample), out[bins] = n (the rank's key
-// count, gathered with the histogram).  k_plan_hist accumulates into tmp
-// (zero on entry), k_plan_hist_out converts and re-zeroes it.
+
+// Sampled top-bit histogram of the multi-GPU plan: key >> shift over every
+// `stride`-th block of `block` keys, i.e. sampled block sb starts at sb *
+// step (step = stride * block; all keys, step = block, when n < 4 * stride *
+// block, as HipOps.sample).  Workgroup g histograms sampled blocks g, g + G,
+// ... in LDS with 16-byte loads and writes its whole row rows[g][*]: no
+// global atomics and no per-key 64-bit index arithmetic (the first version,
+// one 64-bit div/mod per key and 4096 global atomics per workgroup, took
+// 89 us at 2^28 keys).  k_plan_hist_out sums the rows, out[bins] = n.
 template <int BITS>
-__global__ __launch_bounds__(256) void k_plan_hist(const uint32_t* __restrict__ keys, uint64_t n, uint32_t shift,
-                                                   uint64_t block, uint64_t stride, uint32_t* __restrict__ tmp) {
-  constexpr int BINS = 1 << BITS;
+__global__ __launch_bounds__(512) void k_plan_hist(const uint32_t* __restrict__ keys, uint64_t n, uint32_t shift,
+                                                   uint32_t block, uint64_t step, uint64_t nsb, bool full_blocks,
+                                                   uint32_t* __restrict__ rows) {
+  constexpr int BINS = 1 << BITS, T = 512, U = 4;
   __shared__ uint32_t s_h[BINS];
-  for (int i = threadIdx.x; i < BINS; i += 256) s_h[i] = 0u;
+  for (int i = threadIdx.x; i < BINS; i += T) s_h[i] = 0u;
   __syncthreads();
-  const uint64_t nb = n / block;
-  const bool sampled = stride > 1 && nb >= 4 * stride;
-  const uint64_t m = sampled ? ((nb + stride - 1) / stride) * block : n;  // sampled keys
-  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) {
-    const uint64_t src = sampled ? (i / block) * stride * block + i % block : i;
-    atomicAdd(&s_h[(keys[src] >> shift) & (BINS - 1)], 1u);
+  const uint32_t G = gridDim.x;
+  if (full_blocks && ((uintptr_t)keys & 15u) == 0 && (block & 3u) == 0 && (step & 3u) == 0) {
+    // this workgroup's sampled blocks blockIdx.x + k * G as one flat range
+    // of 16-byte vectors, U loads in flight per thread
+    const uint32_t per = block >> 2;
+    const uint32_t total = (uint32_t)((nsb - blockIdx.x + G - 1) / G) * per;
+    auto addr = [&](uint32_t q) {
+      const uint64_t sb = blockIdx.x + (uint64_t)(q / per) * G;
+      return reinterpret_cast<const uint4*>(keys + sb * step) + (q % per);
+    };
+    uint32_t q = threadIdx.x;
+    for (; q + (U - 1) * T < total; q += U * T) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = load_count_vec(addr(q + u * T));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        atomicAdd(&s_h[(v[u].x >> shift) & (BINS - 1)], 1u);
+        atomicAdd(&s_h[(v[u].y >> shift) & (BINS - 1)], 1u);
+        atomicAdd(&s_h[(v[u].z >> shift) & (BINS - 1)], 1u);
+        atomicAdd(&s_h[(v[u].w >> shift) & (BINS - 1)], 1u);
+      }
+    }
+    for (; q < total; q += T) {
+      const uint4 v = load_count_vec(addr(q));
+      atomicAdd(&s_h[(v.x >> shift) & (BINS - 1)], 1u);
+      atomicAdd(&s_h[(v.y >> shift) & (BINS - 1)], 1u);
+      atomicAdd(&s_h[(v.z >> shift) & (BINS - 1)], 1u);
+      atomicAdd(&s_h[(v.w >> shift) & (BINS - 1)], 1u);
+    }
+  } else {
+    for (uint64_t sb = blockIdx.x; sb < nsb; sb += G) {
+      const uint64_t start = sb * step;
+      const uint32_t len = (uint32_t)umin64((uint64_t)block, n - start);
+      for (uint32_t i = threadIdx.x; i < len; i += T) atomicAdd(&s_h[(keys[start + i] >> shift) & (BINS - 1)], 1u);
+    }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < BINS; i += 256) {
-    const uint32_t c = s_h[i];
-    if (c) atomicAdd(&tmp[i], c);
-  }
+  uint32_t* row = rows + (size_t)blockIdx.x * BINS;
+  for (int i = threadIdx.x; i < BINS; i += T) row[i] = s_h[i];
 }
 
-__global__ __launch_bounds__(256) void k_plan_hist_out(uint32_t* __restrict__ tmp, uint32_t bins, uint64_t n,
-                                                       int64_t* __restrict__ out) {
-  for (uint32_t i = threadIdx.x; i < bins; i += 256) {
-    out[i] = (int64_t)tmp[i];
-    tmp[i] = 0u;
+// Column sums of rows[G][bins] -> out (int64), out[bins] = n.  Block b sums
+// 16 columns: thread (r, c) adds rows r, r + 16, ... of column 16b + c, then
+// the 16 partial sums meet in LDS (rows in parallel, not one column per
+// thread walking all G rows).
+__global__ __launch_bounds__(256) void k_plan_hist_out(const uint32_t* __restrict__ rows, uint32_t G, uint32_t bins,
+                                                       uint64_t n, int64_t* __restrict__ out) {
+  __shared__ uint32_t s_p[16][17];
+  const uint32_t c = threadIdx.x & 15u, r = threadIdx.x >> 4, col = blockIdx.x * 16 + c;
+  uint32_t s = 0;
+  if (col < bins)
+    for (uint32_t g = r; g < G; g += 16) s += rows[(size_t)g * bins + col];
+  s_p[r][c] = s;
+  __syncthreads();
+  if (threadIdx.x < 16 && col < bins) {
+    uint64_t t = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += s_p[i][c];
+    out[col] = (int64_t)t;
   }
-  if (threadIdx.x == 0) out[bins] = (int64_t)n;
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[bins] = (int64_t)n;
 }
 
 // Round plan from the gathered rows H[R][ld] (first 4096 entries = the
@@ -2173,24 +2219,24 @@ hipError_t segment_copy_u32(Workspace& ws, const uint32_t* src, uint32_t* dst, s
 
 hipError_t plan_hist_u32(Workspace& ws, const uint32_t* keys, size_t n, int bits, uint64_t block, uint64_t stride,
                          int64_t* d_out, hipStream_t st) {
-  if (bits != 12 || block == 0) return hipErrorInvalidValue;
-  if (ws.hist_tmp_cap < 4096) {
+  constexpr uint32_t BINS = 4096;
+  if (bits != 12 || block == 0 || block > 0xffffffffull) return hipErrorInvalidValue;
+  const uint64_t nb = n / block;
+  const bool sampled = stride > 1 && nb >= 4 * stride;
+  const uint64_t nsb = sampled ? (nb + stride - 1) / stride : (n + block - 1) / block;
+  const uint64_t step = sampled ? stride * block : block;
+  const uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nsb, (uint64_t)std::max(1, ws.num_cus)));
+  if (ws.hist_tmp_cap < (size_t)G * BINS) {
     if (ws.hist_tmp) { (void)hipFree(ws.hist_tmp); ws.hist_tmp = nullptr; }
     ws.hist_tmp_cap = 0;
-    LS_TRY(hipMalloc(&ws.hist_tmp, 4096 * sizeof(uint32_t)));
-    ws.hist_tmp_cap = 4096;
-    LS_TRY(hipMemsetAsync(ws.hist_tmp, 0, 4096 * sizeof(uint32_t), st));  // k_plan_hist_out keeps it zero
+    LS_TRY(hipMalloc(&ws.hist_tmp, (size_t)G * BINS * sizeof(uint32_t)));
+    ws.hist_tmp_cap = (size_t)G * BINS;
   }
   ScopedTimer tm("histogram", st, n);
-  const uint64_t sampled = stride > 1 && n / block >= 4 * stride ? n / stride : n;
-  const uint32_t blocks =
-      (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((sampled + 1023) / 1024, (uint64_t)std::max(1, ws.num_cus) * 2));
-  if (n) {
-    hipLaunchKernelGGL(k_plan_hist<12>, dim3(blocks), dim3(256), 0, st, keys, (uint64_t)n, 32u - 12u, block, stride,
-                       ws.hist_tmp);
-    LS_TRY(hipGetLastError());
-  }
-  hipLaunchKernelGGL(k_plan_hist_out, dim3(1), dim3(256), 0, st, ws.hist_tmp, 4096u, (uint64_t)n, d_out);
+  hipLaunchKernelGGL(k_plan_hist<12>, dim3(G), dim3(512), 0, st, keys, (uint64_t)n, 32u - 12u, (uint32_t)block, step,
+                     nsb, sampled, ws.hist_tmp);
+  LS_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_plan_hist_out, dim3(BINS / 16), dim3(256), 0, st, ws.hist_tmp, G, BINS, (uint64_t)n, d_out);
   return hipGetLastError();
 }
 

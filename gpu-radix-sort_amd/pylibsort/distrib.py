@@ -125,15 +125,15 @@ class HipOps:
     def partition_lut_count_t(self, keys, lut, shift, nbuckets):
         """Count half of the split table partition: bucket starts (int64,
         device) while nothing has moved yet."""
-        b = self.D.partition_lut_count_u32(keys, lut.contiguous(), shift, nbuckets)
-        return b.to(torch.int64) & 0xFFFFFFFF
+        # uint32 starts in an int32 tensor; _sizes_from_starts widens them on
+        # the side stream, so nothing is queued between count and scatter
+        return self.D.partition_lut_count_u32(keys, lut.contiguous(), shift, nbuckets)
 
     def partition_lut_scatter_t(self, keys, lut, shift, nbuckets):
         return self.D.partition_lut_scatter_u32(keys, lut.contiguous(), shift, nbuckets, out=self.empty(keys.numel()))
 
     def partition_lut_pairs_count_t(self, keys, vals, lut, shift, nbuckets):
-        b = self.D.partition_lut_pairs_count_u64_u32(keys, vals, lut.contiguous(), shift, nbuckets)
-        return b.to(torch.int64) & 0xFFFFFFFF
+        return self.D.partition_lut_pairs_count_u64_u32(keys, vals, lut.contiguous(), shift, nbuckets)
 
     def partition_lut_pairs_scatter_t(self, keys, vals, lut, shift, nbuckets):
         n = keys.numel()
@@ -215,6 +215,44 @@ class _HostCopy:
 
 def _to_host_async(t):
     return _HostCopy(t)
+
+
+_side_streams = {}
+
+
+class _SideWork:
+    """Context for bookkeeping work (bucket sizes, their all-gather, the
+    small D2H) that must not delay the partition scatter: on the GPU it runs
+    on a side stream that waits only for the current stream's work up to
+    this object's creation, so the scatter can be queued (and start) first;
+    `uses` are the current-stream tensors it reads."""
+
+    def __init__(self, *uses):
+        self.uses = uses
+        self.ctx = None
+        self.ev = None
+        if uses[0].is_cuda:
+            self.ev = torch.cuda.Event()
+            self.ev.record()
+
+    def __enter__(self):
+        t = self.uses[0]
+        if self.ev is None:
+            return self
+        side = _side_streams.get(t.device)
+        if side is None:
+            side = _side_streams[t.device] = torch.cuda.Stream(device=t.device)
+        side.wait_event(self.ev)
+        for u in self.uses:
+            u.record_stream(side)
+        self.ctx = torch.cuda.stream(side)
+        self.ctx.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+        return False
 
 
 def _alltoallv(send, send_counts, recv_counts, ops, group):
@@ -403,7 +441,9 @@ def _plan(ops, HN, R, K):
 
 
 def _sizes_from_starts(b_t, n):
-    """Bucket sizes (int64) from bucket starts, without a host round trip."""
+    """Bucket sizes (int64) from bucket starts (int64, or uint32 held in an
+    int32 tensor), without a host round trip."""
+    b_t = b_t.to(torch.int64) & 0xFFFFFFFF
     sizes = torch.empty(b_t.numel(), dtype=torch.int64, device=b_t.device)
     if b_t.numel():
         sizes[:-1] = b_t[1:] - b_t[:-1]
@@ -476,17 +516,21 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=4, s
     _mark(trace, "histogram+allgather+plan")
     split = hasattr(ops, "partition_lut_count_t")
     if split:
-        # sizes first: counts + scan, gather, start the small D2H, and only
-        # then queue the scatter, so the host plans and issues the exchange
-        # while the data moves (the one host synchronisation waits for the sizes)
+        # counts + scan, then the scatter right away; the sizes, their gather
+        # and the small D2H run on a side stream beside it, so the host plans
+        # and issues the exchange while the data moves (the one host
+        # synchronisation waits for the sizes only)
         b_t = ops.partition_lut_count_t(keys, lut_t, 32 - HIST_BITS, NB)
+        side = _SideWork(b_t, HN, est_t, lut_t)
+        part = ops.partition_lut_scatter_t(keys, lut_t, 32 - HIST_BITS, NB)
     else:
         part, b_t = ops.partition_lut_t(keys, lut_t, 32 - HIST_BITS, NB)
-    sizes_t = _sizes_from_starts(b_t, n)
-    C_t = _allgather_t(sizes_t, group)                         # [R, NB], bucket j = round * R + dest
-    pending = _to_host_async(torch.cat([C_t.flatten(), HN[:, -1], est_t.to(torch.int64), lut_t.to(torch.int64)]))
-    if split:
-        part = ops.partition_lut_scatter_t(keys, lut_t, 32 - HIST_BITS, NB)
+        side = _SideWork(b_t, HN, est_t, lut_t)
+    with side:                                                 # beside the scatter, not before it
+        sizes_t = _sizes_from_starts(b_t, n)
+        C_t = _allgather_t(sizes_t, group)                     # [R, NB], bucket j = round * R + dest
+        pending = _to_host_async(torch.cat([C_t.flatten(), HN[:, -1], est_t.to(torch.int64),
+                                            lut_t.to(torch.int64)]))
     host = pending.wait()
     _mark(trace, "partition+allgather sizes")
     C = host[:R * NB].reshape(R, NB)
@@ -576,13 +620,15 @@ def _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride, self_local
     split = hasattr(ops, "partition_lut_pairs_count_t")
     if split:
         b_t = ops.partition_lut_pairs_count_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
+        side = _SideWork(b_t)
+        pk, pv = ops.partition_lut_pairs_scatter_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
     else:
         pk, pv, b_t = ops.partition_lut_pairs_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
-    sizes_t = _sizes_from_starts(b_t, n)
-    C_t = _allgather_t(sizes_t, group)
-    pending = _to_host_async(C_t)
-    if split:
-        pk, pv = ops.partition_lut_pairs_scatter_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
+        side = _SideWork(b_t)
+    with side:
+        sizes_t = _sizes_from_starts(b_t, n)
+        C_t = _allgather_t(sizes_t, group)
+        pending = _to_host_async(C_t)
     C = pending.wait()                                         # the one host transfer
     sizes = C[r]
     b = np.concatenate([[0], np.cumsum(sizes)[:-1]])
