@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--keys-log2", type=int, default=None, help="keys (pairs) per GPU = 2^k")
     ap.add_argument("--digit-bits", type=int, default=None, help="configs[1] names 4-bit digits")
     ap.add_argument("--schedule", default="msd", choices=["msd", "lsd"])
-    ap.add_argument("--rounds", type=int, default=4, help="msd exchange rounds")
+    ap.add_argument("--rounds", type=int, default=4, help="msd exchange rounds (pylibsort.distrib.ROUNDS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=26)
     ap.add_argument("--no-variants", action="store_true")

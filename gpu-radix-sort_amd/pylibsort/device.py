@@ -287,7 +287,7 @@ def plan_histogram_u32(keys, block=4096, stride=16, out=None):
     return out
 
 
-def plan_rounds(rows, nranks, rounds, growth=1.6, lut=None, est=None):
+def plan_rounds(rows, nranks, rounds, growth=1.2, lut=None, est=None):
     """(lut uint8[4096], est int64[nranks]) of the msd round plan from the
     gathered int64 rows [nranks, ld >= 4096] (histogram first)."""
     _need(rows, _U64, "rows")

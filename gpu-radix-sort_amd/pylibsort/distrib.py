@@ -36,6 +36,14 @@ import torch
 import torch.distributed as dist
 
 HIST_BITS = 12
+# msd exchange rounds and their size growth.  A round's exchange overlaps the
+# previous round's sort; the first round's exchange and the last round's sort
+# are exposed, and every round costs ~0.1 ms of kernel boundaries (measured).
+# Modelled over exchange times of 1.5-4 ms per 2^28 keys per GPU (DESIGN.md
+# section 7), 4 rounds growing x1.2 gain 0.1-0.4 ms over x1.6 once the
+# exchange takes 2.35 ms or more and lose <= 0.15 ms when it is faster.
+ROUNDS = 4
+GROWTH = 1.2
 
 
 class HipOps:
@@ -151,9 +159,9 @@ class HipOps:
         libsort call instead of sample copy + histogram + cat)."""
         return self.D.plan_histogram_u32(keys, block=block, stride=stride)
 
-    def plan(self, rows, R, K, growth=1.6):
+    def plan(self, rows, R, K, growth=None):
         """(lut uint8[4096], est int64[R]) from the gathered rows, on the device."""
-        return self.D.plan_rounds(rows.contiguous(), R, K, growth)
+        return self.D.plan_rounds(rows.contiguous(), R, K, GROWTH if growth is None else growth)
 
     def sample(self, keys, stride, block=4096):
         """Every `stride`-th block of `block` keys (all keys when few)."""
@@ -451,13 +459,14 @@ def _sizes_from_starts(b_t, n):
     return sizes
 
 
-def _plan_rounds_t(H, R, K, growth=1.6):
+def _plan_rounds_t(H, R, K, growth=None):
     """plan_rounds on torch tensors, on H's device (the GPU under RCCL, so the
     plan needs no host round trip).  Returns (lut uint8, est float64)."""
     G = H.sum(dim=0).to(torch.float64)
     T = G.sum().clamp(min=1.0)                                 # all-zero histograms -> one group
     x = (torch.cumsum(G, 0) - G / 2.0) / T * R                 # rank coordinate of each bucket's middle
     rank = torch.clamp(torch.floor(x).to(torch.int64), max=R - 1)
+    growth = GROWTH if growth is None else growth
     w = growth ** torch.arange(K, dtype=torch.float64, device=H.device)
     cw = torch.cumsum(w, 0) / w.sum()
     rnd = torch.clamp(torch.searchsorted(cw, (x - rank).contiguous(), right=True), max=K - 1)
@@ -468,7 +477,7 @@ def _plan_rounds_t(H, R, K, growth=1.6):
     return lut, est
 
 
-def plan_rounds(H, R, K, hist_bits=HIST_BITS, growth=1.6):
+def plan_rounds(H, R, K, hist_bits=HIST_BITS, growth=None):
     """Contiguous top-bit bucket ranges for (rank, round) from the gathered
     (possibly sampled) histograms H[R, 2^b]: each rank gets about 1/R of the
     estimated keys, split into K rounds whose sizes grow by `growth` (a small
@@ -499,14 +508,14 @@ def _mark(trace, label):
         trace.append((label, time.perf_counter()))
 
 
-def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=4, sample_stride=16, self_local=True,
+def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None, sample_stride=16, self_local=True,
              trace=None):
     """Range-split rounds schedule; see module docstring.  `trace` (a list)
     records synchronised timestamps of the steps (diagnostics only)."""
     R = dist.get_world_size(group)
     r = dist.get_rank(group)
     _mark(trace, "start")
-    K = max(1, min(int(rounds), 256 // R))
+    K = max(1, min(int(ROUNDS if rounds is None else rounds), 256 // R))
     n = keys.numel()
     NB = R * K
     # histogram -> allgather -> plan -> partition -> allgather of the exact
@@ -589,7 +598,7 @@ def _rebalance_pairs(keys, vals, n_all, ops, group):
     return rk, rv
 
 
-def distrib_sort_pairs(keys, vals, ops=None, group=None, rounds=4, sample_stride=16):
+def distrib_sort_pairs(keys, vals, ops=None, group=None, rounds=None, sample_stride=16):
     """Stable sort of the distributed (uint64 key, uint32 payload) array whose
     rank-r shard is (keys, vals) -- SURVEY C5.  The "msd" range-split rounds of
     sort_msd on the top 12 bits of the key: one stable pair partition
@@ -610,7 +619,7 @@ def _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride, self_local
     """The round schedule of distrib_sort_pairs (any world size)."""
     R = dist.get_world_size(group)
     r = dist.get_rank(group)
-    K = max(1, min(int(rounds), 256 // R))
+    K = max(1, min(int(ROUNDS if rounds is None else rounds), 256 // R))
     n = keys.numel()
     NB = R * K
     hi = ops.sample_hi(keys, sample_stride)

@@ -68,6 +68,16 @@ def main():
                 D.sort_keys_range_u32(narrow[i * m:(i + 1) * m], lo, lo + (1 << 27), out=out[i * m:(i + 1) * m],
                                       tmp=tmp[:m])
         res["range27_sort_%d_rounds_ms" % K] = timed(rounds_range, reps=5)
+    for K in (4, 6, 8, 12):                  # K equal rounds of a rank's 2^29-wide range (R = 8)
+        m = n // K
+        span = (1 << 29) // K
+        narrowK = (keys % span) + lo
+
+        def rounds_k():
+            for i in range(K):
+                D.sort_keys_range_u32(narrowK[i * m:(i + 1) * m], lo, lo + span, out=out[i * m:(i + 1) * m],
+                                      tmp=tmp[:m])
+        res["r8_equal_%d_rounds_ms" % K] = timed(rounds_k, reps=5)
     print({k: round(v, 3) for k, v in res.items()})
 
 
