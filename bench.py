@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=26)
     ap.add_argument("--no-variants", action="store_true")
+    ap.add_argument("--no-host-abi", action="store_true", help="skip the PCIe-inclusive providedGpu leg")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--algo", default=None, choices=["auto", "tiles", "onesweep", "rts"],
                     help="force the pass algorithm (LIBSORT_ALGO)")
@@ -239,6 +240,9 @@ def main():
             variants["digit8"] = {"ms_per_step": round(ms8, 4), "value": round(n / (ms8 * 1e-3) / 1e9, 3),
                                   "note": "same sort with 8-bit digits (4 passes, configs[2] digit width); output "
                                           "checked equal to the 4-bit sort"}
+        host_abi = None
+        if world == 1 and not args.no_host_abi and args.workload == "c2":
+            host_abi = host_abi_leg(torch, pylibsort, keys, out)
         sched = ""
         if world > 1:
             sched = (", msd schedule, %d rounds, over %d GPUs (RCCL alltoallv)" % (args.rounds, world)
@@ -276,6 +280,7 @@ def main():
             "kernels": kern,
             "verified": verified,
             "variants": variants or None,
+            "host_abi": host_abi,
         }
         if rehearsal:
             line["rehearsal"] = "gloo, all ranks on one GPU: exercises the N>1 path, not a measurement"
@@ -283,6 +288,32 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def host_abi_leg(torch, pylibsort, keys, sorted_keys, calls=3):
+    """the C-ABI end-to-end time (providedGpu on a
+    pageable host buffer: H2D + sort + D2H), as the reference's callers see
+    it.  Reported beside `value`, never as it; checked against the
+    device-resident sort."""
+    import numpy as np
+    src = keys.cpu().numpy()
+    want = sorted_keys.cpu().numpy()
+    buf = np.empty_like(src)
+    L = pylibsort.lib()
+    ts = []
+    for _ in range(calls):
+        np.copyto(buf, src)
+        t0 = time.perf_counter()
+        if L.providedGpu(buf.ctypes.data, buf.size) != 1:
+            raise RuntimeError("providedGpu failed: %s" % pylibsort.last_error())
+        ts.append(time.perf_counter() - t0)
+    if not np.array_equal(buf, want):
+        raise RuntimeError("providedGpu disagrees with the device-resident sort")
+    t = sorted(ts)[len(ts) // 2]
+    return {"call": "providedGpu (libsort.h, invokers.cu:45-64) on a pageable host buffer", "ms": round(t * 1e3, 2),
+            "value": round(keys.numel() / t / 1e9, 3), "unit": "Gkeys/s", "calls": calls,
+            "note": "PCIe-inclusive (H2D + sort + D2H, median of %d calls), never `value`; "
+                    "output checked equal to the device-resident sort" % calls}
 
 
 def verify(torch, dist, world, keys, res, vals=None):

@@ -14,7 +14,7 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-variants"
+BENCH="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-variants --no-host-abi"
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c -d "$OUT/pmc_$c" -o run --output-format csv \
     --kernel-include-regex "tile_pass|onesweep|downsweep|tile_counts" -- $BENCH > "$OUT/pmc_$c.log" 2>&1
