@@ -124,6 +124,34 @@ def test_plan_histogram(n, stride):
     assert row[4096] == n
 
 
+def _sampled_ref(x, block, stride):
+    """Keys the plan histogram samples: every stride-th block of `block` keys
+    (all keys when there are fewer than 4 * stride whole blocks)."""
+    nb = x.size // block
+    if stride <= 1 or nb < 4 * stride:
+        return x
+    return np.concatenate([x[sb * stride * block:sb * stride * block + block]
+                           for sb in range(-(-nb // stride))])
+
+
+@pytest.mark.parametrize("n,stride,block,offset", [((1 << 22) + 5, 16, 4096, 1), ((1 << 22) + 3, 16, 4096, 3),
+                                                   ((1 << 21) + 7, 8, 1002, 0), ((1 << 21), 8, 1000, 0),
+                                                   (5000, 4, 64, 1)])
+def test_plan_histogram_layouts(n, stride, block, offset):
+    """The plan histogram's scalar paths: a keys pointer off 16-byte alignment
+    (a slice), block sizes that are not multiples of 4, sampled and unsampled."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pylibsort.device as D
+    from oracle import oracle
+    x = oracle.pcg(n + offset, first=n)
+    t = torch.from_numpy(x.view(np.int32)).cuda()[offset:]
+    row = D.plan_histogram_u32(t, block=block, stride=stride).cpu().numpy()
+    ref = np.bincount(_sampled_ref(x[offset:], block, stride) >> 20, minlength=4096)
+    np.testing.assert_array_equal(row[:4096], ref)
+    assert row[4096] == n
+
+
 def test_bench_multi_rank_path_rehearsal():
     """bench.py's N>1 path end to end (2 ranks, gloo, both on the one GPU of
     the test box): timed distributed sorts, max-over-ranks timing, the
