@@ -922,6 +922,41 @@ LIBSORT_EXPORT int libsortPlanRounds(const int64_t* d_rows, uint32_t nranks, uin
              : 0;
 }
 
+LIBSORT_EXPORT int libsortDeltaMaxGapU32(const uint32_t* d_keys, size_t n, uint32_t* d_maxgap, void* stream) {
+  if (!d_maxgap || (n > 0 && !d_keys)) {
+    set_error("libsortDeltaMaxGapU32: bad arguments");
+    return 0;
+  }
+  return hip_ok(delta_maxgap_u32(d_keys, n, d_maxgap, as_stream(stream)), "libsortDeltaMaxGapU32") ? 1 : 0;
+}
+
+LIBSORT_EXPORT int libsortDeltaPackU32(const uint32_t* d_keys, size_t n, const uint32_t* d_maxgap, uint32_t* d_out,
+                                       void* stream) {
+  if (!d_maxgap || (n > 0 && (!d_keys || !d_out))) {
+    set_error("libsortDeltaPackU32: bad arguments");
+    return 0;
+  }
+  return hip_ok(delta_pack_u32(d_keys, n, d_maxgap, d_out, as_stream(stream)), "libsortDeltaPackU32") ? 1 : 0;
+}
+
+LIBSORT_EXPORT int libsortDeltaUnpackU32(const uint32_t* d_in, size_t n, uint32_t bits, uint32_t* d_keys,
+                                         void* stream) {
+  if (bits > 32 || (n > 0 && (!d_in || !d_keys))) {
+    set_error("libsortDeltaUnpackU32: bad arguments");
+    return 0;
+  }
+  return hip_ok(delta_unpack_u32(d_in, n, bits, d_keys, as_stream(stream)), "libsortDeltaUnpackU32") ? 1 : 0;
+}
+
+LIBSORT_EXPORT int libsortMergeU32(const uint32_t* d_a, size_t na, const uint32_t* d_b, size_t nb, uint32_t* d_out,
+                                   void* stream) {
+  if ((na > 0 && !d_a) || (nb > 0 && !d_b) || (na + nb > 0 && !d_out) || (d_out && (d_out == d_a || d_out == d_b))) {
+    set_error("libsortMergeU32: bad arguments (out must be distinct from both inputs)");
+    return 0;
+  }
+  return hip_ok(merge_u32(d_a, na, d_b, nb, d_out, as_stream(stream)), "libsortMergeU32") ? 1 : 0;
+}
+
 LIBSORT_EXPORT int libsortPopulateDevice(uint32_t* d_out, size_t n, uint64_t first, void* stream) {
   return hip_ok(populate_device(d_out, n, first, as_stream(stream)), "libsortPopulateDevice") ? 1 : 0;
 }

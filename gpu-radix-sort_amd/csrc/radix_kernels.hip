@@ -1301,6 +1301,144 @@ __global__ __launch_bounds__(256) void k_segment_copy2d(const uint32_t* __restri
 }
 
 // ----------------------------------------------------------------------------
+// delta-coded exchange of sorted runs (pylibsort.distrib "msdz" schedule for
+// link-bound world sizes): groups of 64 consecutive keys of a sorted run keep
+// their first key as a 32-bit base and the 63 gaps to the previous key in w
+// bits, w = bits of the largest in-group gap of the whole run.  Layout:
+// bases[ng] then ng groups of 2w dwords (64 gaps x w bits; lane 0's gap is 0).
+// ----------------------------------------------------------------------------
+constexpr int kDeltaGroup = 64;
+
+__device__ __forceinline__ uint32_t delta_bits(uint32_t maxgap) { return maxgap ? 32u - __clz(maxgap) : 0u; }
+
+// Largest in-group gap of the sorted run keys[0..n) -> atomicMax into *maxgap
+// (zeroed by the caller).  One wave per group, groups grid-strided.
+__global__ __launch_bounds__(256) void k_delta_maxgap(const uint32_t* __restrict__ keys, uint64_t n,
+                                                      uint32_t* __restrict__ maxgap) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
+  const uint64_t wpb = blockDim.x / kWave;
+  uint32_t m = 0;
+  for (uint64_t g = (uint64_t)blockIdx.x * wpb + threadIdx.x / kWave; g < ng; g += (uint64_t)gridDim.x * wpb) {
+    const uint64_t i = g * kDeltaGroup + lane;
+    const uint32_t k = i < n ? keys[i] : 0u;
+    const uint32_t prev = __shfl_up(k, 1, kWave);
+    if (lane > 0 && i < n) m = max(m, k - prev);
+  }
+  for (int o = kWave / 2; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor(m, o, kWave));
+  if (lane == 0 && m) atomicMax(maxgap, m);
+}
+
+// Pack: w read from *maxgap on the device (so the pack can be queued before
+// the host knows it).  One wave per group; the wave assembles its 2w dwords
+// in LDS with atomicOr, then writes them out.
+__global__ __launch_bounds__(256) void k_delta_pack(const uint32_t* __restrict__ keys, uint64_t n,
+                                                    const uint32_t* __restrict__ maxgap, uint32_t* __restrict__ out) {
+  __shared__ uint32_t s_w[256 / kWave][2 * kDeltaGroup];
+  const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const uint32_t w = delta_bits(*maxgap);
+  const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
+  const uint64_t wpb = blockDim.x / kWave;
+  uint32_t* payload = out + ng;
+  for (uint64_t g = (uint64_t)blockIdx.x * wpb + wv; g < ng; g += (uint64_t)gridDim.x * wpb) {
+    const uint64_t i = g * kDeltaGroup + lane;
+    const uint32_t k = i < n ? keys[i] : 0u;
+    const uint32_t prev = __shfl_up(k, 1, kWave);
+    const uint32_t gap = (lane > 0 && i < n) ? k - prev : 0u;
+    if (lane == 0) out[g] = k;
+    if (w == 0) continue;
+    s_w[wv][lane] = 0u;
+    s_w[wv][lane + kWave] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t bit = lane * w, q = bit >> 5, r = bit & 31u;
+    atomicOr(&s_w[wv][q], gap << r);
+    if (r + w > 32u) atomicOr(&s_w[wv][q + 1], gap >> (32u - r));
+    __builtin_amdgcn_wave_barrier();
+    uint32_t* dst = payload + g * 2 * w;
+    if (lane < 2 * w) dst[lane] = s_w[wv][lane];
+    if (lane + kWave < 2 * w) dst[lane + kWave] = s_w[wv][lane + kWave];
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Unpack: gaps -> inclusive wave scan + base.
+__global__ __launch_bounds__(256) void k_delta_unpack(const uint32_t* __restrict__ in, uint64_t n, uint32_t w,
+                                                      uint32_t* __restrict__ keys) {
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
+  const uint64_t wpb = blockDim.x / kWave;
+  const uint32_t* payload = in + ng;
+  const uint32_t mask = w >= 32u ? 0xffffffffu : ((1u << w) - 1u);
+  for (uint64_t g = (uint64_t)blockIdx.x * wpb + threadIdx.x / kWave; g < ng; g += (uint64_t)gridDim.x * wpb) {
+    uint32_t gap = 0;
+    if (w) {
+      const uint32_t* src = payload + g * 2 * w;
+      const uint32_t bit = lane * w, q = bit >> 5, r = bit & 31u;
+      const uint32_t lo = src[q];
+      const uint32_t hi = (r + w > 32u) ? src[q + 1] : 0u;
+      gap = (uint32_t)((((uint64_t)hi << 32) | lo) >> r) & mask;
+    }
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const uint32_t y = __shfl_up(gap, o, kWave);
+      if ((int)lane >= o) gap += y;
+    }
+    const uint64_t i = g * kDeltaGroup + lane;
+    if (i < n) keys[i] = in[g] + gap;
+  }
+}
+
+// Merge of two sorted runs (merge path).  Block b writes outputs
+// [b*T, (b+1)*T): both split points by binary search on the diagonals, the
+// two input ranges staged in LDS, then each thread merges ITEMS outputs from
+// its own diagonal.  Ties take a first (keys only: order among equal keys is
+// invisible).
+__device__ __forceinline__ uint64_t merge_path_split(const uint32_t* a, uint64_t na, const uint32_t* b, uint64_t nb,
+                                                     uint64_t d) {
+  uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= b[d - mid - 1]) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_merge_u32(const uint32_t* __restrict__ a, uint64_t na,
+                                                   const uint32_t* __restrict__ b, uint64_t nb,
+                                                   uint32_t* __restrict__ out) {
+  constexpr int T = 256, ITEMS = 8, TILE = T * ITEMS;
+  __shared__ uint32_t s[TILE];
+  __shared__ uint64_t s_split[2];
+  const uint64_t total = na + nb;
+  const uint64_t d0 = (uint64_t)blockIdx.x * TILE;
+  const uint64_t d1 = d0 + TILE < total ? d0 + TILE : total;
+  if (threadIdx.x < 2) s_split[threadIdx.x] = merge_path_split(a, na, b, nb, threadIdx.x ? d1 : d0);
+  __syncthreads();
+  const uint64_t a0 = s_split[0], a1 = s_split[1];
+  const uint32_t la = (uint32_t)(a1 - a0), lb = (uint32_t)((d1 - d0) - la);
+  const uint64_t b0 = d0 - a0;
+  for (uint32_t i = threadIdx.x; i < la + lb; i += T) s[i] = i < la ? a[a0 + i] : b[b0 + (i - la)];
+  __syncthreads();
+  const uint32_t* sa = s;
+  const uint32_t* sb = s + la;
+  const uint32_t dd = threadIdx.x * ITEMS;
+  if (dd >= la + lb) return;
+  uint32_t lo = dd > lb ? dd - lb : 0u, hi = dd < la ? dd : la;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (sa[mid] <= sb[dd - mid - 1]) lo = mid + 1;
+    else hi = mid;
+  }
+  uint32_t ia = lo, ib = dd - lo;
+  const uint32_t m = min((uint32_t)ITEMS, la + lb - dd);
+  for (uint32_t j = 0; j < m; ++j) {
+    const bool take_a = ib >= lb || (ia < la && sa[ia] <= sb[ib]);
+    out[d0 + dd + j] = take_a ? sa[ia++] : sb[ib++];
+  }
+}
+
+// ----------------------------------------------------------------------------
 // multi-GPU round plan (pylibsort.distrib.sort_msd) on the device
 // ----------------------------------------------------------------------------
 
@@ -2244,6 +2382,42 @@ hipError_t plan_rounds(const int64_t* d_hist, uint32_t R, uint32_t ld, uint32_t 
                        int64_t* d_est, hipStream_t st) {
   if (R < 1 || R > 256 || K < 1 || R * K > 256 || ld < 4096 || !(growth > 0.0)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_plan_rounds, dim3(1), dim3(1024), 0, st, d_hist, R, ld, K, growth, d_lut, d_est);
+  return hipGetLastError();
+}
+
+hipError_t delta_maxgap_u32(const uint32_t* keys, size_t n, uint32_t* d_maxgap, hipStream_t st) {
+  LS_TRY(hipMemsetAsync(d_maxgap, 0, sizeof(uint32_t), st));
+  if (n < 2) return hipSuccess;
+  const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 3) / 4, 4096);
+  hipLaunchKernelGGL(k_delta_maxgap, dim3(blocks), dim3(256), 0, st, keys, (uint64_t)n, d_maxgap);
+  return hipGetLastError();
+}
+
+hipError_t delta_pack_u32(const uint32_t* keys, size_t n, const uint32_t* d_maxgap, uint32_t* out, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_delta_pack, dim3(blocks), dim3(256), 0, st, keys, (uint64_t)n, d_maxgap, out);
+  return hipGetLastError();
+}
+
+hipError_t delta_unpack_u32(const uint32_t* in, size_t n, uint32_t w, uint32_t* keys, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (w > 32) return hipErrorInvalidValue;
+  const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_delta_unpack, dim3(blocks), dim3(256), 0, st, in, (uint64_t)n, w, keys);
+  return hipGetLastError();
+}
+
+hipError_t merge_u32(const uint32_t* a, size_t na, const uint32_t* b, size_t nb, uint32_t* out, hipStream_t st) {
+  const uint64_t total = (uint64_t)na + nb;
+  if (total == 0) return hipSuccess;
+  const uint64_t tiles = (total + 2047) / 2048;
+  if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  ScopedTimer tm("merge", st, total);
+  hipLaunchKernelGGL(k_merge_u32, dim3((uint32_t)tiles), dim3(256), 0, st, a, (uint64_t)na, b, (uint64_t)nb, out);
   return hipGetLastError();
 }
 

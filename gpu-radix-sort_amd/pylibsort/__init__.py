@@ -75,6 +75,10 @@ _SIGS = [
      [_vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
     ("libsortPlanRounds", ctypes.c_int,
      [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, _vp, _vp, _vp]),
+    ("libsortDeltaMaxGapU32", ctypes.c_int, [_vp, ctypes.c_size_t, _vp, _vp]),
+    ("libsortDeltaPackU32", ctypes.c_int, [_vp, ctypes.c_size_t, _vp, _vp, _vp]),
+    ("libsortDeltaUnpackU32", ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_uint32, _vp, _vp]),
+    ("libsortMergeU32", ctypes.c_int, [_vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp]),
     ("libsortPopulateDevice", ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_uint64, _vp]),
     ("libsortSetDigitBits", ctypes.c_int, [ctypes.c_int]),
     ("libsortGetDigitBits", ctypes.c_int, []),

@@ -300,6 +300,67 @@ def plan_rounds(rows, nranks, rounds, growth=1.2, lut=None, est=None):
     return lut, est
 
 
+DELTA_GROUP = 64
+
+
+def delta_bits(maxgap):
+    """Bit width of the coded gaps for a run whose largest in-group gap is maxgap."""
+    return int(maxgap).bit_length()
+
+
+def delta_words(n, bits):
+    """uint32 words of a delta-coded run of n keys with gap width `bits`."""
+    return -(-int(n) // DELTA_GROUP) * (1 + 2 * int(bits))
+
+
+def delta_maxgap_u32(keys, out=None):
+    """Largest gap between neighbours inside each 64-key group of the sorted
+    run `keys`, as a one-element int32 tensor on the device."""
+    _need(keys, _U32, "keys")
+    out = torch.empty(1, dtype=torch.int32, device=keys.device) if out is None else out
+    _check(_lib().libsortDeltaMaxGapU32(_ptr(keys), keys.numel(), _ptr(out), _stream()), "libsortDeltaMaxGapU32")
+    return out
+
+
+def delta_pack_u32(keys, maxgap, out=None, capacity=None):
+    """Delta-code the sorted run `keys` with the gap width implied by the
+    device word `maxgap` (delta_maxgap_u32).  `out` must hold the coded size
+    (delta_words); without it, a buffer of `capacity` words (default: the
+    32-bit worst case) is allocated."""
+    _need(keys, _U32, "keys")
+    _need(maxgap, _U32, "maxgap")
+    if out is None:
+        out = torch.empty(capacity if capacity is not None else delta_words(keys.numel(), 32),
+                          dtype=torch.int32, device=keys.device)
+    _need(out, _U32, "out")
+    _check(_lib().libsortDeltaPackU32(_ptr(keys), keys.numel(), _ptr(maxgap), _ptr(out), _stream()),
+           "libsortDeltaPackU32")
+    return out
+
+
+def delta_unpack_u32(coded, n, bits, out=None):
+    """Decode n keys from a delta-coded run with gap width `bits`."""
+    _need(coded, _U32, "coded")
+    if coded.numel() < delta_words(n, bits):
+        raise ValueError("coded run holds %d words, %d needed" % (coded.numel(), delta_words(n, bits)))
+    out = torch.empty(n, dtype=torch.int32, device=coded.device) if out is None else out
+    _need(out, _U32, "out")
+    _check(_lib().libsortDeltaUnpackU32(_ptr(coded), int(n), int(bits), _ptr(out), _stream()), "libsortDeltaUnpackU32")
+    return out
+
+
+def merge_u32(a, b, out=None):
+    """Merge two sorted uint32 runs into `out` (distinct from both)."""
+    _need(a, _U32, "a")
+    _need(b, _U32, "b")
+    out = torch.empty(a.numel() + b.numel(), dtype=torch.int32, device=a.device) if out is None else out
+    _need(out, _U32, "out")
+    if out.numel() != a.numel() + b.numel():
+        raise ValueError("out must hold len(a) + len(b) keys")
+    _check(_lib().libsortMergeU32(_ptr(a), a.numel(), _ptr(b), b.numel(), _ptr(out), _stream()), "libsortMergeU32")
+    return out
+
+
 def populate_u32(n, first=0, device=None, out=None):
     """Elements [first, first+n) of the reference populateInput stream (fresh
     process), generated on the device."""

@@ -193,6 +193,24 @@ LIBSORT_API bool libsortPlanHistogramU32(const uint32_t* d_keys, size_t n, uint3
 LIBSORT_API bool libsortPlanRounds(const int64_t* d_rows, uint32_t nranks, uint32_t ld, uint32_t rounds,
                                    double growth, uint8_t* d_lut, int64_t* d_est, void* stream);
 
+/* Delta-coded sorted runs (the "msdz" exchange of pylibsort.distrib for
+ * link-bound world sizes).  A sorted uint32 run of n keys is coded in groups
+ * of 64: the group's first key (uint32) and its 64 gaps to the previous key in
+ * w bits, w = bit width of the largest in-group gap of the run (0 when every
+ * group holds one value).  Coded size: ceil(n/64) * (1 + 2w) uint32 words,
+ * bases first.
+ * libsortDeltaMaxGapU32 writes the largest in-group gap to *d_maxgap (device);
+ * libsortDeltaPackU32 codes the run with w taken from *d_maxgap on the device
+ * (so it can be queued before the host knows w); libsortDeltaUnpackU32
+ * decodes n keys given w (`bits`); libsortMergeU32 merges two sorted runs
+ * into d_out (distinct from both). */
+LIBSORT_API bool libsortDeltaMaxGapU32(const uint32_t* d_keys, size_t n, uint32_t* d_maxgap, void* stream);
+LIBSORT_API bool libsortDeltaPackU32(const uint32_t* d_keys, size_t n, const uint32_t* d_maxgap, uint32_t* d_out,
+                                     void* stream);
+LIBSORT_API bool libsortDeltaUnpackU32(const uint32_t* d_in, size_t n, uint32_t bits, uint32_t* d_keys, void* stream);
+LIBSORT_API bool libsortMergeU32(const uint32_t* d_a, size_t na, const uint32_t* d_b, size_t nb, uint32_t* d_out,
+                                 void* stream);
+
 /* Writes elements [first, first+n) of the populateInput stream of a fresh
  * process (state 0x4d595df4d0f33173) to device memory, by LCG skip-ahead. */
 LIBSORT_API bool libsortPopulateDevice(uint32_t* d_out, size_t n, uint64_t first, void* stream);

@@ -523,3 +523,70 @@ def test_config5_pairs_size(dev, bits):
     finally:
         pylibsort.setDigitBits(prev)
         torch.cuda.empty_cache()
+
+
+def _delta_pack_ref(x):
+    """numpy/Python restatement of the delta-coded run format (libsort.h):
+    per 64-key group the first key, then 64 gaps of w bits packed little-endian
+    at bit lane * w (lane 0's gap is 0)."""
+    n = x.size
+    ng = -(-n // 64)
+    gaps = [0]
+    for g in range(ng):
+        seg = x[g * 64:(g + 1) * 64].astype(np.int64)
+        gaps.append(int(np.diff(seg).max()) if seg.size > 1 else 0)
+    w = max(gaps).bit_length()
+    words = [int(x[g * 64]) for g in range(ng)]
+    for g in range(ng):
+        seg = x[g * 64:(g + 1) * 64].astype(np.int64)
+        d = np.concatenate([[0], np.diff(seg)]) if seg.size else np.zeros(0, np.int64)
+        acc = 0
+        for lane, v in enumerate(d):
+            acc |= int(v) << (lane * w)
+        words += [(acc >> (32 * q)) & 0xFFFFFFFF for q in range(2 * w)]
+    return max(gaps), w, np.array(words, dtype=np.uint32)
+
+
+@pytest.mark.parametrize("kind,n", [("uniform", 1), ("uniform", 63), ("uniform", 64), ("uniform", 65),
+                                    ("uniform", 100003), ("equal", 5000), ("wide", 4097), ("clustered", 70001),
+                                    ("dups", 20000)])
+def test_delta_code_roundtrip(dev, kind, n):
+    """Delta-coded runs (the msdz exchange): the largest gap, the coded words
+    (pinned to a Python restatement of the format) and the decode round trip."""
+    import pylibsort.device as D
+    rng = np.random.default_rng(n)
+    if kind == "uniform":
+        x = np.sort(rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32))
+    elif kind == "equal":
+        x = np.full(n, 0xDEADBEEF, dtype=np.uint32)
+    elif kind == "wide":
+        x = np.sort(np.concatenate([[0, 0xFFFFFFFF], rng.integers(0, 1 << 32, n - 2, dtype=np.uint64)])
+                    .astype(np.uint32))
+    elif kind == "clustered":
+        x = np.sort((rng.integers(0, 8, n, dtype=np.uint64) << np.uint64(29)
+                     | rng.integers(0, 1000, n, dtype=np.uint64)).astype(np.uint32))
+    else:
+        x = np.sort(rng.integers(0, 300, n, dtype=np.uint64).astype(np.uint32))
+    t = torch.from_numpy(x.view(np.int32)).cuda()
+    mg = D.delta_maxgap_u32(t)
+    maxgap, w, ref = _delta_pack_ref(x)
+    assert int(mg.item()) & 0xFFFFFFFF == maxgap
+    assert D.delta_bits(maxgap) == w and D.delta_words(n, w) == ref.size
+    coded = D.delta_pack_u32(t, mg, out=torch.empty(ref.size, dtype=torch.int32, device="cuda"))
+    np.testing.assert_array_equal(coded.cpu().numpy().view(np.uint32), ref)
+    back = D.delta_unpack_u32(coded, n, w)
+    np.testing.assert_array_equal(back.cpu().numpy().view(np.uint32), x)
+
+
+@pytest.mark.parametrize("na,nb", [(0, 0), (0, 5), (7, 0), (1, 1), (2048, 2048), (100003, 77777), (5, 300000),
+                                   (1 << 20, (1 << 20) + 13)])
+def test_merge_u32(dev, na, nb):
+    import pylibsort.device as D
+    rng = np.random.default_rng(na * 7 + nb)
+    hi = 1000 if na == 2048 else 1 << 32                      # ties across the runs
+    a = np.sort(rng.integers(0, hi, na, dtype=np.uint64).astype(np.uint32))
+    b = np.sort(rng.integers(0, hi, nb, dtype=np.uint64).astype(np.uint32))
+    ta = torch.from_numpy(a.view(np.int32)).cuda()
+    tb = torch.from_numpy(b.view(np.int32)).cuda()
+    out = D.merge_u32(ta, tb)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), np.sort(np.concatenate([a, b])))
