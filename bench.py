@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"])
     ap.add_argument("--keys-log2", type=int, default=None, help="keys (pairs) per GPU = 2^k")
     ap.add_argument("--digit-bits", type=int, default=None, help="configs[1] names 4-bit digits")
-    ap.add_argument("--schedule", default="msd", choices=["msd", "lsd"])
+    ap.add_argument("--schedule", default="auto", choices=["auto", "msd", "msdz", "lsd"],
+                    help="auto: msdz (delta-coded exchange) at 2 GPUs, msd otherwise")
     ap.add_argument("--rounds", type=int, default=4, help="msd exchange rounds (pylibsort.distrib.ROUNDS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=26)
@@ -117,9 +118,9 @@ def main():
             return distrib.distrib_sort_pairs(keys, vals, ops=ops, rounds=args.rounds)
         if world == 1:
             return D.sort_keys_u32(keys, out=out, tmp=tmp)
-        if args.schedule == "msd":
-            return distrib.distrib_sort(keys, ops=ops, schedule="msd", rounds=args.rounds)
-        return distrib.distrib_sort(keys, ops=ops, schedule=args.schedule)
+        if args.schedule == "lsd":
+            return distrib.distrib_sort(keys, ops=ops, schedule="lsd")
+        return distrib.distrib_sort(keys, ops=ops, schedule=args.schedule, rounds=args.rounds)
 
     def barrier():
         if world > 1:
@@ -245,8 +246,14 @@ def main():
             host_abi = host_abi_leg(torch, pylibsort, keys, out)
         sched = ""
         if world > 1:
-            sched = (", msd schedule, %d rounds, over %d GPUs (RCCL alltoallv)" % (args.rounds, world)
-                     if pairs or args.schedule == "msd" else ", lsd schedule over %d GPUs (RCCL alltoallv)" % world)
+            sname = args.schedule
+            if sname == "auto":
+                sname = "msdz" if world == 2 else "msd"
+            if pairs:
+                sname = "msd"
+            sched = (", %s schedule%s, %d rounds, over %d GPUs (RCCL point-to-point)"
+                     % (sname, " (delta-coded exchange)" if sname == "msdz" else "", args.rounds, world)
+                     if sname != "lsd" else ", lsd schedule over %d GPUs (RCCL alltoallv)" % world)
         if pairs:
             metric, unit, dtype = "Gpairs/sec (u64 key, u32 payload) stable sort", "Gpairs/s", "u64+u32"
             workload = "configs[4]: 2^%d (u64 key, u32 payload) pairs per GPU, %d-bit digits, stable sort%s" % (

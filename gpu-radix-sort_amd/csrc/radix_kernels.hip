@@ -1311,80 +1311,124 @@ constexpr int kDeltaGroup = 64;
 
 __device__ __forceinline__ uint32_t delta_bits(uint32_t maxgap) { return maxgap ? 32u - __clz(maxgap) : 0u; }
 
+// Each wave takes kDeltaUnroll groups per step (group g = lane-contiguous 64
+// keys, one coalesced load each), all loads issued before any use.
+constexpr int kDeltaUnroll = 4;
+
 // Largest in-group gap of the sorted run keys[0..n) -> atomicMax into *maxgap
-// (zeroed by the caller).  One wave per group, groups grid-strided.
+// (zeroed by the caller).
 __global__ __launch_bounds__(256) void k_delta_maxgap(const uint32_t* __restrict__ keys, uint64_t n,
                                                       uint32_t* __restrict__ maxgap) {
+  constexpr int U = kDeltaUnroll;
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
   const uint64_t wpb = blockDim.x / kWave;
   uint32_t m = 0;
-  for (uint64_t g = (uint64_t)blockIdx.x * wpb + threadIdx.x / kWave; g < ng; g += (uint64_t)gridDim.x * wpb) {
-    const uint64_t i = g * kDeltaGroup + lane;
-    const uint32_t k = i < n ? keys[i] : 0u;
-    const uint32_t prev = __shfl_up(k, 1, kWave);
-    if (lane > 0 && i < n) m = max(m, k - prev);
+  for (uint64_t g0 = ((uint64_t)blockIdx.x * wpb + threadIdx.x / kWave) * U; g0 < ng;
+       g0 += (uint64_t)gridDim.x * wpb * U) {
+    uint32_t k[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = (g0 + u) * kDeltaGroup + lane;
+      k[u] = i < n ? keys[i] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t prev = __shfl_up(k[u], 1, kWave);
+      const uint64_t i = (g0 + u) * kDeltaGroup + lane;
+      if (lane > 0 && i < n) m = max(m, k[u] - prev);
+    }
   }
+  // one atomic per block: same-address atomics from every wave serialise
+  // (16K of them took ~0.8 ms at 2^27 keys)
+  __shared__ uint32_t s_m[256 / kWave];
   for (int o = kWave / 2; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor(m, o, kWave));
-  if (lane == 0 && m) atomicMax(maxgap, m);
+  if (lane == 0) s_m[threadIdx.x / kWave] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t i = 1; i < blockDim.x / kWave; ++i) m = max(m, s_m[i]);
+    if (m) atomicMax(maxgap, m);
+  }
 }
 
 // Pack: w read from *maxgap on the device (so the pack can be queued before
-// the host knows it).  One wave per group; the wave assembles its 2w dwords
-// in LDS with atomicOr, then writes them out.
+// the host knows it).  Each wave assembles a group's 2w dwords in LDS with
+// atomicOr, then writes them out.
 __global__ __launch_bounds__(256) void k_delta_pack(const uint32_t* __restrict__ keys, uint64_t n,
                                                     const uint32_t* __restrict__ maxgap, uint32_t* __restrict__ out) {
-  __shared__ uint32_t s_w[256 / kWave][2 * kDeltaGroup];
+  constexpr int U = kDeltaUnroll;
+  __shared__ uint32_t s_w[256 / kWave][U][2 * kDeltaGroup];
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const uint32_t w = delta_bits(*maxgap);
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
   const uint64_t wpb = blockDim.x / kWave;
   uint32_t* payload = out + ng;
-  for (uint64_t g = (uint64_t)blockIdx.x * wpb + wv; g < ng; g += (uint64_t)gridDim.x * wpb) {
-    const uint64_t i = g * kDeltaGroup + lane;
-    const uint32_t k = i < n ? keys[i] : 0u;
-    const uint32_t prev = __shfl_up(k, 1, kWave);
-    const uint32_t gap = (lane > 0 && i < n) ? k - prev : 0u;
-    if (lane == 0) out[g] = k;
-    if (w == 0) continue;
-    s_w[wv][lane] = 0u;
-    s_w[wv][lane + kWave] = 0u;
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t bit = lane * w, q = bit >> 5, r = bit & 31u;
-    atomicOr(&s_w[wv][q], gap << r);
-    if (r + w > 32u) atomicOr(&s_w[wv][q + 1], gap >> (32u - r));
-    __builtin_amdgcn_wave_barrier();
-    uint32_t* dst = payload + g * 2 * w;
-    if (lane < 2 * w) dst[lane] = s_w[wv][lane];
-    if (lane + kWave < 2 * w) dst[lane + kWave] = s_w[wv][lane + kWave];
-    __builtin_amdgcn_wave_barrier();
+  for (uint64_t g0 = ((uint64_t)blockIdx.x * wpb + wv) * U; g0 < ng; g0 += (uint64_t)gridDim.x * wpb * U) {
+    uint32_t k[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t i = (g0 + u) * kDeltaGroup + lane;
+      k[u] = i < n ? keys[i] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t g = g0 + u;
+      if (g >= ng) break;
+      if (lane == 0) out[g] = k[u];
+      if (w == 0) continue;
+      const uint64_t i = g * kDeltaGroup + lane;
+      const uint32_t prev = __shfl_up(k[u], 1, kWave);
+      const uint32_t gap = (lane > 0 && i < n) ? k[u] - prev : 0u;
+      uint32_t* sw = s_w[wv][u];
+      sw[lane] = 0u;
+      sw[lane + kWave] = 0u;
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t bit = lane * w, q = bit >> 5, r = bit & 31u;
+      atomicOr(&sw[q], gap << r);
+      if (r + w > 32u) atomicOr(&sw[q + 1], gap >> (32u - r));
+      __builtin_amdgcn_wave_barrier();
+      uint32_t* dst = payload + g * 2 * w;
+      if (lane < 2 * w) dst[lane] = sw[lane];
+      if (lane + kWave < 2 * w) dst[lane + kWave] = sw[lane + kWave];
+    }
   }
 }
 
 // Unpack: gaps -> inclusive wave scan + base.
 __global__ __launch_bounds__(256) void k_delta_unpack(const uint32_t* __restrict__ in, uint64_t n, uint32_t w,
                                                       uint32_t* __restrict__ keys) {
+  constexpr int U = kDeltaUnroll;
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
   const uint64_t wpb = blockDim.x / kWave;
   const uint32_t* payload = in + ng;
   const uint32_t mask = w >= 32u ? 0xffffffffu : ((1u << w) - 1u);
-  for (uint64_t g = (uint64_t)blockIdx.x * wpb + threadIdx.x / kWave; g < ng; g += (uint64_t)gridDim.x * wpb) {
-    uint32_t gap = 0;
-    if (w) {
-      const uint32_t* src = payload + g * 2 * w;
-      const uint32_t bit = lane * w, q = bit >> 5, r = bit & 31u;
-      const uint32_t lo = src[q];
-      const uint32_t hi = (r + w > 32u) ? src[q + 1] : 0u;
-      gap = (uint32_t)((((uint64_t)hi << 32) | lo) >> r) & mask;
+  const uint32_t bit = lane * w, q = bit >> 5, r = bit & 31u;
+  for (uint64_t g0 = ((uint64_t)blockIdx.x * wpb + threadIdx.x / kWave) * U; g0 < ng;
+       g0 += (uint64_t)gridDim.x * wpb * U) {
+    uint32_t lo[U], hi[U], base[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint64_t g = g0 + u;
+      lo[u] = hi[u] = 0u;
+      base[u] = g < ng ? in[g] : 0u;
+      if (w && g < ng) {
+        const uint32_t* src = payload + g * 2 * w;
+        lo[u] = src[q];
+        if (r + w > 32u) hi[u] = src[q + 1];
+      }
     }
 #pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const uint32_t y = __shfl_up(gap, o, kWave);
-      if ((int)lane >= o) gap += y;
+    for (int u = 0; u < U; ++u) {
+      uint32_t gap = w ? (uint32_t)((((uint64_t)hi[u] << 32) | lo[u]) >> r) & mask : 0u;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const uint32_t y = __shfl_up(gap, o, kWave);
+        if ((int)lane >= o) gap += y;
+      }
+      const uint64_t i = (g0 + u) * kDeltaGroup + lane;
+      if (i < n) keys[i] = base[u] + gap;
     }
-    const uint64_t i = g * kDeltaGroup + lane;
-    if (i < n) keys[i] = in[g] + gap;
   }
 }
 
@@ -1404,38 +1448,60 @@ __device__ __forceinline__ uint64_t merge_path_split(const uint32_t* a, uint64_t
   return lo;
 }
 
+// Split points of every merge tile: splits[t] = elements of a among the
+// first t * tile outputs (t = 0..tiles), one thread each.
+__global__ __launch_bounds__(256) void k_merge_splits(const uint32_t* __restrict__ a, uint64_t na,
+                                                      const uint32_t* __restrict__ b, uint64_t nb, uint32_t tile,
+                                                      uint64_t tiles, uint64_t* __restrict__ splits) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t > tiles) return;
+  const uint64_t d = t * tile < na + nb ? t * tile : na + nb;
+  splits[t] = merge_path_split(a, na, b, nb, d);
+}
+
 __global__ __launch_bounds__(256) void k_merge_u32(const uint32_t* __restrict__ a, uint64_t na,
                                                    const uint32_t* __restrict__ b, uint64_t nb,
-                                                   uint32_t* __restrict__ out) {
+                                                   const uint64_t* __restrict__ splits, uint32_t* __restrict__ out) {
   constexpr int T = 256, ITEMS = 8, TILE = T * ITEMS;
   __shared__ uint32_t s[TILE];
-  __shared__ uint64_t s_split[2];
   const uint64_t total = na + nb;
   const uint64_t d0 = (uint64_t)blockIdx.x * TILE;
   const uint64_t d1 = d0 + TILE < total ? d0 + TILE : total;
-  if (threadIdx.x < 2) s_split[threadIdx.x] = merge_path_split(a, na, b, nb, threadIdx.x ? d1 : d0);
-  __syncthreads();
-  const uint64_t a0 = s_split[0], a1 = s_split[1];
+  const uint64_t a0 = splits[blockIdx.x], a1 = splits[blockIdx.x + 1];
   const uint32_t la = (uint32_t)(a1 - a0), lb = (uint32_t)((d1 - d0) - la);
   const uint64_t b0 = d0 - a0;
   for (uint32_t i = threadIdx.x; i < la + lb; i += T) s[i] = i < la ? a[a0 + i] : b[b0 + (i - la)];
   __syncthreads();
   const uint32_t* sa = s;
   const uint32_t* sb = s + la;
+  const uint32_t len = la + lb;
   const uint32_t dd = threadIdx.x * ITEMS;
-  if (dd >= la + lb) return;
-  uint32_t lo = dd > lb ? dd - lb : 0u, hi = dd < la ? dd : la;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (sa[mid] <= sb[dd - mid - 1]) lo = mid + 1;
-    else hi = mid;
+  uint32_t v[ITEMS];
+  uint32_t m = 0;
+  if (dd < len) {
+    uint32_t lo = dd > lb ? dd - lb : 0u, hi = dd < la ? dd : la;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (sa[mid] <= sb[dd - mid - 1]) lo = mid + 1;
+      else hi = mid;
+    }
+    uint32_t ia = lo, ib = dd - lo;
+    m = min((uint32_t)ITEMS, len - dd);
+#pragma unroll
+    for (uint32_t j = 0; j < (uint32_t)ITEMS; ++j) {
+      if (j < m) {
+        const bool take_a = ib >= lb || (ia < la && sa[ia] <= sb[ib]);
+        v[j] = take_a ? sa[ia++] : sb[ib++];
+      }
+    }
   }
-  uint32_t ia = lo, ib = dd - lo;
-  const uint32_t m = min((uint32_t)ITEMS, la + lb - dd);
-  for (uint32_t j = 0; j < m; ++j) {
-    const bool take_a = ib >= lb || (ia < la && sa[ia] <= sb[ib]);
-    out[d0 + dd + j] = take_a ? sa[ia++] : sb[ib++];
-  }
+  // through LDS again, so the global stores are lane-contiguous
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < (uint32_t)ITEMS; ++j)
+    if (j < m) s[dd + j] = v[j];
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < len; i += T) out[d0 + i] = s[i];
 }
 
 // ----------------------------------------------------------------------------
@@ -2389,7 +2455,7 @@ hipError_t delta_maxgap_u32(const uint32_t* keys, size_t n, uint32_t* d_maxgap, 
   LS_TRY(hipMemsetAsync(d_maxgap, 0, sizeof(uint32_t), st));
   if (n < 2) return hipSuccess;
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 3) / 4, 4096);
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 15) / 16, 1024);
   hipLaunchKernelGGL(k_delta_maxgap, dim3(blocks), dim3(256), 0, st, keys, (uint64_t)n, d_maxgap);
   return hipGetLastError();
 }
@@ -2397,7 +2463,7 @@ hipError_t delta_maxgap_u32(const uint32_t* keys, size_t n, uint32_t* d_maxgap, 
 hipError_t delta_pack_u32(const uint32_t* keys, size_t n, const uint32_t* d_maxgap, uint32_t* out, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 3) / 4, 8192);
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 15) / 16, 8192);
   hipLaunchKernelGGL(k_delta_pack, dim3(blocks), dim3(256), 0, st, keys, (uint64_t)n, d_maxgap, out);
   return hipGetLastError();
 }
@@ -2406,7 +2472,7 @@ hipError_t delta_unpack_u32(const uint32_t* in, size_t n, uint32_t w, uint32_t* 
   if (n == 0) return hipSuccess;
   if (w > 32) return hipErrorInvalidValue;
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 3) / 4, 8192);
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 15) / 16, 8192);
   hipLaunchKernelGGL(k_delta_unpack, dim3(blocks), dim3(256), 0, st, in, (uint64_t)n, w, keys);
   return hipGetLastError();
 }
@@ -2416,9 +2482,21 @@ hipError_t merge_u32(const uint32_t* a, size_t na, const uint32_t* b, size_t nb,
   if (total == 0) return hipSuccess;
   const uint64_t tiles = (total + 2047) / 2048;
   if (tiles > 0x7fffffffull) return hipErrorInvalidValue;
+  // split points in stream-ordered memory: no workspace, so merges on one
+  // stream never wait for sorts on another
+  uint64_t* splits = nullptr;
+  LS_TRY(hipMallocAsync(reinterpret_cast<void**>(&splits), (tiles + 1) * sizeof(uint64_t), st));
   ScopedTimer tm("merge", st, total);
-  hipLaunchKernelGGL(k_merge_u32, dim3((uint32_t)tiles), dim3(256), 0, st, a, (uint64_t)na, b, (uint64_t)nb, out);
-  return hipGetLastError();
+  hipLaunchKernelGGL(k_merge_splits, dim3((uint32_t)((tiles + 1 + 255) / 256)), dim3(256), 0, st, a, (uint64_t)na, b,
+                     (uint64_t)nb, 2048u, tiles, splits);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_merge_u32, dim3((uint32_t)tiles), dim3(256), 0, st, a, (uint64_t)na, b, (uint64_t)nb,
+                       (const uint64_t*)splits, out);
+    e = hipGetLastError();
+  }
+  const hipError_t f = hipFreeAsync(splits, st);
+  return e != hipSuccess ? e : f;
 }
 
 hipError_t populate_device(uint32_t* out, size_t n, uint64_t first, hipStream_t st) {

@@ -31,6 +31,8 @@ The local operations come from an `ops` backend.  The product backend is
 HipOps (libsort's HIP kernels on torch CUDA tensors).  The CPU tests pass an
 oracle backend explicitly; nothing here falls back to the CPU on its own.
 """
+import contextlib
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -44,6 +46,9 @@ HIST_BITS = 12
 # exchange takes 2.35 ms or more and lose <= 0.15 ms when it is faster.
 ROUNDS = 4
 GROWTH = 1.2
+# msdz (delta-coded exchange) sorts before it sends, so its exposed exchange
+# is the LAST round's: rounds shrink (x0.6: 46 / 28 / 17 / 10% of the keys)
+GROWTH_Z = 0.6
 
 
 class HipOps:
@@ -154,6 +159,18 @@ class HipOps:
                                                       out_keys=self.empty64(n), out_vals=self.empty(n))
         return k, v, b.to(torch.int64) & 0xFFFFFFFF
 
+    def delta_maxgap(self, keys, out):
+        return self.D.delta_maxgap_u32(keys, out=out)
+
+    def delta_pack(self, keys, maxgap, out):
+        return self.D.delta_pack_u32(keys, maxgap, out=out)
+
+    def delta_unpack(self, coded, n, bits, out):
+        return self.D.delta_unpack_u32(coded, n, bits, out=out)
+
+    def merge(self, a, b, out):
+        return self.D.merge_u32(a, b, out=out)
+
     def plan_row(self, keys, stride, block=4096):
         """int64[4097] on the device: sampled top-12-bit histogram + n (one
         libsort call instead of sample copy + histogram + cat)."""
@@ -235,11 +252,11 @@ class _SideWork:
     this object's creation, so the scatter can be queued (and start) first;
     `uses` are the current-stream tensors it reads."""
 
-    def __init__(self, *uses):
+    def __init__(self, *uses, event=None):
         self.uses = uses
         self.ctx = None
-        self.ev = None
-        if uses[0].is_cuda:
+        self.ev = event
+        if uses[0].is_cuda and event is None:
             self.ev = torch.cuda.Event()
             self.ev.record()
 
@@ -440,12 +457,12 @@ def _plan_row(ops, keys, stride):
     return torch.cat([h.to(torch.int64), torch.tensor([keys.numel()], dtype=torch.int64, device=h.device)])
 
 
-def _plan(ops, HN, R, K):
+def _plan(ops, HN, R, K, growth=None):
     """(lut, est) of the round plan from the gathered rows (device kernel on
     HipOps, the torch restatement otherwise)."""
     if hasattr(ops, "plan"):
-        return ops.plan(HN, R, K)
-    return _plan_rounds_t(HN[:, :-1], R, K)
+        return ops.plan(HN, R, K, growth)
+    return _plan_rounds_t(HN[:, :-1], R, K, growth)
 
 
 def _sizes_from_starts(b_t, n):
@@ -508,20 +525,15 @@ def _mark(trace, label):
         trace.append((label, time.perf_counter()))
 
 
-def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None, sample_stride=16, self_local=True,
-             trace=None):
-    """Range-split rounds schedule; see module docstring.  `trace` (a list)
-    records synchronised timestamps of the steps (diagnostics only)."""
-    R = dist.get_world_size(group)
-    r = dist.get_rank(group)
-    _mark(trace, "start")
-    K = max(1, min(int(ROUNDS if rounds is None else rounds), 256 // R))
+def _msd_partition(keys, ops, group, R, K, sample_stride, trace=None, growth=None):
+    """The prefix of the range-round schedules: sampled histogram, all-gather,
+    round plan, table partition into R*K (round, destination) buckets, and the
+    exact bucket sizes of every rank on the host.  Returns (part, C[R, R*K],
+    n_all[R], est[R], lut[4096])."""
     n = keys.numel()
     NB = R * K
-    # histogram -> allgather -> plan -> partition -> allgather of the exact
-    # sizes, all on the device; ONE host transfer afterwards
     HN = _allgather_t(_plan_row(ops, keys, sample_stride), group)     # [R, 4097]: histogram | n
-    lut_t, est_t = _plan(ops, HN, R, K)
+    lut_t, est_t = _plan(ops, HN, R, K, growth)
     _mark(trace, "histogram+allgather+plan")
     split = hasattr(ops, "partition_lut_count_t")
     if split:
@@ -546,6 +558,22 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None
     n_all = host[R * NB:R * NB + R]
     est = host[R * NB + R:R * NB + 2 * R]
     lut = host[R * NB + 2 * R:].astype(np.uint8)
+    return part, C, n_all, est, lut
+
+
+def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None, sample_stride=16, self_local=True,
+             trace=None):
+    """Range-split rounds schedule; see module docstring.  `trace` (a list)
+    records synchronised timestamps of the steps (diagnostics only)."""
+    R = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    _mark(trace, "start")
+    K = max(1, min(int(ROUNDS if rounds is None else rounds), 256 // R))
+    n = keys.numel()
+    NB = R * K
+    # histogram -> allgather -> plan -> partition -> allgather of the exact
+    # sizes, all on the device; ONE host transfer afterwards
+    part, C, n_all, est, lut = _msd_partition(keys, ops, group, R, K, sample_stride, trace)
     N = int(n_all.sum())
     S, _ = shard_cut(N, R)
     hs = float(est.sum())
@@ -573,6 +601,166 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None
             lo, hi = _group_range(lut, i * R + r)              # every key of the round lies in it
             ops.sort_range(recv[int(roff[i]):int(roff[i + 1])], lo, hi, out=out[int(roff[i]):int(roff[i + 1])])
         _mark(trace, "round %d" % i)
+    if not balance:
+        return out
+    n_recv = np.array([int(C[:, d::R].sum()) for d in range(R)], dtype=np.int64)
+    res = _rebalance(out, n_recv, ops, group)
+    _mark(trace, "rebalance")
+    return res
+
+
+def _delta_words(n, bits):
+    """uint32 words of a delta-coded run (libsort.h: 64-key groups, base + 2w words)."""
+    return -(-int(n) // 64) * (1 + 2 * int(bits))
+
+
+def _exchange_pieces(sends, recvs, group):
+    """Point-to-point exchange of whole tensors: sends {dest: tensor},
+    recvs {src: tensor} (exact sizes known on both sides), one batch; returns
+    a handle whose wait() orders the caller after it, or None when nothing is
+    left in flight (device tensors over gloo are staged through host memory
+    synchronously, as in _alltoallv_into)."""
+    R = dist.get_world_size(group)
+    me = dist.get_rank(group)
+    peer = (lambda i: i) if group is None else (lambda i: dist.get_global_rank(group, i))
+    staged = _host_staged(group) and any(t.is_cuda for t in list(sends.values()) + list(recvs.values()))
+    hs = {d: (t.cpu() if staged else t) for d, t in sends.items()}
+    hr = {j: (torch.empty(t.numel(), dtype=t.dtype) if staged else t) for j, t in recvs.items()}
+    ops_ = []
+    for k in range(1, R):
+        i, j = (me + k) % R, (me - k) % R
+        if i in hs:
+            ops_.append(dist.P2POp(dist.isend, hs[i], peer(i), group))
+        if j in hr:
+            ops_.append(dist.P2POp(dist.irecv, hr[j], peer(j), group))
+    if not ops_:
+        return None
+    works = _Works(dist.batch_isend_irecv(ops_))
+    if staged:
+        works.wait()
+        for j, t in recvs.items():
+            t.copy_(hr[j])
+        return None
+    return works
+
+
+def _merge_runs(runs, ops, out):
+    """Merge sorted runs into `out` (pairwise, in levels)."""
+    runs = [t for t in runs if t.numel()]
+    if not runs:
+        return out
+    if len(runs) == 1:
+        out.copy_(runs[0])
+        return out
+    while len(runs) > 2:
+        nxt = [ops.merge(runs[j], runs[j + 1], ops.empty(runs[j].numel() + runs[j + 1].numel()))
+               for j in range(0, len(runs) - 1, 2)]
+        if len(runs) % 2:
+            nxt.append(runs[-1])
+        runs = nxt
+    return ops.merge(runs[0], runs[1], out)
+
+
+def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None, sample_stride=16, trace=None):
+    """Range rounds with delta-coded exchange, for link-bound world sizes (the
+    bench default at 2 GPUs, where one xGMI link carries half of every shard).
+    The same plan and table partition as sort_msd; then per round the SENDER
+    sorts the round's slice (one range sort covers every destination's piece:
+    the pieces are disjoint key ranges in destination order), codes each
+    outgoing piece as gaps (libsortDeltaPackU32; uniform keys: ~9 bits instead
+    of 32), the gap widths are all-gathered (exact receive sizes), the coded
+    pieces travel point to point, and the receiver decodes them and merges
+    them with its own sorted piece into its slice of the output.  Sorts are
+    queued for every round up front on the current stream; each round's
+    exchange runs on a communication stream after that round's coding, and
+    decode + merge on a third stream, so sorting, exchange and merging of
+    different rounds overlap.  Same result as sort_msd (a full sort is
+    unique); the skew fallback is the same."""
+    R = dist.get_world_size(group)
+    r = dist.get_rank(group)
+    _mark(trace, "start")
+    K = max(1, min(int(ROUNDS if rounds is None else rounds), 256 // R))
+    n = keys.numel()
+    part, C, n_all, est, lut = _msd_partition(keys, ops, group, R, K, sample_stride, trace, GROWTH_Z)
+    N = int(n_all.sum())
+    S, _ = shard_cut(N, R)
+    hs = float(est.sum())
+    if N and hs and est.max() * N / hs > max_imbalance * S + 4096:
+        return sort_lsd(keys, ops, group)                      # identical decision on every rank
+    sizes = C[r]
+    b = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    recv_tot = np.array([int(C[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
+    roff = np.concatenate([[0], np.cumsum(recv_tot)])
+    out = ops.empty(int(roff[-1]))
+    srt = ops.empty(n)
+    cuda = keys.is_cuda
+    mg = torch.zeros(R * K, dtype=torch.int32, device=keys.device)
+    # worst-case (32-bit gaps) regions for the coded outgoing pieces
+    cap = np.array([_delta_words(sizes[j], 32) if j % R != r else 0 for j in range(R * K)], dtype=np.int64)
+    coff = np.concatenate([[0], np.cumsum(cap)])
+    coded = ops.empty(int(coff[-1]))
+    evs = []
+    for i in range(K):
+        s0, s1 = int(b[i * R]), int(b[i * R]) + int(sizes[i * R:(i + 1) * R].sum())
+        if s1 > s0:
+            bk = np.nonzero((lut >= i * R) & (lut < (i + 1) * R))[0]
+            lo, hi = int(bk[0]) << (32 - HIST_BITS), (int(bk[-1]) + 1) << (32 - HIST_BITS)
+            ops.sort_range(part[s0:s1], lo, hi, out=srt[s0:s1])
+        for d in range(R):
+            j = i * R + d
+            if d != r and sizes[j]:
+                piece = srt[int(b[j]):int(b[j]) + int(sizes[j])]
+                ops.delta_maxgap(piece, out=mg[j:j + 1])
+                ops.delta_pack(piece, mg[j:j + 1], out=coded[int(coff[j]):int(coff[j + 1])])
+        ev = None
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+        evs.append(ev)
+    _mark(trace, "rounds sorted and coded")
+    comm = torch.cuda.Stream(device=keys.device) if cuda else None
+    mstream = torch.cuda.Stream(device=keys.device) if cuda else None
+    keep = []
+    for i in range(K):
+        # the gap widths of round i are gathered only now, after round i-1's
+        # exchange was posted: RCCL runs one group's operations in issue order,
+        # so gathering every round up front would hold the first exchange
+        # until the last round was coded
+        with _SideWork(mg, event=evs[i]):
+            pend = _to_host_async(_allgather_t(mg[i * R:(i + 1) * R].to(torch.int64) & 0xFFFFFFFF, group))
+        G = pend.wait()                                        # [R, R]: largest gap of rank s's piece for d
+        sends, recvs = {}, {}
+        for d in range(R):
+            j = i * R + d
+            if d != r and sizes[j]:
+                w = int(G[r][d]).bit_length()
+                sends[d] = coded[int(coff[j]):int(coff[j]) + _delta_words(sizes[j], w)]
+        for src in range(R):
+            m = int(C[src][i * R + r])
+            if src != r and m:
+                recvs[src] = ops.empty(_delta_words(m, int(G[src][r]).bit_length()))
+        with (torch.cuda.stream(comm) if cuda else contextlib.nullcontext()):
+            if cuda:
+                comm.wait_event(evs[i])
+            works = _exchange_pieces(sends, recvs, group)
+        with (torch.cuda.stream(mstream) if cuda else contextlib.nullcontext()):
+            if cuda:
+                mstream.wait_event(evs[i])
+                mstream.wait_stream(comm)                      # host-staged receives land on comm
+            if works is not None:
+                works.wait()
+            j = i * R + r
+            runs = [srt[int(b[j]):int(b[j]) + int(sizes[j])]]
+            for src, coded_in in recvs.items():
+                m = int(C[src][i * R + r])
+                runs.append(ops.delta_unpack(coded_in, m, int(G[src][r]).bit_length(), ops.empty(m)))
+            if recv_tot[i]:
+                _merge_runs(runs, ops, out[int(roff[i]):int(roff[i + 1])])
+            keep.append((sends, recvs, runs))
+    if cuda:
+        torch.cuda.current_stream().wait_stream(mstream)
+        torch.cuda.current_stream().wait_stream(comm)
+    _mark(trace, "exchanged and merged")
     if not balance:
         return out
     n_recv = np.array([int(C[:, d::R].sum()) for d in range(R)], dtype=np.int64)
@@ -673,12 +861,16 @@ def distrib_sort(keys, ops=None, group=None, schedule="msd", **kw):
     ops = HipOps() if ops is None else ops
     if dist.get_world_size(group) == 1:
         return ops.sort(keys)
+    if schedule == "auto":                                     # delta-coded exchange where one link carries it
+        schedule = "msdz" if dist.get_world_size(group) == 2 else "msd"
     if schedule == "msd":
         return sort_msd(keys, ops, group, **kw)
+    if schedule == "msdz":
+        return sort_msdz(keys, ops, group, **kw)
     if schedule == "lsd":
         return sort_lsd(keys, ops, group, **kw)
-    raise ValueError("schedule must be 'msd' or 'lsd'")
+    raise ValueError("schedule must be 'auto', 'msd', 'msdz' or 'lsd'")
 
 
-__all__ = ["HipOps", "distrib_sort", "distrib_sort_pairs", "sort_lsd", "sort_msd", "plan_msd", "plan_rounds",
+__all__ = ["HipOps", "distrib_sort", "distrib_sort_pairs", "sort_lsd", "sort_msd", "sort_msdz", "plan_msd", "plan_rounds",
            "shard_cut"]

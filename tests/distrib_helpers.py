@@ -101,6 +101,57 @@ class OracleOps:
             return keys
         return keys[:nb * block].view(nb, block)[::stride].contiguous().view(-1)
 
+    @staticmethod
+    def _groups(x):
+        ng = -(-x.size // 64)
+        pad = np.zeros(ng * 64, dtype=np.int64)
+        pad[:x.size] = x
+        g = pad.reshape(ng, 64)
+        gaps = np.zeros_like(g)
+        gaps[:, 1:] = g[:, 1:] - g[:, :-1]
+        valid = (np.arange(ng * 64) < x.size).reshape(ng, 64)
+        gaps[~valid] = 0
+        return g, gaps
+
+    def delta_maxgap(self, keys, out):
+        x = self._np(keys)
+        m = int(self._groups(x)[1].max()) if x.size > 1 else 0
+        out.numpy().view(np.uint32)[0] = m
+        return out
+
+    def delta_pack(self, keys, maxgap, out):
+        x = self._np(keys)
+        w = int(maxgap.numpy().view(np.uint32)[0]).bit_length()
+        g, gaps = self._groups(x)
+        words = list(g[:, 0].astype(np.uint32))
+        for row in gaps:
+            acc = 0
+            for lane, v in enumerate(row):
+                acc |= int(v) << (lane * w)
+            words += [(acc >> (32 * q)) & 0xFFFFFFFF for q in range(2 * w)]
+        o = out.numpy().view(np.uint32)
+        o[:len(words)] = np.array(words, dtype=np.uint32)
+        return out
+
+    def delta_unpack(self, coded, n, bits, out):
+        c = coded.numpy().view(np.uint32)
+        ng = -(-n // 64)
+        res = np.empty(ng * 64, dtype=np.uint64)
+        for g in range(ng):
+            acc = 0
+            for q in range(2 * bits):
+                acc |= int(c[ng + g * 2 * bits + q]) << (32 * q)
+            run = int(c[g])
+            for lane in range(64):
+                run += (acc >> (lane * bits)) & ((1 << bits) - 1) if bits else 0
+                res[g * 64 + lane] = run
+        out.numpy().view(np.uint32)[:] = res[:n].astype(np.uint32)
+        return out
+
+    def merge(self, a, b, out):
+        out.copy_(self._t(np.sort(np.concatenate([self._np(a), self._np(b)]))))
+        return out
+
     def segment_copy(self, src, dst, so, do, ln):
         s = src.numpy()
         d = dst.numpy()

@@ -31,6 +31,9 @@ def main():
         out = distrib.sort_msd(keys, ops, rounds=rounds, self_local=False)  # self sends through RCCL
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy().view(np.uint32), ref), "msd rounds=%d" % rounds
+        out = distrib.sort_msdz(keys, ops, rounds=rounds)  # streams, coded widths gathered over RCCL
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), ref), "msdz rounds=%d" % rounds
     rng = np.random.default_rng(3)
     m = (1 << 20) + 77
     k = rng.integers(0, 1 << 14, m, dtype=np.uint64) * np.uint64(0x0004000000000101)  # equal keys

@@ -161,3 +161,31 @@ def test_distrib_pairs_eight_ranks_gloo(tmp_path):
     rk, rv = oracle.stable_sort_kv64(k, np.arange(n, dtype=np.uint32))
     np.testing.assert_array_equal(np.concatenate(ks), rk)
     np.testing.assert_array_equal(np.concatenate(vs), rv)
+
+
+@pytest.mark.parametrize("world,rounds,case", [(2, 4, "pcg"), (2, 1, "dups"), (3, 3, "pcg"), (2, 5, "clustered"),
+                                               (4, 2, "pcg")])
+def test_msdz_delta_coded_exchange_gloo(tmp_path, world, rounds, case):
+    """The delta-coded schedule (sender-side round sorts, coded pieces,
+    receiver-side merges): shard for shard equal to the oracle, including
+    duplicate-heavy input (zero gaps) and clustered keys (wide gaps)."""
+    from oracle import oracle
+    rng = np.random.default_rng(world * 10 + rounds)
+    if case == "pcg":
+        x = oracle.pcg(40009, first=world + rounds)
+    elif case == "dups":
+        x = rng.integers(0, 1 << 20, 30011, dtype=np.uint64).astype(np.uint32) << np.uint32(12)
+    else:
+        x = (rng.integers(0, 16, 30011, dtype=np.uint64) << np.uint64(28)
+             | rng.integers(0, 5000, 30011, dtype=np.uint64)).astype(np.uint32)
+    shards = run_ranks(x, world, "msdz", tmp_path, port=30100 + 13 * world + rounds, kw={"rounds": rounds})
+    np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))
+    assert [s.size for s in shards] == [s.size for s in shard_inputs(x, world)]
+
+
+def test_auto_schedule_gloo(tmp_path):
+    """schedule="auto" (the bench default) picks the delta-coded schedule at 2 ranks."""
+    from oracle import oracle
+    x = oracle.pcg(20011, first=5)
+    shards = run_ranks(x, 2, "auto", tmp_path, port=30190)
+    np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))

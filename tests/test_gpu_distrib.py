@@ -47,6 +47,20 @@ def test_msd_rounds_hip_backend(tmp_path, rounds):
     assert [s.size for s in shards] == [s.size for s in shard_inputs(x, 2)]
 
 
+@pytest.mark.parametrize("world,rounds", [(2, 4), (2, 1), (3, 3)])
+def test_msdz_hip_backend(tmp_path, world, rounds):
+    """The delta-coded schedule with libsort's kernels (range sorts, gap
+    coding, merges) on the GPU; ranks share the GPU, exchanges over gloo."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle import oracle
+    x = oracle.pcg((1 << 20) + 4321, first=world * 10 + rounds)
+    shards = run_ranks(x, world, "msdz", tmp_path, use_gpu=True, port=30300 + 10 * world + rounds,
+                       kw={"rounds": rounds})
+    np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))
+    assert [s.size for s in shards] == [s.size for s in shard_inputs(x, world)]
+
+
 def test_distrib_pairs_hip_backend(tmp_path):
     """C5 path on the GPU: stable (u64 key, u32 payload) sort over 2 ranks."""
     if not torch.cuda.is_available():
