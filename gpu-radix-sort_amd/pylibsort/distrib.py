@@ -855,9 +855,10 @@ def _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride, self_local
     return _rebalance_pairs(ok_, ov, n_recv, ops, group)
 
 
-def distrib_sort(keys, ops=None, group=None, schedule="msd", **kw):
+def distrib_sort(keys, ops=None, group=None, schedule="auto", **kw):
     """Sort the distributed uint32 array whose rank-r shard is `keys`.
-    Returns this rank's shard of the sorted array (ceil(N/R) keys per rank)."""
+    Returns this rank's shard of the sorted array (ceil(N/R) keys per rank).
+    schedule: "auto" (msdz at 2 ranks, msd otherwise), "msd", "msdz", "lsd"."""
     ops = HipOps() if ops is None else ops
     if dist.get_world_size(group) == 1:
         return ops.sort(keys)
