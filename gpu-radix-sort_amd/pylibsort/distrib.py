@@ -245,6 +245,16 @@ def _to_host_async(t):
 _side_streams = {}
 
 
+def _named_stream(name, device):
+    """One long-lived stream per (purpose, device), created once (torch's
+    pool hands out a fixed set of streams round robin)."""
+    key = (name, device)
+    st = _side_streams.get(key)
+    if st is None:
+        st = _side_streams[key] = torch.cuda.Stream(device=device)
+    return st
+
+
 class _SideWork:
     """Context for bookkeeping work (bucket sizes, their all-gather, the
     small D2H) that must not delay the partition scatter: on the GPU it runs
@@ -718,8 +728,8 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
             ev.record()
         evs.append(ev)
     _mark(trace, "rounds sorted and coded")
-    comm = torch.cuda.Stream(device=keys.device) if cuda else None
-    mstream = torch.cuda.Stream(device=keys.device) if cuda else None
+    comm = _named_stream("comm", keys.device) if cuda else None
+    mstream = _named_stream("merge", keys.device) if cuda else None
     keep = []
     for i in range(K):
         # the gap widths of round i are gathered only now, after round i-1's
