@@ -18,16 +18,17 @@ def _cases():
         "dups": rng.integers(0, 50, 30011, dtype=np.uint64).astype(np.uint32),
         "allequal": np.full(9001, 12345, dtype=np.uint32),
         "skewtop": (rng.integers(0, 1 << 20, 20000, dtype=np.uint64).astype(np.uint32)),  # one top bucket
+        "tiny": oracle.pcg(2, first=9),                                                    # an empty shard at 3 ranks
     }
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("schedule", ["lsd", "msd"])
-@pytest.mark.parametrize("case", ["pcg1111", "pcg40001", "dups", "allequal", "skewtop"])
+@pytest.mark.parametrize("schedule", ["lsd", "msd", "msdz"])
+@pytest.mark.parametrize("case", ["pcg1111", "pcg40001", "dups", "allequal", "skewtop", "tiny"])
 def test_distributed_sort_gloo(tmp_path, world, schedule, case):
     from oracle import oracle
     x = _cases()[case]
-    port = 29600 + world * 10 + (1 if schedule == "msd" else 0) + 2 * list(_cases()).index(case)
+    port = 29600 + world * 30 + ["lsd", "msd", "msdz"].index(schedule) + 3 * list(_cases()).index(case)
     shards = run_ranks(x, world, schedule, tmp_path, port=port)
     got = np.concatenate(shards)
     np.testing.assert_array_equal(got, oracle.sort_u32(x))
