@@ -10,8 +10,10 @@ c2 (default; the bench line): configs[1] = "256M uint32, 4-bit digits,
     device-resident form of providedGpu).
     N>1: launched by torch.distributed.run, one rank per GPU; rank r holds keys
     [r*2^28, (r+1)*2^28) of the same stream (weak scaling); one step = one
-    distributed sort (pylibsort.distrib, "msd" schedule: one table partition,
-    range-split RCCL alltoallv rounds overlapped with the per-round sorts)
+    distributed sort (pylibsort.distrib, schedule "auto": at 4 and 8 GPUs
+    "msd" -- one table partition, range-split RCCL point-to-point rounds
+    overlapped with the per-round sorts; at 2 GPUs "msdz" -- the same rounds
+    sorted before sending and exchanged gap-coded, merged on arrival)
     ending with rank r holding keys [r*S, (r+1)*S) of the sorted array.
 c3: configs[2], 2^30 keys, 8-bit digits, one GPU.
 c5: configs[4], stable (u64 key, u32 payload) sort, 2^28 pairs per GPU (2^31
