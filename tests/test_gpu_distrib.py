@@ -187,3 +187,33 @@ def test_bench_multi_rank_path_rehearsal():
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["verified"] is True and line["rehearsal"]
     assert line["config"]["global_keys"] == 2 << 20 and line["variants"]["digit8"]["value"] > 0
+
+
+def test_bench_single_gpu_line_contract():
+    """bench.py at N=1 (small steps): one JSON line with the driver's keys,
+    the roofline object (live per-launch pass time), a verified sort, the
+    8-bit variant and the PCIe-inclusive host-ABI leg checked against the
+    device sort."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import json
+    import pathlib
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    cmd = [sys.executable, str(root / "bench.py"), "--steps", "3", "--warmup", "1", "--keys-log2", "24",
+           "--cpu-sample-log2", "18"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=str(root))
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["verified"] is True and d["value"] > 0
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and 0 < rf["frac"] < 1
+    assert abs(rf["achieved"] / rf["peak"] - rf["frac"]) < 1e-3
+    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] == 1
+    assert d["host_abi"]["value"] > 0 and d["variants"]["digit8"]["value"] > 0
