@@ -5,16 +5,19 @@
 
 c2 (default; the bench line): configs[1] = "256M uint32, 4-bit digits,
     gpuFullSort on 1 MI355X": 2^28 keys of the reference populateInput stream
-    per GPU (generated on the GPU by skip-ahead), one step = one full 32-bit
-    LSD sort through the libsort C ABI (libsortSortKeysU32 = the
-    device-resident form of providedGpu).
-    N>1: launched by torch.distributed.run, one rank per GPU; rank r holds keys
-    [r*2^28, (r+1)*2^28) of the same stream (weak scaling); one step = one
-    distributed sort (pylibsort.distrib, schedule "auto": at 4 and 8 GPUs
-    "msd" -- one table partition, range-split RCCL point-to-point rounds
-    overlapped with the per-round sorts; at 2 GPUs "msdz" -- the same rounds
-    sorted before sending and exchanged gap-coded, merged on arrival)
-    ending with rank r holding keys [r*S, (r+1)*S) of the sorted array.
+    (generated on the GPU by skip-ahead), one step = one full 32-bit LSD sort
+    through the libsort C ABI (libsortSortKeysU32 = the device-resident form
+    of providedGpu).
+    N>1 = configs[3] ("2^32 uint32 sharded 8xMI355X"): 2^29 keys per GPU
+    (2^32 at N=8); rank r holds keys [r*2^29, (r+1)*2^29) of the same stream
+    (weak scaling); one step = one distributed sort (pylibsort.distrib,
+    schedule "auto": one table partition, range-split RCCL point-to-point
+    rounds overlapped with the per-round sorts -- "msd" at 4 and 8 GPUs,
+    "msdz" at 2, the same rounds sorted before sending and exchanged
+    gap-coded) ending with rank r holding keys [r*S, (r+1)*S) of the sorted
+    array.  `python bench.py --gpus N` with no launcher starts its N ranks
+    itself: torch.distributed.run as a CHILD process (no exec), rank 0's JSON
+    line relayed, non-zero exit if any rank fails.
 c3: configs[2], 2^30 keys, 8-bit digits, one GPU.
 c5: configs[4], stable (u64 key, u32 payload) sort, 2^28 pairs per GPU (2^31
     on 8 GPUs); key = (draw 2i << 32) | draw 2i+1 of the stream, payload = the
@@ -49,32 +52,90 @@ def parse():
                     help="auto: msdz (delta-coded exchange) at 2 GPUs, msd otherwise")
     ap.add_argument("--rounds", type=int, default=4, help="msd exchange rounds (pylibsort.distrib.ROUNDS)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-log2", type=int, default=26)
+    ap.add_argument("--cpu-sample-log2", type=int, default=28,
+                    help="keys of the providedCpu baseline sample (BASELINE.md section 3: 2^28)")
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--no-host-abi", action="store_true", help="skip the PCIe-inclusive providedGpu leg")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--algo", default=None, choices=["auto", "tiles", "onesweep", "rts"],
                     help="force the pass algorithm (LIBSORT_ALGO)")
     a = ap.parse_args()
-    defaults = {"c2": (28, 4), "c3": (30, 8), "c5": (28, 8)}[a.workload]
+    # c2 at N>1 is configs[3]: 2^29 keys per GPU, 2^32 over 8 GPUs
+    defaults = {"c2": (28 if a.gpus == 1 else 29, 4), "c3": (30, 8), "c5": (28, 8)}[a.workload]
     a.keys_log2 = defaults[0] if a.keys_log2 is None else a.keys_log2
     a.digit_bits = defaults[1] if a.digit_bits is None else a.digit_bits
     return a
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nranks, argv):
+    """`bench.py --gpus N` without a launcher: start torch.distributed.run
+    with N ranks as a child process (never exec: nothing here has touched the
+    GPU, and the ranks initialise it themselves), pass its stderr through,
+    relay rank 0's JSON line and return the launcher's exit status (non-zero
+    when any rank failed)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nranks),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(pathlib.Path(__file__).resolve())]
+    cmd += list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = []
+    for ln in p.stdout:
+        if ln.startswith("{"):
+            lines.append(ln.strip())
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = p.wait()
+    if rc != 0:
+        sys.stderr.write("bench.py: torch.distributed.run exited with %d\n" % rc)
+        return rc if rc > 0 else 1
+    if len(lines) != 1:
+        sys.stderr.write("bench.py: expected one JSON line from rank 0, got %d\n" % len(lines))
+        return 1
+    print(lines[0], flush=True)
+    return 0
+
+
+def launch_probe(mode):
+    """BENCH_LAUNCH_PROBE (CPU tests of the launcher): every rank joins a gloo
+    group and rank 0 prints one JSON line; "fail" makes rank 1 exit 3.  No GPU
+    is touched."""
+    import torch.distributed as dist
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    if mode == "fail" and rank == 1:
+        sys.exit(3)
+    dist.init_process_group("gloo")
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"probe": True, "world": world}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
     args = parse()
     if args.algo:
         os.environ["LIBSORT_ALGO"] = args.algo
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    probe = os.environ.get("BENCH_LAUNCH_PROBE")
+    if probe:
+        return launch_probe(probe)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if world == 1:
-            raise SystemExit("--gpus %d needs torch.distributed.run with %d processes" % (args.gpus, args.gpus))
     if args.workload == "c3" and world > 1:
         raise SystemExit("c3 is a single-GPU configuration")
     # BENCH_REHEARSAL=1: several ranks on ONE GPU over gloo (host-staged
@@ -198,29 +259,20 @@ def main():
         if ds:
             bytes_per_launch = unit_bytes * ds["keys_per_launch"]
             achieved = bytes_per_launch / (ds["avg_us"] * 1e-6) / 1e9
-            traffic = None
-            pmc = ROOT / "profiles" / ("pmc_%s.json" % ds_name)
-            # the committed PMC profile is of the N=1 configs[1] line only
-            if pmc.exists() and args.workload == "c2" and world == 1 and args.keys_log2 == 28:
-                try:
-                    traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
-                except Exception:
-                    traffic = None
             roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
                         "kernel": "k_%s (rank + scatter pass)" % ds_name, "algorithmic_bytes_per_launch": bytes_per_launch,
-                        "avg_launch_us": round(ds["avg_us"], 2)}
+                        "avg_launch_us": round(ds["avg_us"], 2), "launches": ds["launches"],
+                        "timing": "live hipEvents around every pass launch of the timed steps, on libsort's stream"}
+            # the committed profiles of THIS round's build and bench command
+            # (tools/collect_profiles.sh): HBM bytes per launch from the PMC
+            # passes, and the same kernel's average duration in rocprofv3's
+            # kernel trace, so `frac` can be re-derived from profiles/
+            if args.workload == "c2" and world == 1 and args.keys_log2 == 28 and ds_name == "tilepass":
+                roofline.update(committed_profile(bytes_per_launch))
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not pairs:
-            from oracle import oracle  # CPU baseline leg only (the checker's std::sort)
-            m = 1 << args.cpu_sample_log2
-            x = oracle.pcg(m)
-            c0 = time.perf_counter()
-            oracle.lib().oracle_sort_u32(oracle._p32(x), x.size)
-            c1 = time.perf_counter()
-            cpu = {"value": round(m / (c1 - c0) / 1e9, 5), "unit": "Gkeys/s", "cores": 1, "kind": "port",
-                   "sample": "std::sort (providedCpu, invokers.cu:68-71) of the first 2^%d populateInput keys, "
-                             "1 thread, %.2f s" % (args.cpu_sample_log2, c1 - c0)}
+            cpu = cpu_baseline_leg(torch, pylibsort, keys, out, args.cpu_sample_log2)
         variants = {}
         if world > 1 and variant8 is not None:
             variants["digit8"] = variant8
@@ -243,6 +295,11 @@ def main():
             variants["digit8"] = {"ms_per_step": round(ms8, 4), "value": round(n / (ms8 * 1e-3) / 1e9, 3),
                                   "note": "same sort with 8-bit digits (4 passes, configs[2] digit width); output "
                                           "checked equal to the 4-bit sort"}
+        if world == 1 and not args.no_variants and args.workload == "c2" and args.keys_log2 == 28:
+            # the other single-GPU configurations, each with its own live
+            # per-kernel timings (never `value`)
+            variants["c3"] = config_leg(torch, pylibsort, D, "c3", max(5, args.steps // 2))
+            variants["c5"] = config_leg(torch, pylibsort, D, "c5", max(5, args.steps // 2))
         host_abi = None
         if world == 1 and not args.no_host_abi and args.workload == "c2":
             host_abi = host_abi_leg(torch, pylibsort, keys, out)
@@ -263,9 +320,12 @@ def main():
         else:
             metric, unit, dtype = "Gkeys/sec uint32 full sort", "Gkeys/s", "u32"
             if world > 1:
-                workload = ("configs[3] (sharded full sort, range rounds + RCCL alltoallv) at configs[1]'s "
-                            "2^%d uint32 keys per GPU, %d-bit digits, weak scaling from the N=1 line%s"
-                            % (args.keys_log2, args.digit_bits, sched))
+                workload = ("configs[3]: sharded full sort of 2^%d uint32 keys = 2^%d per GPU (configs[3] names "
+                            "2^32 over 8 GPUs), %d-bit digits in the local sorts, weak scaling%s"
+                            % (args.keys_log2 + (world - 1).bit_length(), args.keys_log2, args.digit_bits, sched)
+                            if world & (world - 1) == 0 else
+                            "configs[3]: sharded full sort, 2^%d uint32 keys per GPU over %d GPUs, %d-bit digits%s"
+                            % (args.keys_log2, world, args.digit_bits, sched))
             else:
                 workload = "configs[%d]: 2^%d uint32 keys per GPU, %d-bit digits, full sort%s" % (
                     1 if args.workload == "c2" else 2, args.keys_log2, args.digit_bits, sched)
@@ -297,6 +357,128 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+PROFILE_TAG = "r02"  # profiles/<tag>_* of this round's build (tools/collect_profiles.sh)
+
+
+def committed_profile(bytes_per_launch):
+    """traffic + rocprof agreement fields from profiles/<PROFILE_TAG>_*.json."""
+    out = {}
+    pmc = ROOT / "profiles" / ("%s_pmc_tilepass.json" % PROFILE_TAG)
+    rp = ROOT / "profiles" / ("%s_rocprof_tilepass.json" % PROFILE_TAG)
+    try:
+        d = json.loads(pmc.read_text())
+        out["traffic"] = d["hbm_bytes_per_launch"]
+        out["traffic_source"] = "profiles/%s (%s)" % (pmc.name, d.get("method", ""))
+    except (OSError, ValueError, KeyError):
+        pass
+    try:
+        d = json.loads(rp.read_text())
+        us = float(d["avg_launch_us"])
+        out["rocprof"] = {"avg_launch_us": round(us, 2), "launches": d.get("launches"),
+                          "frac": round(bytes_per_launch / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4),
+                          "source": "profiles/%s" % rp.name, "cmd": d.get("cmd")}
+    except (OSError, ValueError, KeyError):
+        pass
+    return out
+
+
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_leg(torch, pylibsort, keys, sorted_keys, sample_log2):
+    """SURVEY.md section 8(d) CPU baseline: this library's exported
+    providedCpu (std::sort, invokers.cu:68-71; single thread, as the
+    reference) on the first 2^k keys of the same workload, timed on this
+    box's host; the result is checked equal to the GPU sort when the sample
+    is the whole workload."""
+    import numpy as np
+    m = min(1 << sample_log2, keys.numel())
+    buf = np.ascontiguousarray(keys[:m].cpu().numpy().view(np.uint32))
+    L = pylibsort.lib()
+    c0 = time.perf_counter()
+    if L.providedCpu(buf.ctypes.data, buf.size) != 1:
+        raise RuntimeError("providedCpu failed: %s" % pylibsort.last_error())
+    c1 = time.perf_counter()
+    checked = m == keys.numel()
+    if checked and not np.array_equal(buf, sorted_keys.cpu().numpy().view(np.uint32)):
+        raise RuntimeError("providedCpu disagrees with the GPU sort")
+    return {"value": round(m / (c1 - c0) / 1e9, 5), "unit": "Gkeys/s", "cores": 1, "kind": "port",
+            "sample": "libsort providedCpu (std::sort, invokers.cu:68-71), 1 thread, on the first 2^%d keys of the "
+                      "bench workload: %.2f s%s" % (sample_log2, c1 - c0,
+                                                    "; output equal to the GPU sort" if checked else ""),
+            "host_cpu": _cpu_model(), "nproc": os.cpu_count()}
+
+
+def config_leg(torch, pylibsort, D, which, reps):
+    """configs[2] (2^30 uint32 keys, 8-bit digits) or configs[4]'s per-GPU
+    share (2^28 (u64 key, u32 payload) pairs, stable), timed like the main
+    line with live per-kernel events; verified by sortedness + checksums
+    (tests/test_gpu_parity.py pins both bit-exact)."""
+    kind = {"c3": (30, 8), "c5": (28, 8)}[which]
+    n = 1 << kind[0]
+    prev = pylibsort.setDigitBits(kind[1])
+    try:
+        if which == "c3":
+            keys = D.populate_u32(n)
+            out, tmp = torch.empty_like(keys), torch.empty_like(keys)
+            vals = None
+
+            def step():
+                return D.sort_keys_u32(keys, out=out, tmp=tmp)
+        else:
+            w = D.populate_u32(2 * n).view(n, 2).to(torch.int64)
+            keys = (w[:, 0] << 32) | (w[:, 1] & 0xFFFFFFFF)
+            del w
+            vals = torch.arange(n, dtype=torch.int64, device="cuda").to(torch.int32)
+            out, outv = torch.empty_like(keys), torch.empty_like(vals)
+            tmp, tmpv = torch.empty_like(keys), torch.empty_like(vals)
+
+            def step():
+                return D.sort_pairs_u64_u32(keys, vals, out_keys=out, out_vals=outv, tmp_keys=tmp, tmp_vals=tmpv)
+        for _ in range(2):
+            res = step()
+        torch.cuda.synchronize()
+        D.timing_reset()
+        D.timing_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            res = step()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        D.timing_enable(False)
+        kern = {}
+        for name in ("tilecounts", "colscan", "tilepass"):
+            launches, ms, kk = D.timing_query(name)
+            if launches:
+                kern[name] = {"launches": launches, "avg_us": round(1e3 * ms / launches, 2)}
+        ok = verify(torch, None, 1, keys, res, vals)
+        ms = 1e3 * (t1 - t0) / reps
+        unit_bytes = 24.0 if which == "c5" else 8.0
+        tp = kern.get("tilepass")
+        leg = {"ms_per_step": round(ms, 4), "value": round(n / (ms * 1e-3) / 1e9, 3),
+               "unit": "Gpairs/s" if which == "c5" else "Gkeys/s", "verified": ok, "kernels": kern,
+               "workload": ("configs[2]: 2^30 uint32 keys, 8-bit digits, full sort" if which == "c3" else
+                            "configs[4] per-GPU share: 2^28 (u64 key, u32 payload) pairs, 8-bit digits, stable")}
+        if tp:
+            ach = unit_bytes * n / (tp["avg_us"] * 1e-6) / 1e9
+            leg["scatter_roofline"] = {"achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                       "frac": round(ach / HBM_PEAK_GBPS, 4),
+                                       "bytes_per_unit": unit_bytes}
+        if not ok:
+            raise RuntimeError("%s leg failed verification" % which)
+        return leg
+    finally:
+        pylibsort.setDigitBits(prev)
+        torch.cuda.empty_cache()
 
 
 def host_abi_leg(torch, pylibsort, keys, sorted_keys, calls=3):

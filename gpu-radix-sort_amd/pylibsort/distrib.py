@@ -637,7 +637,7 @@ def _exchange_pieces(sends, recvs, group):
     hs = {d: (t.cpu() if staged else t) for d, t in sends.items()}
     hr = {j: (torch.empty(t.numel(), dtype=t.dtype) if staged else t) for j, t in recvs.items()}
     ops_ = []
-    for k in range(1, R):
+    for k in range(R):  # k = 0: a self piece (sort_msdz self_local=False)
         i, j = (me + k) % R, (me - k) % R
         if i in hs:
             ops_.append(dist.P2POp(dist.isend, hs[i], peer(i), group))
@@ -671,7 +671,8 @@ def _merge_runs(runs, ops, out):
     return ops.merge(runs[0], runs[1], out)
 
 
-def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None, sample_stride=16, trace=None):
+def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None, sample_stride=16, trace=None,
+              self_local=True):
     """Range rounds with delta-coded exchange, for link-bound world sizes (the
     bench default at 2 GPUs, where one xGMI link carries half of every shard).
     The same plan and table partition as sort_msd; then per round the SENDER
@@ -685,7 +686,9 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
     exchange runs on a communication stream after that round's coding, and
     decode + merge on a third stream, so sorting, exchange and merging of
     different rounds overlap.  Same result as sort_msd (a full sort is
-    unique); the skew fallback is the same."""
+    unique); the skew fallback is the same.  self_local=False: the rank's own
+    piece is coded and sent to itself through the communicator too (tests:
+    a one-rank RCCL communicator then carries every exchange)."""
     R = dist.get_world_size(group)
     r = dist.get_rank(group)
     _mark(trace, "start")
@@ -706,7 +709,8 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
     cuda = keys.is_cuda
     mg = torch.zeros(R * K, dtype=torch.int32, device=keys.device)
     # worst-case (32-bit gaps) regions for the coded outgoing pieces
-    cap = np.array([_delta_words(sizes[j], 32) if j % R != r else 0 for j in range(R * K)], dtype=np.int64)
+    remote = (lambda d: d != r) if self_local else (lambda d: True)
+    cap = np.array([_delta_words(sizes[j], 32) if remote(j % R) else 0 for j in range(R * K)], dtype=np.int64)
     coff = np.concatenate([[0], np.cumsum(cap)])
     coded = ops.empty(int(coff[-1]))
     evs = []
@@ -718,7 +722,7 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
             ops.sort_range(part[s0:s1], lo, hi, out=srt[s0:s1])
         for d in range(R):
             j = i * R + d
-            if d != r and sizes[j]:
+            if remote(d) and sizes[j]:
                 piece = srt[int(b[j]):int(b[j]) + int(sizes[j])]
                 ops.delta_maxgap(piece, out=mg[j:j + 1])
                 ops.delta_pack(piece, mg[j:j + 1], out=coded[int(coff[j]):int(coff[j + 1])])
@@ -742,12 +746,12 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
         sends, recvs = {}, {}
         for d in range(R):
             j = i * R + d
-            if d != r and sizes[j]:
+            if remote(d) and sizes[j]:
                 w = int(G[r][d]).bit_length()
                 sends[d] = coded[int(coff[j]):int(coff[j]) + _delta_words(sizes[j], w)]
         for src in range(R):
             m = int(C[src][i * R + r])
-            if src != r and m:
+            if remote(src) and m:
                 recvs[src] = ops.empty(_delta_words(m, int(G[src][r]).bit_length()))
         with (torch.cuda.stream(comm) if cuda else contextlib.nullcontext()):
             if cuda:
@@ -760,7 +764,7 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
             if works is not None:
                 works.wait()
             j = i * R + r
-            runs = [srt[int(b[j]):int(b[j]) + int(sizes[j])]]
+            runs = [srt[int(b[j]):int(b[j]) + int(sizes[j])]] if self_local else []
             for src, coded_in in recvs.items():
                 m = int(C[src][i * R + r])
                 runs.append(ops.delta_unpack(coded_in, m, int(G[src][r]).bit_length(), ops.empty(m)))

@@ -34,6 +34,11 @@ def main():
         out = distrib.sort_msdz(keys, ops, rounds=rounds)  # streams, coded widths gathered over RCCL
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy().view(np.uint32), ref), "msdz rounds=%d" % rounds
+        # the coded pieces through RCCL on the comm stream, decoded and merged
+        # on the merge stream, widths gathered on the side stream
+        out = distrib.sort_msdz(keys, ops, rounds=rounds, self_local=False)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy().view(np.uint32), ref), "msdz self-send rounds=%d" % rounds
     rng = np.random.default_rng(3)
     m = (1 << 20) + 77
     k = rng.integers(0, 1 << 14, m, dtype=np.uint64) * np.uint64(0x0004000000000101)  # equal keys

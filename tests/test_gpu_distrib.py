@@ -166,10 +166,13 @@ def test_plan_histogram_layouts(n, stride, block, offset):
     assert row[4096] == n
 
 
-def test_bench_multi_rank_path_rehearsal():
-    """bench.py's N>1 path end to end (2 ranks, gloo, both on the one GPU of
-    the test box): timed distributed sorts, max-over-ranks timing, the
-    collective verification and the 8-bit variant all complete and verify."""
+def test_bench_self_launch_rehearsal():
+    """bench.py's N>1 path end to end as the driver's 8-GPU job starts it
+    (`python bench.py --gpus N`, no launcher: the bench starts
+    torch.distributed.run itself as a child) with 2 ranks on the one GPU of
+    the test box over gloo: timed distributed sorts, max-over-ranks timing,
+    the collective verification and the 8-bit variant all complete, and the
+    parent relays exactly one line."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import json
@@ -178,13 +181,14 @@ def test_bench_multi_rank_path_rehearsal():
     import subprocess
     import sys
     root = pathlib.Path(__file__).resolve().parents[1]
-    env = dict(os.environ, BENCH_REHEARSAL="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", "29557", str(root / "bench.py"), "--gpus", "2",
-           "--steps", "2", "--warmup", "1", "--keys-log2", "20"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["BENCH_REHEARSAL"] = "1"
+    cmd = [sys.executable, str(root / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--keys-log2", "20"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=180, cwd=str(root))
     assert r.returncode == 0, r.stderr[-4000:]
-    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
     assert line["n_gpus"] == 2 and line["verified"] is True and line["rehearsal"]
     assert line["config"]["global_keys"] == 2 << 20 and line["variants"]["digit8"]["value"] > 0
 
@@ -216,4 +220,5 @@ def test_bench_single_gpu_line_contract():
     assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and 0 < rf["frac"] < 1
     assert abs(rf["achieved"] / rf["peak"] - rf["frac"]) < 1e-3
     assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] == 1
+    assert d["cpu_baseline"]["nproc"] >= 1 and d["cpu_baseline"]["host_cpu"]
     assert d["host_abi"]["value"] > 0 and d["variants"]["digit8"]["value"] > 0
