@@ -1,0 +1,293 @@
+// distrib_plan.h -- host arithmetic of the single-process multi-GPU sort
+// (distrib.cpp): shard cut, round plan, exchange tables and rebalance.  Pure
+// C++17 with no HIP types, so the same code is compiled into libsort.so and
+// into the CPU simulation test (tests/cpp/distrib_sim.cpp, built with
+// AddressSanitizer), which runs both schedules on host arrays against the
+// oracle.
+//
+// Reference semantics (paths relative to the reference checkout):
+//   - equal re-cut of the global order into chunks of ceil(N/R) keys:
+//     benchmark/pkg/sort/distrib.go:113, helpers.go:94-121;
+//   - BSP LSD rounds (global order per round: bucket-major, worker-minor):
+//     distrib.go:119-176, localTest/benchmarks.cpp:91-143.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+namespace lsort {
+namespace dplan {
+
+constexpr int kHistBits = 12;                 // top-bit buckets of the round plan
+constexpr int kHistBins = 1 << kHistBits;     // 4096
+constexpr int kLutShift = 32 - kHistBits;     // bucket = key >> 20
+
+// The reference's equal re-cut: S = ceil(N / R) keys per rank.
+inline uint64_t shard_size(uint64_t N, int R) { return R > 0 ? (N + (uint64_t)R - 1) / (uint64_t)R : 0; }
+
+// |[a, a + len) ∩ [d*S, (d+1)*S)| for every d (the last shard is open-ended,
+// distrib.go:113 gives it the remainder), added into out[0..R).
+inline void add_interval_counts(uint64_t a, uint64_t len, uint64_t S, int R, uint64_t* out) {
+  if (!len || R <= 0) return;
+  const uint64_t b = a + len;
+  if (S == 0) {
+    out[R - 1] += len;
+    return;
+  }
+  uint64_t d0 = std::min<uint64_t>(a / S, (uint64_t)R - 1), d1 = std::min<uint64_t>((b - 1) / S, (uint64_t)R - 1);
+  for (uint64_t d = d0; d <= d1; ++d) {
+    const uint64_t lo = d * S, hi = (d + 1 == (uint64_t)R) ? UINT64_MAX : (d + 1) * S;
+    out[d] += std::min(b, hi) - std::max(a, lo);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// round plan ("msd"): contiguous top-12-bit bucket ranges -> (rank, round)
+// ---------------------------------------------------------------------------
+// H: R rows of ld >= 4096 int64 (sampled histograms of the top 12 key bits).
+// lut[b] = round * R + rank for bucket b; est[r] = estimated keys of rank r.
+// Bucket b's middle in rank coordinates x = (cum(b) - G(b)/2) / total * R
+// gives rank floor(x); its round is the first i with x - rank < cw[i] (cw =
+// normalised prefix of growth^i); rank * K + round is made monotone over the
+// buckets (cumulative max).  The same arithmetic as the device planner
+// (k_plan_rounds) and pylibsort.distrib._plan_rounds_t.
+inline void plan_rounds(const int64_t* H, int R, size_t ld, int K, double growth, uint8_t* lut, int64_t* est) {
+  std::vector<double> cw(K);
+  double acc = 0.0, p = 1.0;
+  for (int i = 0; i < K; ++i) {
+    cw[i] = acc + p;
+    acc += p;
+    p *= growth;
+  }
+  for (int i = 0; i < K; ++i) cw[i] /= acc;
+  std::vector<uint64_t> G(kHistBins, 0);
+  uint64_t total = 0;
+  for (int b = 0; b < kHistBins; ++b) {
+    for (int r = 0; r < R; ++r) G[b] += (uint64_t)H[(size_t)r * ld + b];
+    total += G[b];
+  }
+  const double Td = total ? (double)total : 1.0;
+  for (int r = 0; r < R; ++r) est[r] = 0;
+  uint64_t cum = 0;
+  uint32_t run = 0;
+  for (int b = 0; b < kHistBins; ++b) {
+    cum += G[b];
+    const double x = ((double)cum - (double)G[b] / 2.0) / Td * (double)R;
+    int64_t rank = (int64_t)std::floor(x);
+    rank = std::max<int64_t>(0, std::min<int64_t>(rank, R - 1));
+    const double f = x - (double)rank;
+    int rnd = 0;
+    while (rnd < K && cw[rnd] <= f) ++rnd;
+    rnd = std::min(rnd, K - 1);
+    run = std::max(run, (uint32_t)(rank * K + rnd));
+    const uint32_t rk = run / (uint32_t)K, rd = run % (uint32_t)K;
+    lut[b] = (uint8_t)(rd * (uint32_t)R + rk);
+    est[rk] += (int64_t)G[b];
+  }
+}
+
+// [lo, hi) key range of the buckets with lut == code (false if none).
+inline bool group_range(const uint8_t* lut, int code, uint64_t* lo, uint64_t* hi) {
+  int first = -1, last = -1;
+  for (int b = 0; b < kHistBins; ++b)
+    if (lut[b] == code) {
+      if (first < 0) first = b;
+      last = b;
+    }
+  if (first < 0) return false;
+  *lo = (uint64_t)first << kLutShift;
+  *hi = (uint64_t)(last + 1) << kLutShift;
+  return true;
+}
+
+// Skew fallback of the range schedule (identical on every rank): a rank
+// would receive more than max_imbalance * S (+ one tile) keys.
+inline bool msd_too_skewed(const int64_t* est, int R, uint64_t N, double max_imbalance = 1.5) {
+  double hs = 0.0, mx = 0.0;
+  for (int r = 0; r < R; ++r) {
+    hs += (double)est[r];
+    mx = std::max(mx, (double)est[r]);
+  }
+  if (!N || hs <= 0.0) return false;
+  return mx * (double)N / hs > max_imbalance * (double)shard_size(N, R) + 4096.0;
+}
+
+// One piece of an exchange: `count` keys from rank `src` at element offset
+// `src_off` of its send buffer to rank `dst` at `dst_off` of its receive
+// buffer.
+struct Piece {
+  int src, dst;
+  uint64_t src_off, dst_off, count;
+};
+
+// The range-round exchange.  C[r][j] = keys of rank r in partition bucket j
+// = round * R + dest (from its table partition's bucket starts).  Round i of
+// rank r receives, in source-rank order, C[s][i*R + r] keys from every s,
+// into recv[roff[r][i] ...); the pieces of round i are rounds[i].
+struct MsdPlan {
+  int R = 0, K = 0;
+  std::vector<uint64_t> send_start;             // [R][R*K]: bucket starts of rank r's partition
+  std::vector<uint64_t> roff;                   // [R][K+1]: round offsets of rank r's receive buffer
+  std::vector<std::vector<Piece>> rounds;       // [K]
+  std::vector<uint64_t> n_recv;                 // [R]
+};
+
+inline MsdPlan msd_plan(const std::vector<std::vector<uint64_t>>& C, int K) {
+  MsdPlan p;
+  const int R = (int)C.size();
+  p.R = R;
+  p.K = K;
+  const int NB = R * K;
+  p.send_start.assign((size_t)R * NB, 0);
+  for (int r = 0; r < R; ++r) {
+    uint64_t run = 0;
+    for (int j = 0; j < NB; ++j) {
+      p.send_start[(size_t)r * NB + j] = run;
+      run += C[r][j];
+    }
+  }
+  p.roff.assign((size_t)R * (K + 1), 0);
+  p.n_recv.assign(R, 0);
+  for (int r = 0; r < R; ++r) {
+    uint64_t run = 0;
+    for (int i = 0; i < K; ++i) {
+      p.roff[(size_t)r * (K + 1) + i] = run;
+      for (int s = 0; s < R; ++s) run += C[s][(size_t)i * R + r];
+    }
+    p.roff[(size_t)r * (K + 1) + K] = run;
+    p.n_recv[r] = run;
+  }
+  p.rounds.assign(K, {});
+  for (int i = 0; i < K; ++i) {
+    for (int d = 0; d < R; ++d) {
+      uint64_t at = p.roff[(size_t)d * (K + 1) + i];
+      for (int s = 0; s < R; ++s) {
+        const uint64_t m = C[s][(size_t)i * R + d];
+        if (m) p.rounds[i].push_back(Piece{s, d, p.send_start[(size_t)s * NB + (size_t)i * R + d], at, m});
+        at += m;
+      }
+    }
+  }
+  return p;
+}
+
+// Placement of the per-rank results (rank r holds n_have[r] keys, the
+// concatenation over ranks in rank order is the sorted array) into the equal
+// re-cut: rank d ends with global positions [d*S, (d+1)*S).
+inline std::vector<Piece> recut_pieces(const std::vector<uint64_t>& n_have) {
+  const int R = (int)n_have.size();
+  uint64_t N = 0;
+  for (uint64_t x : n_have) N += x;
+  const uint64_t S = shard_size(N, R);
+  std::vector<Piece> out;
+  uint64_t g = 0;
+  for (int s = 0; s < R; ++s) {
+    uint64_t a = g, left = n_have[s];
+    while (left) {
+      const int d = S ? (int)std::min<uint64_t>(a / S, (uint64_t)R - 1) : R - 1;
+      const uint64_t hi = (d == R - 1) ? a + left : std::min(a + left, (uint64_t)(d + 1) * S);
+      const uint64_t m = hi - a;
+      out.push_back(Piece{s, d, a - g, a - (uint64_t)d * S, m});
+      a += m;
+      left -= m;
+    }
+    g += n_have[s];
+  }
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// BSP LSD round ("lsd", the reference's semantics)
+// ---------------------------------------------------------------------------
+// C[s][b] = keys of rank s in bucket b after its local stable partition
+// (bucket starts from gpuPartial's boundaries).  The global order of the
+// round is bucket-major, rank-minor; rank r receives positions [r*S,
+// (r+1)*S).  Rank s's data for rank d is ONE contiguous slice of its
+// partitioned shard (local order -> global position is monotone), so the
+// exchange pieces are contiguous; the receiver then gathers its pieces into
+// bucket-major order with the segment table `seg` (src offsets in its
+// receive buffer, which holds the pieces in source-rank order).
+struct LsdRound {
+  std::vector<Piece> pieces;                       // send slices (src_off in the sender's shard, dst_off in recv)
+  std::vector<uint64_t> n_next;                    // [R]: keys per rank after the round
+  std::vector<std::vector<uint64_t>> seg_src, seg_dst, seg_len;  // [R]: gather table of each receiver
+};
+
+inline LsdRound lsd_round(const std::vector<std::vector<uint64_t>>& C, uint64_t S) {
+  const int R = (int)C.size();
+  const size_t nb = R ? C[0].size() : 0;
+  LsdRound o;
+  o.n_next.assign(R, 0);
+  o.seg_src.assign(R, {});
+  o.seg_dst.assign(R, {});
+  o.seg_len.assign(R, {});
+  // G[s][b]: global start of (s, b); L[s][b]: local start
+  std::vector<std::vector<uint64_t>> G(R, std::vector<uint64_t>(nb)), L(R, std::vector<uint64_t>(nb));
+  uint64_t g = 0;
+  for (size_t b = 0; b < nb; ++b)
+    for (int s = 0; s < R; ++s) {
+      G[s][b] = g;
+      g += C[s][b];
+    }
+  for (int s = 0; s < R; ++s) {
+    uint64_t l = 0;
+    for (size_t b = 0; b < nb; ++b) {
+      L[s][b] = l;
+      l += C[s][b];
+    }
+  }
+  // walk the (s, b) runs cut at shard boundaries: fn(s, d, local start,
+  // position in shard d, length)
+  auto walk = [&](bool bucket_major, auto&& fn) {
+    const size_t outer = bucket_major ? nb : (size_t)R, inner = bucket_major ? (size_t)R : nb;
+    for (size_t x = 0; x < outer; ++x)
+      for (size_t y = 0; y < inner; ++y) {
+        const int s = (int)(bucket_major ? y : x);
+        const size_t bk = bucket_major ? x : y;
+        uint64_t a = G[s][bk], left = C[s][bk], la = L[s][bk];
+        while (left) {
+          const int d = S ? (int)std::min<uint64_t>(a / S, (uint64_t)R - 1) : R - 1;
+          const uint64_t hi = (d == R - 1) ? a + left : std::min(a + left, (uint64_t)(d + 1) * S);
+          const uint64_t m = hi - a;
+          fn(s, d, la, a - (uint64_t)d * S, m);
+          a += m;
+          la += m;
+          left -= m;
+        }
+      }
+  };
+  // send counts M[s][d] and where each slice starts in the sender's shard
+  // (rank-major walk: for fixed s the local order is the global order)
+  std::vector<std::vector<uint64_t>> M(R, std::vector<uint64_t>(R, 0)), first(R, std::vector<uint64_t>(R, UINT64_MAX));
+  walk(false, [&](int s, int d, uint64_t la, uint64_t, uint64_t m) {
+    if (first[s][d] == UINT64_MAX) first[s][d] = la;
+    M[s][d] += m;
+  });
+  // receive buffer of d: the slices in source-rank order
+  std::vector<std::vector<uint64_t>> base(R, std::vector<uint64_t>(R, 0));
+  for (int d = 0; d < R; ++d) {
+    uint64_t run = 0;
+    for (int s = 0; s < R; ++s) {
+      base[s][d] = run;
+      run += M[s][d];
+    }
+    o.n_next[d] = run;
+  }
+  for (int s = 0; s < R; ++s)
+    for (int d = 0; d < R; ++d)
+      if (M[s][d]) o.pieces.push_back(Piece{s, d, first[s][d], base[s][d], M[s][d]});
+  // gather tables in the round's global order (bucket-major, rank-minor)
+  walk(true, [&](int s, int d, uint64_t la, uint64_t pos, uint64_t m) {
+    o.seg_src[d].push_back(base[s][d] + (la - first[s][d]));
+    o.seg_dst[d].push_back(pos);
+    o.seg_len[d].push_back(m);
+  });
+  return o;
+}
+
+}  // namespace dplan
+}  // namespace lsort

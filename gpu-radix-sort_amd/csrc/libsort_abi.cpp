@@ -92,7 +92,7 @@ struct WsOrder {
 static std::mutex g_order_mu;
 static std::vector<WsOrder> g_order;
 
-static bool ws_acquire_stream(int dev, hipStream_t st) {
+bool ws_acquire_stream(int dev, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_order_mu);
   if ((size_t)dev >= g_order.size()) g_order.resize(dev + 1);
   WsOrder& o = g_order[dev];
@@ -104,7 +104,7 @@ static bool ws_acquire_stream(int dev, hipStream_t st) {
   if (o.used && o.last != st) return hip_ok(hipStreamWaitEvent(st, o.evt, 0), "hipStreamWaitEvent");
   return true;
 }
-static void ws_release_stream(int dev, hipStream_t st) {
+void ws_release_stream(int dev, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_order_mu);
   WsOrder& o = g_order[dev];
   (void)hipEventRecord(o.evt, st);
@@ -250,6 +250,50 @@ class Reservation {
     }
   }
   int dev_ = -1;
+};
+
+// RAII reservation of k pool devices for one multi-GPU call.  Multi-device
+// reservations are serialised (two of them each holding part of the pool
+// cannot wait on each other); single-device callers keep taking devices as
+// they free up.
+static std::mutex g_multi_mu;
+class MultiReservation {
+ public:
+  ~MultiReservation() {
+    for (int d : devs_) {
+      g_dev_locks[d].clear();
+      g_dev_sem->up();
+    }
+  }
+  bool reserve(int k) {
+    if (!g_dev_sem) {
+      set_error("initLibSort() must be called before using the GPU entry points");
+      return false;
+    }
+    if (k < 1 || k > g_ndev) {
+      set_error("gpuDistribSort: ngpu must be in [1, " + std::to_string(g_ndev) + "] (the device pool)");
+      return false;
+    }
+    std::lock_guard<std::mutex> lk(g_multi_mu);
+    for (int j = 0; j < k; ++j) {
+      g_dev_sem->down();
+      int got = -1;
+      for (int i = 0; i < g_ndev && got < 0; ++i)
+        if (!g_dev_locks[i].test_and_set()) got = i;
+      if (got < 0) {
+        g_dev_sem->up();
+        set_error("failed to find an available device (pool invariant broken)");
+        return false;
+      }
+      devs_.push_back(got);
+    }
+    std::sort(devs_.begin(), devs_.end());
+    return true;
+  }
+  const std::vector<int>& devices() const { return devs_; }
+
+ private:
+  std::vector<int> devs_;
 };
 
 // ---------------------------------------------------------------------------
@@ -977,7 +1021,44 @@ LIBSORT_EXPORT int libsortTimingQuery(const char* kernel, uint64_t* launches, do
   return timing_query(kernel, launches, total_ms, total_keys) ? 1 : 0;
 }
 
+LIBSORT_EXPORT int gpuDistribSort(uint32_t* h_in, size_t len, int ngpu) {
+  MultiReservation res;
+  if (!res.reserve(ngpu <= 0 ? g_ndev : ngpu)) return 0;
+  if (len == 0) return 1;
+  if (!h_in) {
+    set_error("gpuDistribSort: h_in must not be NULL");
+    return 0;
+  }
+  const std::vector<int>& d = res.devices();
+  return distrib_sort_host_u32(h_in, len, d.data(), (int)d.size(), 0u, g_digit_bits.load()) ? 1 : 0;
+}
+
+LIBSORT_EXPORT int libsortDistribSortU32(int nranks, const int* devices, const uint32_t* const* d_in,
+                                         const size_t* n_in, uint32_t* const* d_out, size_t* n_out, uint32_t flags) {
+  if (nranks < 1 || !devices || !d_in || !n_in || !d_out || !n_out) {
+    set_error("libsortDistribSortU32: need nranks >= 1 and non-NULL tables");
+    return 0;
+  }
+  if (flags & ~(kDistribLsd | kDistribCopy | kDistribSelfRccl)) {
+    set_error("libsortDistribSortU32: unknown flags");
+    return 0;
+  }
+  int ndev = 0;
+  if (!hip_ok(hipGetDeviceCount(&ndev), "hipGetDeviceCount")) return 0;
+  for (int r = 0; r < nranks; ++r)
+    if (devices[r] < 0 || devices[r] >= ndev) {
+      set_error("libsortDistribSortU32: device out of range");
+      return 0;
+    }
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  const bool ok = distrib_sort_u32(devices, nranks, d_in, n_in, d_out, n_out, flags, g_digit_bits.load());
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return ok ? 1 : 0;
+}
+
 LIBSORT_EXPORT int libsortReleaseWorkspace(void) {
+  distrib_release();
   release_all_workspaces();
   return 1;
 }

@@ -201,6 +201,26 @@ hipError_t merge_u32(const uint32_t* a, size_t na, const uint32_t* b, size_t nb,
 hipError_t plan_rounds(const int64_t* d_hist, uint32_t R, uint32_t ld, uint32_t K, double growth, uint8_t* d_lut,
                        int64_t* d_est, hipStream_t stream);
 
+// Cross-stream ordering of a device's workspace (libsort_abi.cpp): a call on
+// stream `st` first waits for the previous call's work on another stream;
+// release records the point after this call's work.
+bool ws_acquire_stream(int dev, hipStream_t st);
+void ws_release_stream(int dev, hipStream_t st);
+
+// ---- single-process multi-GPU sort (distrib.cpp) ----
+constexpr unsigned kDistribLsd = 1u;       // the reference's BSP LSD rounds instead of the range rounds
+constexpr unsigned kDistribCopy = 2u;      // exchanges as peer copies instead of RCCL
+constexpr unsigned kDistribSelfRccl = 4u;  // a rank's own pieces through RCCL too (tests)
+// Rank r's shard d_in[r] (n_in[r] keys, on device devices[r]; devices may
+// repeat) -> d_out[r] = keys [r*S, (r+1)*S) of the sorted whole, S =
+// ceil(N/R); n_out[r] receives the count.  Synchronous.
+bool distrib_sort_u32(const int* devices, int R, const uint32_t* const* d_in, const size_t* n_in, uint32_t* const* d_out,
+                      size_t* n_out, unsigned flags, int digit_bits);
+// Host-pointer form: h[0..len) is cut into R shards of ceil(len/R) keys,
+// sorted across the ranks' devices and copied back in place.
+bool distrib_sort_host_u32(uint32_t* h, size_t len, const int* devices, int R, unsigned flags, int digit_bits);
+void distrib_release();
+
 // ---- per-kernel timing (hipEvents on the launch stream) ----
 bool timing_enabled();
 void timing_enable(bool on);

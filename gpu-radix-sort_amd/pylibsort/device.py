@@ -361,6 +361,34 @@ def merge_u32(a, b, out=None):
     return out
 
 
+LIBSORT_DISTRIB_LSD, LIBSORT_DISTRIB_COPY, LIBSORT_DISTRIB_SELF_RCCL = 1, 2, 4
+
+
+def distrib_sort_u32(shards, flags=0):
+    """libsortDistribSortU32: the single-process multi-GPU sort over the
+    shards' devices (tensors may share a device).  Returns rank r's shard of
+    the sorted whole (keys [r*S, (r+1)*S), S = ceil(N/R)) on shard r's device.
+    Synchronous; the shards' producers are waited for first."""
+    R = len(shards)
+    devs = []
+    for i, t in enumerate(shards):
+        _need(t, _U32, "shards[%d]" % i)
+        devs.append(t.device.index)
+    for d in sorted(set(devs)):
+        torch.cuda.synchronize(d)
+    N = sum(t.numel() for t in shards)
+    S = -(-N // R) if R else 0
+    outs = [torch.empty(max(S, 1), dtype=torch.int32, device=t.device) for t in shards]
+    arr_dev = (ctypes.c_int * R)(*devs)
+    arr_in = (ctypes.c_void_p * R)(*[t.data_ptr() for t in shards])
+    arr_n = (ctypes.c_size_t * R)(*[t.numel() for t in shards])
+    arr_out = (ctypes.c_void_p * R)(*[t.data_ptr() for t in outs])
+    arr_nout = (ctypes.c_size_t * R)()
+    _check(_lib().libsortDistribSortU32(R, arr_dev, arr_in, arr_n, arr_out, arr_nout, flags),
+           "libsortDistribSortU32")
+    return [o[:int(arr_nout[r])] for r, o in enumerate(outs)]
+
+
 def populate_u32(n, first=0, device=None, out=None):
     """Elements [first, first+n) of the reference populateInput stream (fresh
     process), generated on the device."""

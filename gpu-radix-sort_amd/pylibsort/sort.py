@@ -11,7 +11,7 @@ from . import _state, require_gpu
 
 __all__ = [
     "sortException", "sortResultException", "groupBits", "bytesToInts", "checkOrder",
-    "checkSortFull", "checkPartial", "sortFull", "sortPartial", "generateInputs",
+    "checkSortFull", "checkPartial", "sortFull", "sortFullDistrib", "sortPartial", "generateInputs",
     "boundariesToCaps", "setDigitBits", "getDigitBits", "setAlgorithm",
 ]
 
@@ -110,6 +110,18 @@ def sortFull(buf: bytearray):
     cRaw = (ctypes.c_uint8 * len(buf)).from_buffer(buf)
     res = _state.sortLib.providedGpu(ctypes.addressof(cRaw), ctypes.c_size_t(nElem))
     if not res:
+        raise RuntimeError("Libsort had an internal error")
+
+
+def sortFullDistrib(buf: bytearray, ngpu=0):
+    """Sort buf (C uint32s) in place across ngpu GPUs of the device pool
+    (gpuDistribSort; ngpu <= 0: all of them)."""
+    require_gpu()
+    nElem = int(len(buf) / 4)
+    if nElem == 0:
+        return
+    cRaw = (ctypes.c_uint8 * len(buf)).from_buffer(buf)
+    if not _state.sortLib.gpuDistribSort(ctypes.addressof(cRaw), ctypes.c_size_t(nElem), ctypes.c_int(ngpu)):
         raise RuntimeError("Libsort had an internal error")
 
 

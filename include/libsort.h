@@ -211,6 +211,39 @@ LIBSORT_API bool libsortDeltaUnpackU32(const uint32_t* d_in, size_t n, uint32_t 
 LIBSORT_API bool libsortMergeU32(const uint32_t* d_a, size_t na, const uint32_t* d_b, size_t nb, uint32_t* d_out,
                                  void* stream);
 
+/* Multi-GPU sort in one process (replaces the
+ * reference's distributed drivers localTest/benchmarks.cpp:70-160 and
+ * benchmark/pkg/sort/distrib.go:90-179, whose exchange goes through host
+ * memory or files).  The ranks' shards are exchanged over a single-process
+ * RCCL communicator (ncclCommInitAll over the ranks' devices, xGMI
+ * point-to-point); the result is the reference's equal re-cut: rank r holds
+ * keys [r*S, (r+1)*S) of the sorted whole, S = ceil(N / nranks)
+ * (distrib.go:113).
+ *
+ * gpuDistribSort: h_in[0..len) (host) is cut into ngpu shards of
+ * ceil(len/ngpu) keys, sorted across ngpu devices taken from the device pool
+ * (ngpu <= 0: all of them) and copied back in place; ascending, the same
+ * result as providedGpu / std::sort, for len up to ngpu * (2^32 - 1).
+ * Blocks while the devices are busy, like the other pool entry points. */
+LIBSORT_API bool gpuDistribSort(uint32_t* h_in, size_t len, int ngpu);
+
+/* Device-resident form: rank r's shard d_in[r] (n_in[r] <= 2^32-1 keys in
+ * memory of device devices[r], read-only) -> d_out[r] (device devices[r],
+ * capacity ceil(N/nranks) keys), n_out[r] (host) = keys written.  Devices may
+ * repeat (ranks sharing a GPU run one after another and exchange by device
+ * copies; RCCL refuses two ranks on one GPU).  Synchronous: returns when every
+ * device is done.  flags: LIBSORT_DISTRIB_LSD runs the reference's BSP LSD
+ * rounds (8-bit digits, bucket-major / rank-minor re-cut after every round)
+ * instead of the default range rounds; LIBSORT_DISTRIB_COPY exchanges with
+ * peer copies (hipMemcpyPeerAsync) instead of RCCL; LIBSORT_DISTRIB_SELF_RCCL
+ * sends a rank's own pieces through RCCL too (tests). */
+#define LIBSORT_DISTRIB_LSD 1u
+#define LIBSORT_DISTRIB_COPY 2u
+#define LIBSORT_DISTRIB_SELF_RCCL 4u
+LIBSORT_API bool libsortDistribSortU32(int nranks, const int* devices, const uint32_t* const* d_in,
+                                       const size_t* n_in, uint32_t* const* d_out, size_t* n_out,
+                                       uint32_t flags);
+
 /* Writes elements [first, first+n) of the populateInput stream of a fresh
  * process (state 0x4d595df4d0f33173) to device memory, by LCG skip-ahead. */
 LIBSORT_API bool libsortPopulateDevice(uint32_t* d_out, size_t n, uint64_t first, void* stream);

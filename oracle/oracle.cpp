@@ -259,4 +259,39 @@ void oracle_stable_sort_kv64v64(uint64_t* k, uint64_t* v, size_t n) {
   }
 }
 
+// The sorted order of a keys-only array is fixed by how often each value
+// occurs (std::sort, invokers.cu:68-71, has a unique result), so the sorted
+// PCG stream at sizes std::sort cannot finish in seconds is restated as a
+// counting sort: counts[v] = occurrences of v among elements [first,
+// first+n) of the fresh-process populateInput stream (utils.cu:65-80),
+// generated here (no key array is stored).  counts has 2^32 one-byte
+// entries; returns the largest count (the caller rejects 255 = saturation).
+uint32_t oracle_pcg_value_counts(uint8_t* counts, size_t n, uint64_t first) {
+  const uint64_t mult = 6364136223846793005ull, inc = 1442695040888963407ull;
+  // skip-ahead: state after `first` steps (LCG jump by squaring)
+  uint64_t s = 0x4d595df4d0f33173ull, am = mult, ac = inc, m = 1, c = 0;
+  for (uint64_t k = first; k; k >>= 1) {
+    if (k & 1) {
+      m *= am;
+      c = c * am + ac;
+    }
+    ac = (am + 1) * ac;
+    am *= am;
+  }
+  s = m * s + c;
+  uint32_t mx = 0;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t x = s;
+    const unsigned count = (unsigned)(x >> 59);
+    s = x * mult + inc;
+    x ^= x >> 18;
+    const uint32_t v = (uint32_t)(x >> 27);
+    const uint32_t key = (v >> count) | (v << ((0u - count) & 31u));
+    const uint32_t q = counts[key];
+    if (q < 255) counts[key] = (uint8_t)(q + 1);
+    if (q + 1 > mx) mx = q + 1;
+  }
+  return mx;
+}
+
 }  // extern "C"

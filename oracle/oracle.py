@@ -41,6 +41,8 @@ def lib():
         L.oracle_stable_sort_kv32.argtypes = [_u32p, _u32p, ctypes.c_size_t]
         L.oracle_sort_u64.argtypes = [_u64p, ctypes.c_size_t]
         L.oracle_stable_sort_kv64v64.argtypes = [_u64p, _u64p, ctypes.c_size_t]
+        L.oracle_pcg_value_counts.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
+        L.oracle_pcg_value_counts.restype = ctypes.c_uint32
         _lib = L
     return _lib
 
@@ -149,3 +151,25 @@ def stable_sort_kv64v64(k, v):
     vv = np.array(v, dtype=np.uint64, copy=True)
     lib().oracle_stable_sort_kv64v64(_p64(kk), _p64(vv), kk.size)
     return kk, vv
+
+
+def sorted_pcg_sha256(n, first=0, chunk_values=1 << 24):
+    """sha256 (hex) of std::sort of elements [first, first+n) of the
+    populateInput stream, little-endian uint32, without sorting: a one-byte
+    count per value (4 GiB), expanded in value order chunk by chunk."""
+    import hashlib
+    counts = np.zeros(1 << 32, dtype=np.uint8)
+    mx = lib().oracle_pcg_value_counts(counts.ctypes.data, n, first)
+    if mx >= 255:
+        raise RuntimeError("a value occurs 255+ times: one-byte counts saturate")
+    h = hashlib.sha256()
+    total = 0
+    for a in range(0, 1 << 32, chunk_values):
+        c = counts[a:a + chunk_values]
+        nz = np.nonzero(c)[0]
+        if nz.size:
+            vals = np.repeat((nz + a).astype(np.uint32), c[nz])
+            total += vals.size
+            h.update(vals.astype("<u4").tobytes())
+    assert total == n
+    return h.hexdigest()

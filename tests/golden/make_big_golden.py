@@ -1,0 +1,61 @@
+"""Golden sha256 of the configurations too large for the element-wise
+oracle comparison (test_gpu_parity.py: test_config3_2pow30,
+test_maximum_size, test_config5_pairs_size), computed with the oracle here
+(minutes of CPU time), committed as tests/golden/big_golden.json.
+
+  sorted keys:  oracle.sorted_pcg_sha256 -- std::sort (invokers.cu:68-71) of
+                the populateInput stream (utils.cu:65-80) restated as a
+                counting sort; pinned against the reference's own 2^20 and
+                2^28 sorted hashes in pcg_golden.json before anything is written.
+  C5 pairs:     std::stable_sort by key (oracle_stable_sort_kv64) of the
+                bench/test pair construction: key_i = (draw 2i << 32) | draw
+                2i+1, the first n/64 keys masked to 11 bits (many ties),
+                payload_i = i.
+
+Run: python tests/golden/make_big_golden.py
+"""
+import hashlib
+import json
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+from oracle import oracle  # noqa: E402
+
+
+def c5_pairs(n):
+    w = oracle.pcg(2 * n).astype(np.uint64).reshape(n, 2)
+    keys = (w[:, 0] << np.uint64(32)) | w[:, 1]
+    del w
+    keys[: n // 64] &= np.uint64(0x7FF)
+    vals = np.arange(n, dtype=np.uint32)
+    return keys, vals
+
+
+def main():
+    gold = json.loads((ROOT / "tests" / "golden" / "pcg_golden.json").read_text())["sha256_prefix"]
+    out = {"method": __doc__.strip().splitlines()[0], "sorted_u32": {}, "c5_pairs": {}}
+    for n in (1 << 20, 1 << 28):           # pin the restatement on the reference's own hashes
+        h = oracle.sorted_pcg_sha256(n)
+        assert h[:16] == gold[str(n)]["sorted"], (n, h)
+        print("pinned", n, h[:16], flush=True)
+    for n in (1 << 30, (1 << 32) - 1):
+        t = time.time()
+        out["sorted_u32"][str(n)] = oracle.sorted_pcg_sha256(n)
+        print(n, out["sorted_u32"][str(n)], "%.0f s" % (time.time() - t), flush=True)
+    n = 1 << 28
+    t = time.time()
+    k, v = c5_pairs(n)
+    k, v = oracle.stable_sort_kv64(k, v)
+    out["c5_pairs"][str(n)] = {"keys": hashlib.sha256(k.astype("<u8").tobytes()).hexdigest(),
+                               "payloads": hashlib.sha256(v.astype("<u4").tobytes()).hexdigest()}
+    print("c5", out["c5_pairs"][str(n)], "%.0f s" % (time.time() - t), flush=True)
+    (ROOT / "tests" / "golden" / "big_golden.json").write_text(json.dumps(out, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()

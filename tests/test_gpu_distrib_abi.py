@@ -1,0 +1,138 @@
+"""The multi-GPU sort behind the C ABI (libsort.h gpuDistribSort /
+libsortDistribSortU32, csrc/distrib.cpp) on the one-GPU test box:
+
+- one rank over a real single-process RCCL communicator (ncclCommInitAll of
+  one device) with every piece sent through RCCL (LIBSORT_DISTRIB_SELF_RCCL),
+  both schedules;
+- 2-5 ranks sharing the GPU (device-copy exchanges: RCCL refuses two ranks
+  on one GPU), both schedules, ragged and empty shards, duplicate-heavy and
+  skewed inputs (the range schedule falls back to the LSD rounds);
+- the host-pointer entry point gpuDistribSort against the reference's golden
+  sorted hashes.
+
+Parity: the concatenated shards equal std::sort (oracle) bit for bit and
+each shard holds ceil(N/R) keys (the reference's re-cut, distrib.go:113);
+the LSD schedule's shards equal the reference BSP driver's output shard for
+shard (oracle_distrib_bsp_u32)."""
+import hashlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+LSD, COPY, SELF_RCCL = 1, 2, 4
+
+
+@pytest.fixture(scope="module")
+def D():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pylibsort
+    import pylibsort.device as D
+    assert pylibsort.gpu_ready(), pylibsort.last_error()
+    return D
+
+
+@pytest.fixture(params=[4, 8], ids=["digit4", "digit8"])
+def bits(request):
+    import pylibsort
+    prev = pylibsort.setDigitBits(request.param)
+    yield request.param
+    pylibsort.setDigitBits(prev)
+
+
+def _cut(x, R, ragged=False):
+    """R input shards of x (equal, or deliberately ragged with an empty one)."""
+    if not ragged:
+        S = -(-x.size // R)
+        return [x[r * S:(r + 1) * S] for r in range(R)]
+    w = np.array([3, 0, 1, 5, 2][:R], dtype=np.float64) + 1e-9
+    cuts = np.concatenate([[0], np.round(np.cumsum(w) / w.sum() * x.size).astype(np.int64)])
+    cuts[-1] = x.size
+    return [x[cuts[r]:cuts[r + 1]] for r in range(R)]
+
+
+def _run(D, x, R, flags, ragged=False):
+    shards = [torch.from_numpy(np.ascontiguousarray(s).view(np.int32)).cuda() for s in _cut(x, R, ragged)]
+    outs = D.distrib_sort_u32(shards, flags)
+    return [o.cpu().numpy().view(np.uint32) for o in outs]
+
+
+def _check(oracle, x, outs, R, lsd):
+    want = oracle.sort_u32(x)
+    S = -(-x.size // R)
+    assert [o.size for o in outs] == [max(0, min(x.size, (r + 1) * S) - r * S) for r in range(R)]
+    np.testing.assert_array_equal(np.concatenate(outs) if outs else np.empty(0, np.uint32), want)
+    if lsd and x.size:
+        ref, _ = oracle.distrib_bsp_u32(x, R, 8)
+        for r, o in enumerate(outs):
+            np.testing.assert_array_equal(o, ref[r * S:(r + 1) * S])
+
+
+@pytest.mark.parametrize("flags", [SELF_RCCL, SELF_RCCL | LSD, 0, LSD], ids=["rccl-range", "rccl-lsd", "range", "lsd"])
+def test_one_rank_over_rccl(D, oracle_mod, bits, flags):
+    x = oracle_mod.pcg((1 << 22) + 12345, first=5)
+    _check(oracle_mod, x, _run(D, x, 1, flags), 1, flags & LSD)
+
+
+def _cases(oracle):
+    rng = np.random.default_rng(5)
+    return {
+        "pcg": oracle.pcg((1 << 20) + 4321, first=17),
+        "dups": rng.integers(0, 50, 300007, dtype=np.uint64).astype(np.uint32),
+        "skewtop": rng.integers(0, 1 << 20, 200003, dtype=np.uint64).astype(np.uint32),  # one top bucket
+        "allequal": np.full(100001, 7, dtype=np.uint32),
+        "small": oracle.pcg(1111),
+        "tiny": oracle.pcg(3, first=2),
+    }
+
+
+@pytest.mark.parametrize("R", [2, 3, 5])
+@pytest.mark.parametrize("lsd", [False, True], ids=["range", "lsd"])
+@pytest.mark.parametrize("case", ["pcg", "dups", "skewtop", "allequal", "small", "tiny"])
+def test_ranks_sharing_the_gpu(D, oracle_mod, R, lsd, case):
+    x = _cases(oracle_mod)[case]
+    outs = _run(D, x, R, COPY | (LSD if lsd else 0), ragged=(case == "pcg"))
+    _check(oracle_mod, x, outs, R, lsd)
+
+
+def test_repeated_calls_reuse_the_context(D, oracle_mod):
+    """Same ranks, different sizes and inputs back to back (grow-only
+    buffers, cached communicator, stream ordering of the workspaces)."""
+    for i, n in enumerate([1 << 21, 5000, (1 << 21) + 777, 0, 1 << 16]):
+        x = oracle_mod.pcg(n, first=i * 1000)
+        _check(oracle_mod, x, _run(D, x, 3, COPY), 3, False)
+        _check(oracle_mod, x, _run(D, x, 1, SELF_RCCL), 1, False)
+
+
+def test_host_entry_point_golden(D, golden):
+    import pylibsort
+    g, _ = golden
+    for n in (1021, 1111, 4099):
+        x = pylibsort.lib()
+        buf = np.empty(n, dtype=np.uint32)
+        # a fresh stream: elements [0, n) by skip-ahead on the device
+        buf[:] = D.populate_u32(n).cpu().numpy().view(np.uint32)
+        assert hashlib.sha256(buf.tobytes()).hexdigest()[:16] == g["sha256_prefix"][str(n)]["input"]
+        assert x.gpuDistribSort(buf.ctypes.data, n, 1) == 1, pylibsort.last_error()
+        assert hashlib.sha256(buf.tobytes()).hexdigest()[:16] == g["sha256_prefix"][str(n)]["sorted"]
+    # ngpu beyond the pool fails loudly
+    buf = np.arange(10, dtype=np.uint32)
+    assert pylibsort.lib().gpuDistribSort(buf.ctypes.data, buf.size, 64) == 0
+    assert "ngpu" in pylibsort.last_error()
+
+
+@pytest.mark.slow
+def test_reference_size_over_rccl(D, golden):
+    """configs[1]'s 2^28 keys through the distributed path (one RCCL rank,
+    every piece through RCCL): the reference's sorted sha256."""
+    import pylibsort
+    g, _ = golden
+    n = 1 << 28
+    x = D.populate_u32(n)
+    out = D.distrib_sort_u32([x], SELF_RCCL)[0]
+    h = hashlib.sha256(out.cpu().numpy().view(np.uint32).tobytes()).hexdigest()[:16]
+    assert h == g["sha256_prefix"][str(n)]["sorted"]
+    assert pylibsort.lib().libsortDeviceErrors() == 0

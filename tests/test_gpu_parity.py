@@ -428,6 +428,20 @@ def test_reference_size_full_sort_sha(dev, golden, digit_bits):
     assert int(np.count_nonzero(host[1:] == host[:-1])) == g["sha256_prefix"][str(n)]["duplicate_keys"]
 
 
+def _big_golden():
+    import json
+    import pathlib
+    return json.loads((pathlib.Path(__file__).resolve().parent / "golden" / "big_golden.json").read_text())
+
+
+def _device_sha256(t, np_dtype, chunk=1 << 27):
+    """sha256 of a device tensor's little-endian bytes, copied in chunks."""
+    h = hashlib.sha256()
+    for i in range(0, t.numel(), chunk):
+        h.update(t[i:i + chunk].cpu().numpy().view(np_dtype).astype(np_dtype.newbyteorder("<")).tobytes())
+    return h.hexdigest()
+
+
 def _device_sorted_and_checksums(x, out):
     """Size-independent parity at configs too large for the host oracle:
     out is non-decreasing as uint32 and holds the same multiset as x
@@ -462,6 +476,8 @@ def test_config3_2pow30(dev, bits):
         assert pylibsort.lib().libsortDeviceErrors() == 0
         ok, same = _device_sorted_and_checksums(x, out)
         assert ok and same
+        # bit-exact: the oracle's std::sort of the same stream (big_golden.json)
+        assert _device_sha256(out, np.dtype(np.uint32)) == _big_golden()["sorted_u32"][str(n)]
     finally:
         pylibsort.setDigitBits(prev)
 
@@ -470,7 +486,8 @@ def test_config3_2pow30(dev, bits):
 def test_maximum_size(dev, bits):
     """n = 2^32 - 1 keys, the largest the ABI accepts: 32-bit run offsets up to
     the last tile (whose next-tile index wraps), 2^19 / 2^20 tiles.  The keys
-    are the PCG stream; parity by sortedness + multiset checksums."""
+    are the PCG stream; parity: sha256 of the output equal to the oracle's
+    std::sort of the same stream (tests/golden/big_golden.json)."""
     import pylibsort
     if torch.cuda.get_device_properties(0).total_memory < (80 << 30):
         pytest.skip("needs ~64 GiB of device memory")
@@ -481,8 +498,8 @@ def test_maximum_size(dev, bits):
         out = dev.sort_keys_u32(x)
         torch.cuda.synchronize()
         assert pylibsort.lib().libsortDeviceErrors() == 0
-        ok, same = _device_sorted_and_checksums(x, out)
-        assert ok and same
+        del x
+        assert _device_sha256(out, np.dtype(np.uint32)) == _big_golden()["sorted_u32"][str(n)]
     finally:
         pylibsort.setDigitBits(prev)
         torch.cuda.empty_cache()
@@ -491,10 +508,10 @@ def test_maximum_size(dev, bits):
 @pytest.mark.parametrize("bits", [8, 4])
 def test_config5_pairs_size(dev, bits):
     """C5's per-GPU share as one sort: 2^28 (u64 key, u32 payload) pairs with
-    the bench's keys (two consecutive PCG draws) and payload = index.  Parity
-    by properties: keys non-decreasing (uint64 order), payloads increasing
-    inside every run of equal keys (stability), and the (key, payload) pairs
-    unchanged as a multiset (checksum of a mix of both)."""
+    the bench's keys (two consecutive PCG draws) and payload = index.  Parity:
+    sha256 of keys and payloads equal to std::stable_sort of the same pairs
+    (tests/golden/big_golden.json), plus the properties (keys non-decreasing,
+    payloads increasing inside runs of equal keys)."""
     import pylibsort
     prev = pylibsort.setDigitBits(bits)
     try:
@@ -520,6 +537,10 @@ def test_config5_pairs_size(dev, bits):
         def mix(k, p):
             return (((k & 0xFFFFFF) * 1000003 + (k >> 40) * 7 + p) % 1000000007).sum()
         assert int(mix(keys, vals.to(torch.int64) & 0xFFFFFFFF)) == int(mix(ok_, v))
+        # bit-exact: std::stable_sort of the same pairs (big_golden.json)
+        g = _big_golden()["c5_pairs"][str(n)]
+        assert _device_sha256(ok_, np.dtype(np.uint64)) == g["keys"]
+        assert _device_sha256(ov, np.dtype(np.uint32)) == g["payloads"]
     finally:
         pylibsort.setDigitBits(prev)
         torch.cuda.empty_cache()

@@ -125,3 +125,21 @@ def test_u64_oracles_match_numpy(oracle_mod):
     rk, rv = oracle_mod.stable_sort_kv64v64(k, v)
     np.testing.assert_array_equal(rk, k[idx])
     np.testing.assert_array_equal(rv, v[idx])
+
+
+def test_counting_sort_restatement_pinned(oracle_mod, golden):
+    """oracle.sorted_pcg_sha256 (the counting-sort restatement that produced
+    tests/golden/big_golden.json for 2^30 and 2^32-1 keys) reproduces the
+    reference's own sorted hash (pcg_golden.json, recorded from utils.cu +
+    std::sort) at 2^20, and agrees with std::sort at an offset."""
+    import hashlib
+    import json
+    import pathlib
+    g, _ = golden
+    assert oracle_mod.sorted_pcg_sha256(1 << 20)[:16] == g["sha256_prefix"][str(1 << 20)]["sorted"]
+    x = oracle_mod.pcg(70001, first=123)
+    want = hashlib.sha256(oracle_mod.sort_u32(x).astype("<u4").tobytes()).hexdigest()
+    assert oracle_mod.sorted_pcg_sha256(70001, first=123) == want
+    big = json.loads((pathlib.Path(__file__).resolve().parent / "golden" / "big_golden.json").read_text())
+    assert set(big["sorted_u32"]) == {str(1 << 30), str((1 << 32) - 1)}
+    assert set(big["c5_pairs"][str(1 << 28)]) == {"keys", "payloads"}
