@@ -1207,20 +1207,94 @@ __global__ void k_bounds_from_scan(const uint32_t* __restrict__ l1, const uint32
 }
 
 // From sorted data (reference gpu_groups, sort.cu:14-27, plus the host fill
-// loop sort.cu:384-391, but writing the exclusive prefix for empty groups in
-// the same launch): position i writes bounds[g] = i for every group g in
-// (group(i-1), group(i)]; position n closes the remaining groups.
+// loop sort.cu:384-391, but writing the exclusive prefix for every empty
+// group in parallel): bounds[] is first filled with the sentinel ~0u; each
+// position where the group changes marks bounds[group] = i (k_bounds_mark);
+// an empty group then takes the start of the next non-empty group, i.e. a
+// suffix minimum over bounds (k_bounds_min_blocks -> k_bounds_min_top ->
+// k_bounds_min_apply), and trailing empty groups become n.  Every thread
+// does O(16) work whatever the width (up to 2^31 groups).
+constexpr int kBmItems = 16, kBmBlock = 256, kBmTile = kBmItems * kBmBlock;
 template <typename K>
-__global__ void k_group_bounds(const K* __restrict__ sorted, uint32_t n, uint32_t shift,
-                               uint32_t gmask, uint32_t ngroups, uint32_t* __restrict__ bounds) {
+__global__ void k_bounds_mark(const K* __restrict__ sorted, uint32_t n, uint32_t shift, uint32_t gmask,
+                              uint32_t* __restrict__ bounds) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += stride) {
-    const int64_t cur = i < n ? (int64_t)((uint32_t)(sorted[i] >> shift) & gmask) : (int64_t)ngroups;
-    const int64_t prev = i > 0 ? (int64_t)((uint32_t)(sorted[i - 1] >> shift) & gmask) : -1;
-    if (cur != prev) {
-      const int64_t last = cur < (int64_t)ngroups ? cur : (int64_t)ngroups - 1;
-      for (int64_t g = prev + 1; g <= last; ++g) bounds[g] = (uint32_t)i;
-    }
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t cur = (uint32_t)(sorted[i] >> shift) & gmask;
+    if (i == 0 || cur != ((uint32_t)(sorted[i - 1] >> shift) & gmask)) bounds[cur] = (uint32_t)i;
+  }
+}
+
+// min over each kBmTile-entry block of bounds -> mins[block]
+__global__ __launch_bounds__(kBmBlock) void k_bounds_min_blocks(const uint32_t* __restrict__ bounds, uint64_t ng,
+                                                              uint32_t* __restrict__ mins) {
+  __shared__ uint32_t s_m[kBmBlock / kWave];
+  const uint64_t base = (uint64_t)blockIdx.x * kBmTile + (uint64_t)threadIdx.x * kBmItems;
+  uint32_t m = ~0u;
+#pragma unroll
+  for (int j = 0; j < kBmItems; ++j)
+    if (base + j < ng) m = min(m, bounds[base + j]);
+#pragma unroll
+  for (int o = kWave / 2; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor(m, o, kWave));
+  if ((threadIdx.x & (kWave - 1)) == 0) s_m[threadIdx.x / kWave] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t r = ~0u;
+    for (int w = 0; w < kBmBlock / kWave; ++w) r = min(r, s_m[w]);
+    mins[blockIdx.x] = r;
+  }
+}
+
+// In-place exclusive suffix minimum of mins[0..nb) (one block): mins[b] =
+// min over mins[b+1 ..].  Thread t owns a contiguous chunk.
+__global__ __launch_bounds__(1024) void k_bounds_min_top(uint32_t* __restrict__ mins, uint32_t nb) {
+  __shared__ uint32_t s_c[1024];
+  const uint32_t t = threadIdx.x, per = (nb + 1023) / 1024;
+  const uint32_t a = min(nb, t * per), z = min(nb, a + per);
+  uint32_t m = ~0u;
+  for (uint32_t i = a; i < z; ++i) m = min(m, mins[i]);
+  s_c[t] = m;
+  __syncthreads();
+  // inclusive suffix min over the chunk minima (Hillis-Steele, 10 steps)
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    const uint32_t v = t + o < 1024 ? s_c[t + o] : ~0u;
+    __syncthreads();
+    s_c[t] = min(s_c[t], v);
+    __syncthreads();
+  }
+  uint32_t run = t + 1 < 1024 ? s_c[t + 1] : ~0u;  // suffix of the chunks after t
+  for (uint32_t i = z; i > a; --i) {
+    const uint32_t v = mins[i - 1];
+    mins[i - 1] = run;
+    run = min(run, v);
+  }
+}
+
+// bounds[g] = min(bounds[g..]) with the sentinel mapped to n
+__global__ __launch_bounds__(kBmBlock) void k_bounds_min_apply(uint32_t* __restrict__ bounds, uint64_t ng,
+                                                             const uint32_t* __restrict__ carry, uint32_t n) {
+  __shared__ uint32_t s_c[kBmBlock];
+  const uint32_t t = threadIdx.x;
+  const uint64_t base = (uint64_t)blockIdx.x * kBmTile + (uint64_t)t * kBmItems;
+  uint32_t v[kBmItems], m = ~0u;
+#pragma unroll
+  for (int j = 0; j < kBmItems; ++j) {
+    v[j] = base + j < ng ? bounds[base + j] : ~0u;
+    m = min(m, v[j]);
+  }
+  s_c[t] = m;
+  __syncthreads();
+  for (uint32_t o = 1; o < kBmBlock; o <<= 1) {
+    const uint32_t w = t + o < kBmBlock ? s_c[t + o] : ~0u;
+    __syncthreads();
+    s_c[t] = min(s_c[t], w);
+    __syncthreads();
+  }
+  uint32_t run = min(carry[blockIdx.x], t + 1 < kBmBlock ? s_c[t + 1] : ~0u);
+#pragma unroll
+  for (int j = kBmItems - 1; j >= 0; --j) {
+    run = min(run, v[j]);
+    if (base + j < ng) bounds[base + j] = run == ~0u ? n : run;
   }
 }
 
@@ -2201,6 +2275,32 @@ hipError_t sort_impl(Workspace& ws, const K* in, K* out, K* tmp, const V* vin, V
   return hipSuccess;
 }
 
+// gpuPartial boundaries from the sorted keys (n > 0): sentinel fill, marks,
+// suffix-minimum scan (k_bounds_*).  Scratch: ws.hist_tmp.
+hipError_t group_bounds(Workspace& ws, const uint32_t* sorted, size_t n, int lo, uint32_t ngroups, uint32_t* d_bounds,
+                        hipStream_t st) {
+  const uint64_t nb = ((uint64_t)ngroups + kBmTile - 1) / kBmTile;
+  if (ws.hist_tmp_cap < nb) {
+    if (ws.hist_tmp) { (void)hipFree(ws.hist_tmp); ws.hist_tmp = nullptr; }
+    ws.hist_tmp_cap = 0;
+    LS_TRY(hipMalloc(&ws.hist_tmp, nb * sizeof(uint32_t)));
+    ws.hist_tmp_cap = nb;
+  }
+  LS_TRY(hipMemsetAsync(d_bounds, 0xff, (size_t)ngroups * sizeof(uint32_t), st));
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(k_bounds_mark<uint32_t>, dim3(blocks), dim3(256), 0, st, sorted, (uint32_t)n, (uint32_t)lo,
+                     ngroups - 1u, d_bounds);
+  LS_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_bounds_min_blocks, dim3((uint32_t)nb), dim3(kBmBlock), 0, st, d_bounds, (uint64_t)ngroups,
+                     ws.hist_tmp);
+  LS_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_bounds_min_top, dim3(1), dim3(1024), 0, st, ws.hist_tmp, (uint32_t)nb);
+  LS_TRY(hipGetLastError());
+  hipLaunchKernelGGL(k_bounds_min_apply, dim3((uint32_t)nb), dim3(kBmBlock), 0, st, d_bounds, (uint64_t)ngroups,
+                     ws.hist_tmp, (uint32_t)n);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n, int lo,
@@ -2219,10 +2319,7 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
       LS_TRY(hipMemcpyAsync(d_bounds, tiles_digit_starts(ws, tp_tiles<uint32_t>(n, digit_bits), digit_bits),
                             (size_t)ngroups * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
     } else if (ws.last_algo == 3) {
-      const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 256) / 256, 4096);
-      hipLaunchKernelGGL(k_group_bounds<uint32_t>, dim3(blocks), dim3(256), 0, st, out, (uint32_t)n,
-                         (uint32_t)lo, ngroups - 1u, ngroups, d_bounds);
-      LS_TRY(hipGetLastError());
+      LS_TRY(group_bounds(ws, out, n, lo, ngroups, d_bounds, st));
     } else if (ws.last_algo == 1 && width <= 8) {
       // onesweep: window 0 holds exactly the group histogram
       hipLaunchKernelGGL(k_bounds_from_window, dim3(1), dim3(256), 0, st, ws.os_small + kOsWhist, ngroups,
@@ -2236,10 +2333,7 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
                          ws.scan_l2, grid, ngroups, d_bounds);
       LS_TRY(hipGetLastError());
     } else {
-      const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 256) / 256, 4096);
-      hipLaunchKernelGGL(k_group_bounds<uint32_t>, dim3(blocks), dim3(256), 0, st, out, (uint32_t)n,
-                         (uint32_t)lo, ngroups - 1u, ngroups, d_bounds);
-      LS_TRY(hipGetLastError());
+      LS_TRY(group_bounds(ws, out, n, lo, ngroups, d_bounds, st));
     }
   }
   return hipSuccess;

@@ -92,6 +92,45 @@ def test_partial_sort_and_boundaries(dev, oracle_mod, digit_bits, n, offset, wid
         np.testing.assert_array_equal(_u32(b), ref_bounds)
 
 
+@pytest.mark.parametrize("n,width,offset", [(3, 31, 0), (1000, 31, 1), (5, 24, 8), (100003, 24, 0), (1, 20, 12)])
+def test_wide_group_boundaries(dev, oracle_mod, n, width, offset):
+    """Boundaries of wide groups (up to 2^31 of them) from few keys: every
+    empty group takes the next non-empty group's start, in parallel (the
+    first version filled the gap after the last key in one thread: ~2^31
+    serial stores for n = 3).  Complete check without copying 8 GiB: the
+    bounds are non-decreasing and exact at g = 0, the last group, and every
+    present group value v and v + 1 -- a non-decreasing sequence pinned there
+    is pinned everywhere."""
+    import time
+    x = oracle_mod.pcg(n, first=width * 7 + n)
+    ng = 1 << width
+    b = torch.empty(ng, dtype=torch.int32, device="cuda")
+    t = _tensor(x)
+    out = dev.sort_keys_u32(t, offset=offset, width=width, boundaries=b)   # warm-up (allocations)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = dev.sort_keys_u32(t, offset=offset, width=width, boundaries=b)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    grp = (x.astype(np.uint64) >> np.uint64(offset)) & np.uint64(ng - 1)
+    o = np.argsort(grp, kind="stable")
+    np.testing.assert_array_equal(_u32(out), x[o])
+    sg = np.sort(grp)
+    bb = (b.to(torch.int64) & 0xFFFFFFFF)
+    chunk = 1 << 26
+    for i in range(0, ng, chunk):
+        seg = bb[i:i + chunk + 1]
+        assert bool((seg[1:] >= seg[:-1]).all())
+    probes = np.unique(np.concatenate([[0, ng - 1], sg, np.minimum(sg + 1, ng - 1)]).astype(np.int64))
+    got = bb[torch.from_numpy(probes).cuda()].cpu().numpy()
+    np.testing.assert_array_equal(got, np.searchsorted(sg, probes.astype(np.uint64), side="left"))
+    if width <= 24:
+        np.testing.assert_array_equal(bb.cpu().numpy(), np.searchsorted(sg, np.arange(ng, dtype=np.uint64)))
+    assert elapsed < 0.5, elapsed
+    del b, bb
+    torch.cuda.empty_cache()
+
+
 def test_partial_matches_reference_kernel_emulation(dev, oracle_mod, digit_bits):
     # exact emulation of the reference's 2-bit kernels == our stable partition
     for n, off, w in ((1111, 0, 8), (1021, 4, 8), (300, 6, 4), (4099, 0, 32)):

@@ -1,13 +1,17 @@
 #!/usr/bin/env python3
-"""Turns gpurun_out/prof_TAG into committed summaries under profiles/:
-  profiles/TAG_kernel_stats.csv      rocprofv3 --stats of the bench command
-  profiles/TAG_bench.json            the bench line
-  profiles/TAG_bw_probe.txt          HBM ceiling probes (tools/bw_probe)
-  profiles/pmc_<kernel>.json         HBM bytes per launch from FETCH_SIZE /
-                                     WRITE_SIZE (read by bench.py as `traffic`)
+"""Turns gpurun_out/prof_TAG (tools/collect_profiles.sh) into committed
+summaries under profiles/ -- all of the driver's exact bench command:
+  TAG_kernel_stats.csv        rocprofv3 --stats
+  TAG_rocprof_tilepass.json   average duration of the headline pass kernel
+                              (4-bit k_tile_pass on the 2^28-key workload) in
+                              the kernel trace: all its launches, and the
+                              timed steps' launches (bench.py reads this)
+  TAG_pmc_tilepass.json       HBM bytes per launch of the same launches from
+                              FETCH_SIZE / WRITE_SIZE (bench.py's `traffic`)
+  TAG_bench.json, TAG_bw_probe.txt, TAG_calib_copy_rocprim.txt
 gfx950 correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE reports half the
-bytes of a streaming read, verified on this box with tools/calib_copy for
-both 4-byte and 16-byte loads; WRITE_SIZE is exact.  Both are in KiB."""
+bytes of a streaming read (verified on the box with tools/calib_copy, 4- and
+16-byte loads); WRITE_SIZE is exact.  Both are in KiB."""
 import csv
 import glob
 import json
@@ -15,45 +19,71 @@ import pathlib
 import shutil
 import sys
 
-tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
 src = pathlib.Path("gpurun_out") / ("prof_" + tag)
 dst = pathlib.Path("profiles")
-dst.mkdir(exist_ok=True)
-for f in glob.glob(str(src / "stats" / "*kernel_stats.csv")):
+cmd = (src / "cmd.txt").read_text().strip() if (src / "cmd.txt").exists() else "?"
+for f in glob.glob(str(src / "stats" / "**" / "*kernel_stats.csv"), recursive=True):
     shutil.copy(f, dst / ("%s_kernel_stats.csv" % tag))
-if (src / "bench.json").exists():
-    shutil.copy(src / "bench.json", dst / ("%s_bench.json" % tag))
-if (src / "calib.txt").exists():
-    shutil.copy(src / "calib.txt", dst / ("%s_calib_copy_rocprim.txt" % tag))
-if (src / "bw_probe.txt").exists():
-    shutil.copy(src / "bw_probe.txt", dst / ("%s_bw_probe.txt" % tag))
+for name, out in (("bench.json", "bench.json"), ("calib.txt", "calib_copy_rocprim.txt"),
+                  ("bw_probe.txt", "bw_probe.txt")):
+    if (src / name).exists():
+        shutil.copy(src / name, dst / ("%s_%s" % (tag, out)))
+
+KEYS = 1 << 28
+HEADLINE = "k_tile_pass<4, 256, 16, unsigned int, lsort::NoValue"
 
 
-def per_kernel(counter):
-    out = {}
+def headline(row):
+    """The bench's headline pass: 4-bit keys-only RadixDigit k_tile_pass over
+    the 2^28-key workload (65536 tiles of 4096 keys)."""
+    name = row.get("Kernel_Name", "")
+    if HEADLINE not in name or "BiasedDigit" in name or "LutDigit" in name:
+        return False
+    gx = int(float(row.get("Grid_Size_X", row.get("Grid_Size", 0)) or 0))
+    wx = int(float(row.get("Workgroup_Size_X", row.get("Workgroup_Size", 256)) or 256))
+    groups = gx // wx if gx >= wx * 1024 else gx  # grid in work-items or in workgroups
+    return groups == KEYS // 4096
+
+
+trace = sorted(glob.glob(str(src / "stats" / "**" / "*kernel_trace.csv"), recursive=True))
+durs = []
+for f in trace:
+    for r in csv.DictReader(open(f)):
+        if headline(r):
+            durs.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+durs.sort()
+if durs:
+    us = [d for _, d in durs]
+    steps, per = 20, 8  # the command's timed steps, passes per sort
+    timed = us[-steps * per:]
+    rec = {"kernel": "k_tile_pass<4,...> (4-bit keys-only pass, 65536 tiles)", "cmd": cmd,
+           "launches": len(timed), "avg_launch_us": sum(timed) / len(timed),
+           "all_launches": len(us), "avg_all_us": sum(us) / len(us),
+           "min_us": min(us), "max_us": max(us),
+           "note": "avg_launch_us = the last 160 launches (the 20 timed sorts; the warm-up sorts come first in the "
+                   "trace), avg_all_us includes the warm-up"}
+    (dst / ("%s_rocprof_tilepass.json" % tag)).write_text(json.dumps(rec, indent=1) + "\n")
+    print(json.dumps(rec))
+
+
+def pmc(counter):
+    vals = []
     for f in glob.glob(str(src / ("pmc_" + counter) / "**" / "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"]
-            key = ("tilepass" if "tile_pass" in name else "onesweep" if "onesweep" in name else
-                   "downsweep" if "downsweep" in name else "tilecounts" if "tile_counts" in name else None)
-            if key:
-                out.setdefault(key, []).append(float(r["Counter_Value"]))
-    return out
+            if headline(r):
+                vals.append(float(r["Counter_Value"]))
+    return vals
 
 
-fetch, write = per_kernel("FETCH_SIZE"), per_kernel("WRITE_SIZE")
-stats = {}
-for f in glob.glob(str(src / "stats" / "*kernel_stats.csv")):
-    for r in csv.DictReader(open(f)):
-        stats[r["Name"]] = r
-for k in sorted(set(fetch) & set(write)):
-    fr = sum(fetch[k]) / len(fetch[k]) * 1024 * 2  # corrected read bytes
-    wr = sum(write[k]) / len(write[k]) * 1024
-    rec = {"kernel": k, "launches_sampled": len(fetch[k]), "read_bytes_per_launch": fr,
-           "write_bytes_per_launch": wr, "hbm_bytes_per_launch": fr + wr,
-           "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
-                     "`bench.py --steps 5 --warmup 2`; read = 2 x FETCH_SIZE (gfx950, calibrated with "
-                     "tools/calib_copy), write = WRITE_SIZE; KiB -> bytes",
+fetch, write = pmc("FETCH_SIZE"), pmc("WRITE_SIZE")
+if fetch and write:
+    fr = sum(fetch) / len(fetch) * 1024 * 2
+    wr = sum(write) / len(write) * 1024
+    rec = {"kernel": "tilepass", "launches_sampled": len(fetch), "read_bytes_per_launch": fr,
+           "write_bytes_per_launch": wr, "hbm_bytes_per_launch": fr + wr, "algorithmic_bytes_per_launch": 8.0 * KEYS,
+           "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of `%s`; "
+                     "read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE; KiB -> bytes; headline pass launches only" % cmd,
            "round": tag}
-    (dst / ("pmc_%s.json" % k)).write_text(json.dumps(rec, indent=1) + "\n")
+    (dst / ("%s_pmc_tilepass.json" % tag)).write_text(json.dumps(rec, indent=1) + "\n")
     print(json.dumps(rec))
