@@ -56,6 +56,7 @@ def parse():
                     help="keys of the providedCpu baseline sample (BASELINE.md section 3: 2^28)")
     ap.add_argument("--no-variants", action="store_true")
     ap.add_argument("--no-host-abi", action="store_true", help="skip the PCIe-inclusive providedGpu leg")
+    ap.add_argument("--no-legs", action="store_true", help="skip the configs[2] / configs[4] legs of the N=1 line")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--algo", default=None, choices=["auto", "tiles", "onesweep", "rts"],
                     help="force the pass algorithm (LIBSORT_ALGO)")
@@ -295,7 +296,7 @@ def main():
             variants["digit8"] = {"ms_per_step": round(ms8, 4), "value": round(n / (ms8 * 1e-3) / 1e9, 3),
                                   "note": "same sort with 8-bit digits (4 passes, configs[2] digit width); output "
                                           "checked equal to the 4-bit sort"}
-        if world == 1 and not args.no_variants and args.workload == "c2" and args.keys_log2 == 28:
+        if world == 1 and not args.no_variants and not args.no_legs and args.workload == "c2" and args.keys_log2 == 28:
             # the other single-GPU configurations, each with its own live
             # per-kernel timings (never `value`)
             variants["c3"] = config_leg(torch, pylibsort, D, "c3", max(5, args.steps // 2))

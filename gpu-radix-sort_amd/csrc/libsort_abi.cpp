@@ -22,6 +22,7 @@
 #include <string>
 #include <vector>
 
+#include "boundaries.h"
 #include "radix.h"
 
 #define LIBSORT_EXPORT extern "C" __attribute__((visibility("default")))
@@ -319,6 +320,16 @@ static int env_algorithm() {
 }
 static std::atomic<int> g_algorithm{env_algorithm()};
 
+// gpuPartial boundaries: 0 = the exclusive prefix of group counts (what every
+// reference caller and test expects, tests.cpp:41-83, distrib.go:45-52), 1 =
+// the reference's GetBoundaries output bit for bit, quirk included
+// (sort.cu:367-394; boundaries.h).  LIBSORT_BOUNDARIES=reference selects 1.
+static int env_boundary_mode() {
+  const char* s = getenv("LIBSORT_BOUNDARIES");
+  return (s && (s[0] == 'r' || s[0] == 'R' || s[0] == '1')) ? 1 : 0;
+}
+static std::atomic<int> g_boundary_mode{env_boundary_mode()};
+
 int get_algorithm() { return g_algorithm.load(std::memory_order_relaxed); }
 int set_algorithm(int a) {
   if (a < 0 || a > 3) return -1;
@@ -576,6 +587,7 @@ static bool host_sort(uint32_t* h, uint32_t* bounds, size_t len, uint32_t offset
                 "D2H boundaries");
   ws_release_stream(ws->device, st);
   if (ok) ok = hip_ok(hipStreamSynchronize(st), "hipStreamSynchronize");
+  if (ok && partial && g_boundary_mode.load() == 1) reference_boundaries_from_prefix(bounds, ngroups, len);
   return ok;
 }
 
@@ -1013,6 +1025,11 @@ LIBSORT_EXPORT int libsortSetDigitBits(int bits) {
 LIBSORT_EXPORT int libsortGetDigitBits(void) { return g_digit_bits.load(); }
 
 LIBSORT_EXPORT int libsortSetAlgorithm(int algo) { return set_algorithm(algo); }
+
+LIBSORT_EXPORT int libsortSetBoundaryMode(int mode) {
+  if (mode != 0 && mode != 1) return -1;
+  return g_boundary_mode.exchange(mode);
+}
 
 LIBSORT_EXPORT void libsortTimingEnable(bool on) { timing_enable(on); }
 LIBSORT_EXPORT void libsortTimingReset(void) { timing_reset(); }

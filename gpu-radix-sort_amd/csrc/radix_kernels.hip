@@ -1008,9 +1008,14 @@ __device__ __forceinline__ uint32_t xcd_tile_of_block() {
 // a wave's sorted keys mostly share d and slot, so its LDS atomics spread
 // over consecutive dn banks).  The tile's row of C is zeroed after use (it
 // becomes the C_next of the pass after the next).
+#ifdef LIBSORT_TP_WAVES_PER_EU  // A/B knob: occupancy target of the pass kernel
+#define LS_TP_ATTR __attribute__((amdgpu_waves_per_eu(LIBSORT_TP_WAVES_PER_EU)))
+#else
+#define LS_TP_ATTR
+#endif
 template <int BITS, int BLOCK, int ITEMS, typename K, typename V, bool FUSE, typename Op = RadixDigit,
           typename OpN = RadixDigit>
-__global__ __launch_bounds__(BLOCK) void k_tile_pass(const K* __restrict__ kin, K* __restrict__ kout,
+__global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restrict__ kin, K* __restrict__ kout,
                                                      const V* __restrict__ vin, V* __restrict__ vout,
                                                      uint32_t n, Op op_in, OpN op_next,
                                                      uint32_t* __restrict__ C, const uint32_t* __restrict__ B,
@@ -2029,9 +2034,12 @@ constexpr int tp_items() { return sizeof(K) == 8 ? 8 : 16; }
 #ifndef LIBSORT_TP8_BLOCK64
 #define LIBSORT_TP8_BLOCK64 512  // threads of an 8-bit tile of 64-bit keys (8 keys each)
 #endif
+#ifndef LIBSORT_TP4_BLOCK
+#define LIBSORT_TP4_BLOCK 256  // threads of a 4-bit tile (A/B knob)
+#endif
 template <typename K>
 constexpr int tp_block(int bits) {
-  return bits == 4 ? 256 : (sizeof(K) == 8 ? LIBSORT_TP8_BLOCK64 : LIBSORT_TP8_BLOCK);
+  return bits == 4 ? LIBSORT_TP4_BLOCK : (sizeof(K) == 8 ? LIBSORT_TP8_BLOCK64 : LIBSORT_TP8_BLOCK);
 }
 template <typename K>
 uint32_t tp_tiles(size_t n, int bits) {

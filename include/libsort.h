@@ -263,6 +263,18 @@ LIBSORT_API int libsortGetDigitBits(void);
  * if `algo` is invalid. */
 LIBSORT_API int libsortSetAlgorithm(int algo);
 
+/* Boundaries returned by gpuPartial / gpuPartialProfile / gpuPartialSort:
+ * 0 (default) = for every group g the number of elements whose group is < g
+ * (the exclusive prefix every reference caller and test expects:
+ * localTest/tests.cpp:41-83, benchmark/pkg/sort/distrib.go:45-52,
+ * faasTest/pylibsort/data.py:301-304); 1 = bit-for-bit the reference
+ * SortState::GetBoundaries output (sort.cu:367-394), whose host fill leaves an
+ * empty group 1 at 0 and overwrites a first non-empty group >= 2 with the
+ * next group's start.  The two agree whenever group 1 is non-empty.  Initial
+ * value from LIBSORT_BOUNDARIES ("reference" selects 1).  Returns the
+ * previous mode, or -1 if `mode` is invalid. */
+LIBSORT_API int libsortSetBoundaryMode(int mode);
+
 /* Per-kernel timing with hipEvents on the launch stream.  Names: "whist",
  * "onesweep", "upsweep", "scan", "downsweep", "bounds", "histogram",
  * "populate", "segcopy". */

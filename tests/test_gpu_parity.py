@@ -358,6 +358,36 @@ def test_host_abi_matches_golden(dev, golden):
             pylibsort.checkPartial(v["in_%d" % n].tobytes(), bytes(buf), b, off, w)
 
 
+def test_reference_boundaries_mode(dev, oracle_mod, golden):
+    """libsortSetBoundaryMode(1): gpuPartial returns the reference
+    GetBoundaries output bit for bit, quirk included (sort.cu:367-394; the
+    oracle's restatement), on the survey's quirk cases and on inputs with
+    group 1 empty; mode 0 (default) keeps the exclusive prefix."""
+    import pylibsort
+    g, _ = golden
+    L = pylibsort.lib()
+    rng = np.random.default_rng(9)
+    cases = [(np.array(c["input"], dtype=np.uint32), c["offset"], c["width"]) for c in g["boundary_quirk_cases"]]
+    for n, w in ((1021, 8), (5000, 4), (77, 6)):
+        x = rng.integers(0, 1 << w, n, dtype=np.uint64).astype(np.uint32)
+        x[(x & ((1 << w) - 1)) <= 1] |= 2                            # groups 0 and 1 empty
+        cases.append((x, 0, w))
+    cases.append((oracle_mod.pcg(1111), 0, 8))                       # group 1 non-empty: modes agree
+    prev = L.libsortSetBoundaryMode(1)
+    try:
+        for x, off, w in cases:
+            buf = bytearray(x.tobytes())
+            b = pylibsort.sortPartial(buf, off, w)
+            d, _ = oracle_mod.partial_u32(x, off, w)
+            np.testing.assert_array_equal(np.frombuffer(buf, dtype=np.uint32), d)
+            np.testing.assert_array_equal(np.array(b, dtype=np.uint32), oracle_mod.ref_boundaries(d, off, w))
+    finally:
+        L.libsortSetBoundaryMode(prev)
+    x, off, w = cases[0]
+    b = pylibsort.sortPartial(bytearray(x.tobytes()), off, w)
+    assert b == g["boundary_quirk_cases"][0]["exclusive_prefix"]
+
+
 def test_host_abi_edge_cases(dev):
     import pylibsort
     L = pylibsort.lib()

@@ -6,9 +6,9 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out/ab
 rm -f gpurun_out/ab/*.json
 for i in $(seq 1 ${AB_REPS:-2}); do
-  timeout -k 10 200 python bench.py --no-cpu-baseline > gpurun_out/ab/intree_$i.json 2>/dev/null || exit 1
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-legs --no-host-abi $AB_ARGS > gpurun_out/ab/intree_$i.json 2>/dev/null || exit 1
   for lib in "$@"; do
-    LIBSORT_PATH=$PWD/$lib timeout -k 10 200 python bench.py --no-cpu-baseline \
+    LIBSORT_PATH=$PWD/$lib timeout -k 10 200 python bench.py --no-cpu-baseline --no-legs --no-host-abi $AB_ARGS \
       > gpurun_out/ab/$(basename $lib .so)_$i.json 2>/dev/null || exit 1
   done
 done
