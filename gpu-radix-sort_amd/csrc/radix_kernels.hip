@@ -187,8 +187,8 @@ __device__ __forceinline__ uint64_t ballot_nz(uint32_t x) {
 // branch).  FULL: every lane holds a valid key (no predicate).  (A leader-only
 // ds_add_rtn + ds_bpermute variant, which lets the items' LDS round trips
 // overlap, cost 20-30 VGPRs and one wave/SIMD of occupancy and was slower.)
-template <int BITS, bool FULL, int ITEMS, typename K, typename Op>
-__device__ __forceinline__ void rank_items_t(const K (&k)[ITEMS], uint32_t (&rk)[ITEMS], uint32_t* row,
+template <int BITS, bool FULL, int ITEMS, typename K, typename Op, typename R>
+__device__ __forceinline__ void rank_items_t(const K (&k)[ITEMS], uint32_t (&rk)[ITEMS], R* row,
                                              uint32_t valid, uint32_t wbase, uint32_t lane, Op op) {
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
@@ -216,12 +216,12 @@ __device__ __forceinline__ void rank_items_t(const K (&k)[ITEMS], uint32_t (&rk)
     const uint32_t cnt = (uint32_t)(__builtin_popcount(plo) + __builtin_popcount(phi));
     const uint32_t base = row[d];
     rk[j] = base + below;
-    if (FULL || ok) row[d] = base + cnt;  // all peers write the same value
+    if (FULL || ok) row[d] = (R)(base + cnt);  // all peers write the same value
   }
 }
 
-template <int BITS, int ITEMS, typename K, typename Op>
-__device__ __forceinline__ void rank_items(const K (&k)[ITEMS], uint32_t (&rk)[ITEMS], uint32_t* row,
+template <int BITS, int ITEMS, typename K, typename Op, typename R>
+__device__ __forceinline__ void rank_items(const K (&k)[ITEMS], uint32_t (&rk)[ITEMS], R* row,
                                            bool full, uint32_t valid, uint32_t wbase, uint32_t lane,
                                            Op op) {
   if (full)
@@ -229,6 +229,14 @@ __device__ __forceinline__ void rank_items(const K (&k)[ITEMS], uint32_t (&rk)[I
   else
     rank_items_t<BITS, false, ITEMS>(k, rk, row, valid, wbase, lane, op);
 }
+
+// Per-wave digit counter of the tile pass: 16-bit (a wave ranks at most 1024
+// keys and the running offsets stay below the 8192-key tile), which keeps the
+// 8-bit pass's 8 x 256 counters at 4 KB (measured no slower than 32-bit ones
+// for 4- and 8-bit digits, tools/ab_c5.sh + tools/ab_libs.sh).
+using WaveCount = uint16_t;
+__device__ __forceinline__ uint32_t ob_base(uint32_t o) { return o; }
+__device__ __forceinline__ uint32_t ob_base(const uint2& o) { return o.x; }
 
 // Writes the locally sorted tile s_keys[0..valid) (and values) to global
 // memory: position i goes to outbase[digit] + i.  Full tiles are unrolled so
@@ -1006,8 +1014,9 @@ __device__ __forceinline__ uint32_t xcd_tile_of_block() {
 // digits: a run of one digit covers at most two destination tiles, so the
 // per-tile aggregate has 2 x RADIX x RADIX entries, laid out [slot][d][dn]:
 // a wave's sorted keys mostly share d and slot, so its LDS atomics spread
-// over consecutive dn banks).  The tile's row of C is zeroed after use (it
-// becomes the C_next of the pass after the next).
+// over consecutive dn banks).  FUSE: the tile's row of C is zeroed after use
+// (it becomes the C_next of the pass after the next); otherwise the count
+// kernel rewrites every row.
 #ifdef LIBSORT_TP_WAVES_PER_EU  // A/B knob: occupancy target of the pass kernel
 #define LS_TP_ATTR __attribute__((amdgpu_waves_per_eu(LIBSORT_TP_WAVES_PER_EU)))
 #else
@@ -1033,11 +1042,20 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   static_assert(RADIX <= BLOCK, "one digit per thread in the block phase");
   static_assert(!FUSE || (BITS == 4 && NEXT % BLOCK == 0), "fused next-pass counts: 4-bit digits");
 
+  // STAGE_V (pair tiles of 8192 64-bit keys): the values are not given LDS
+  // of their own; after the keys have been written to HBM they are scattered
+  // into the key buffer and written from there (LDS 69 KB per block instead
+  // of 101 KB: two blocks per CU).
+  constexpr bool STAGE_V = HAS_V && sizeof(K) == 8 && ITEMS == 16;
+  static_assert(!STAGE_V || (!FUSE && sizeof(VS) <= sizeof(K)), "staged values: 8-bit pair tiles");
+  // LDS per block (occupancy: 160 KiB per CU): the per-wave digit counters
+  // are 16-bit, and the destination-tile entries exist only for FUSE.
+  using OB = typename std::conditional<FUSE, uint2, uint32_t>::type;
   __shared__ K s_keys[TILE];
-  __shared__ VS s_vals[HAS_V ? TILE : 1];
-  __shared__ uint32_t s_whist[WAVES][RADIX];
-  __shared__ uint2 s_ob[RADIX];  // (run base - local start, local position where the run enters the next tile)
-  __shared__ uint32_t s_tfirst[RADIX];
+  __shared__ VS s_vals[HAS_V && !STAGE_V ? TILE : 1];
+  __shared__ WaveCount s_whist[WAVES][RADIX];
+  __shared__ OB s_ob[RADIX];  // run base - local start (FUSE: and the local position where the run enters the next tile)
+  __shared__ uint32_t s_tfirst[FUSE ? RADIX : 1];
   __shared__ uint32_t s_next[FUSE ? NEXT : 1];
   __shared__ uint32_t s_wsum[WAVES];
   __shared__ __attribute__((aligned(16))) uint8_t s_lut[OpLds<Op>::bytes];
@@ -1057,7 +1075,7 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   uint32_t gofs = 0;
   if (tid < RADIX) {
     gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid] + D[tid];
-    C[(size_t)t * RADIX + tid] = 0u;
+    if constexpr (FUSE) C[(size_t)t * RADIX + tid] = 0u;  // the C_next of the pass after the next
   }
 
   const uint64_t tile_base = (uint64_t)t * TILE;
@@ -1106,12 +1124,17 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 #pragma unroll
     for (int i = 0; i < WAVES; ++i) {
       const uint32_t c = s_whist[i][tid];
-      s_whist[i][tid] = run;
+      s_whist[i][tid] = (WaveCount)run;
       run += c;
     }
-    const uint32_t ob = gofs - excl, tf = gofs / TILE;
-    s_ob[tid] = make_uint2(ob, (tf + 1) * TILE - ob);
-    s_tfirst[tid] = tf;
+    const uint32_t ob = gofs - excl;
+    if constexpr (FUSE) {
+      const uint32_t tf = gofs / TILE;
+      s_ob[tid] = make_uint2(ob, (tf + 1) * TILE - ob);
+      s_tfirst[tid] = tf;
+    } else {
+      s_ob[tid] = ob;
+    }
   }
   __syncthreads();
 
@@ -1121,10 +1144,38 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
     if (ok) {
       const uint32_t pos = s_whist[w][op(k[j])] + rk[j];
       s_keys[pos] = k[j];
-      if constexpr (HAS_V) s_vals[pos] = v[j];
+      if constexpr (STAGE_V) rk[j] = pos;
+      else if constexpr (HAS_V) s_vals[pos] = v[j];
     }
   }
   __syncthreads();
+
+  if constexpr (STAGE_V) {
+    // keys (remembering each written position's run base), then the values
+    // through the same buffer
+    uint32_t obk[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t i = tid + j * BLOCK;
+      if (full || i < valid) {
+        const K kk = s_keys[i];
+        obk[j] = ob_base(s_ob[op(kk)]);
+        kout[obk[j] + i] = kk;
+      }
+    }
+    __syncthreads();
+    VS* s_v = reinterpret_cast<VS*>(s_keys);
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (full || wbase + j * kWave + lane < valid) s_v[rk[j]] = v[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t i = tid + j * BLOCK;
+      if (full || i < valid) vout[obk[j] + i] = s_v[i];
+    }
+    return;
+  }
 
   if (full) {
     // unrolled halves: the LDS reads of a half issue back to back, then its
@@ -1132,7 +1183,7 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 #pragma unroll
     for (int h = 0; h < SPLIT; ++h) {
       K kk[SP];
-      uint2 ob[SP];
+      OB ob[SP];
 #pragma unroll
       for (int j = 0; j < SP; ++j) kk[j] = s_keys[tid + (h * SP + j) * BLOCK];
 #pragma unroll
@@ -1140,8 +1191,8 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 #pragma unroll
       for (int j = 0; j < SP; ++j) {
         const uint32_t i = tid + (h * SP + j) * BLOCK;
-        kout[ob[j].x + i] = kk[j];
-        if constexpr (HAS_V) vout[ob[j].x + i] = s_vals[i];
+        kout[ob_base(ob[j]) + i] = kk[j];
+        if constexpr (HAS_V) vout[ob_base(ob[j]) + i] = s_vals[i];
       }
       if constexpr (FUSE) {
 #pragma unroll
@@ -1164,9 +1215,9 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
     for (uint32_t i = tid; i < valid; i += BLOCK) {
       const K kk = s_keys[i];
       const uint32_t d = op(kk);
-      const uint2 ob = s_ob[d];
-      kout[ob.x + i] = kk;
-      if constexpr (HAS_V) vout[ob.x + i] = s_vals[i];
+      const OB ob = s_ob[d];
+      kout[ob_base(ob) + i] = kk;
+      if constexpr (HAS_V) vout[ob_base(ob) + i] = s_vals[i];
       if constexpr (FUSE) {
         const uint32_t slot = i >= ob.y ? (uint32_t)(RADIX * RADIX) : 0u;
         atomicAdd(&s_next[slot + d * RADIX + op_next(kk)], 1u);
@@ -2026,8 +2077,18 @@ int choose_algorithm(size_t n, int bits) {
 // the next pass's counts fused into the pass kernel.  8-bit digits: 512-thread
 // tiles of 8192 keys (longer digit runs, fewer count rows) and a separate
 // per-tile count kernel per pass.
-template <typename K>
-constexpr int tp_items() { return sizeof(K) == 8 ? 8 : 16; }
+// Pairs with 64-bit keys at 8-bit digits: 512 x 16 tiles (8192 pairs, 32-pair
+// runs), their values staged through the key buffer after the keys are
+// written (k_tile_pass STAGE_V).  A compute-free skeleton of the pair scatter
+// (tools/run_probe, 2^28 pairs) runs 1219 us with 16-pair runs and 1096 us
+// with 32-pair runs.  LIBSORT_TP8_PAIR_ITEMS=8 keeps the 4096-pair tiles.
+#ifndef LIBSORT_TP8_PAIR_ITEMS
+#define LIBSORT_TP8_PAIR_ITEMS 16
+#endif
+template <typename K, typename V = NoValue>
+constexpr int tp_items(int bits) {
+  return sizeof(K) != 8 ? 16 : (bits == 8 && !std::is_same<V, NoValue>::value) ? LIBSORT_TP8_PAIR_ITEMS : 8;
+}
 #ifndef LIBSORT_TP8_BLOCK
 #define LIBSORT_TP8_BLOCK 512  // threads of an 8-bit tile (16 keys each)
 #endif
@@ -2041,9 +2102,9 @@ template <typename K>
 constexpr int tp_block(int bits) {
   return bits == 4 ? LIBSORT_TP4_BLOCK : (sizeof(K) == 8 ? LIBSORT_TP8_BLOCK64 : LIBSORT_TP8_BLOCK);
 }
-template <typename K>
+template <typename K, typename V = NoValue>
 uint32_t tp_tiles(size_t n, int bits) {
-  const uint64_t t = (uint64_t)tp_block<K>(bits) * tp_items<K>();
+  const uint64_t t = (uint64_t)tp_block<K>(bits) * tp_items<K, V>(bits);
   return (uint32_t)((n + t - 1) / t);
 }
 inline uint32_t tp_chunks(uint32_t tiles, int bits) {
@@ -2051,7 +2112,7 @@ inline uint32_t tp_chunks(uint32_t tiles, int bits) {
   return (tiles + ch - 1) / ch;
 }
 
-template <int BITS, typename K, typename Op = RadixDigit>
+template <int BITS, typename K, typename Op = RadixDigit, typename V = NoValue>
 hipError_t tiles_counts(Workspace& ws, const K* in, size_t n, Op op, uint32_t tiles, uint32_t* C,
                         uint32_t* zero, uint32_t zero_words, hipStream_t st) {
   // the same tiles as the pass kernel, a different block shape: 4-bit u32
@@ -2059,8 +2120,8 @@ hipError_t tiles_counts(Workspace& ws, const K* in, size_t n, Op op, uint32_t ti
   // interleaved A/B; the pass itself is faster as 256 x 16)
   constexpr int B = tp_block<K>(BITS);
   constexpr int CB = (BITS == 4 && sizeof(K) == 4) ? 512 : B;
-  constexpr int CI = B * tp_items<K>() / CB;
-  static_assert(CB * CI == B * tp_items<K>(), "count tiles = pass tiles");
+  constexpr int CI = B * tp_items<K, V>(BITS) / CB;
+  static_assert(CB * CI == B * tp_items<K, V>(BITS), "count tiles = pass tiles");
   ScopedTimer tm("tilecounts", st, n);
   hipLaunchKernelGGL((k_tile_counts<BITS, CB, CI, K, Op>), dim3(tiles), dim3(CB), 0, st, in, (uint32_t)n, op, C, zero,
                      zero_words);
@@ -2089,15 +2150,15 @@ hipError_t tiles_colscan(Workspace& ws, uint32_t* C, uint32_t tiles, hipStream_t
 }
 
 // Sort prologue of the tile path: buffers, and (4-bit) the pass-0 counts.
-template <typename K, typename Op = RadixDigit>
+template <typename K, typename V, typename Op = RadixDigit>
 hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, int bits, hipStream_t st,
                           uint32_t bias = 0) {
-  const uint32_t tiles = tp_tiles<K>(n, bits);
+  const uint32_t tiles = tp_tiles<K, V>(n, bits);
   const uint32_t radix = 1u << bits;
   LS_TRY(ws.ensure_tiles((size_t)tiles * radix, ((size_t)tp_chunks(tiles, bits) + 1) * radix));
   if (bits != 4) return hipSuccess;
   const int nb = std::min(4, hi - lo);
-  return tiles_counts<4, K, Op>(ws, in, n, make_digit<Op>((uint32_t)lo, (1u << nb) - 1u, bias), tiles, ws.tc[0],
+  return tiles_counts<4, K, Op, V>(ws, in, n, make_digit<Op>((uint32_t)lo, (1u << nb) - 1u, bias), tiles, ws.tc[0],
                                 ws.tc[1], tiles * 16u, st);
 }
 
@@ -2105,7 +2166,7 @@ template <int BITS, typename K, typename V, typename Op = RadixDigit>
 hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout, size_t n, int p, int P,
                       int lo, int hi, hipStream_t st, uint32_t bias = 0) {
   constexpr int B = tp_block<K>(BITS);
-  const uint32_t tiles = tp_tiles<K>(n, BITS);
+  const uint32_t tiles = tp_tiles<K, V>(n, BITS);
   const int shift = lo + BITS * p;
   const int nb = std::min(BITS, hi - shift);
   const Op op = make_digit<Op>((uint32_t)shift, (1u << nb) - 1u, bias);
@@ -2120,18 +2181,18 @@ hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vou
   uint32_t* cur = fused_counts ? ws.tc[p & 1] : ws.tc[0];
   uint32_t* nxt = ws.tc[(p + 1) & 1];
   if (!fused_counts && !(BITS == 4 && p == 0))
-    LS_TRY((tiles_counts<BITS, K, Op>(ws, kin, n, op, tiles, cur, nullptr, 0, st)));
+    LS_TRY((tiles_counts<BITS, K, Op, V>(ws, kin, n, op, tiles, cur, nullptr, 0, st)));
   LS_TRY(tiles_colscan<BITS>(ws, cur, tiles, st));
   const bool fuse = fused_counts && p + 1 < P;
   const int nb2 = fuse ? std::min(BITS, hi - shift - BITS) : 1;
   const Op op_next = make_digit<Op>((uint32_t)(fuse ? shift + BITS : 0), (1u << nb2) - 1u, bias);
   ScopedTimer tm("tilepass", st, n);
   if (fuse)
-    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, BITS == 4, Op, Op>), dim3(tiles), dim3(B), 0, st,
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K, V>(BITS), K, V, BITS == 4, Op, Op>), dim3(tiles), dim3(B), 0, st,
                        kin, kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, tiles_digit_starts(ws, tiles, BITS),
                        nxt);
   else
-    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, false, Op, Op>), dim3(tiles), dim3(B), 0, st, kin,
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K, V>(BITS), K, V, false, Op, Op>), dim3(tiles), dim3(B), 0, st, kin,
                        kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, tiles_digit_starts(ws, tiles, BITS),
                        nxt);
   return hipGetLastError();
@@ -2247,9 +2308,9 @@ hipError_t sort_impl(Workspace& ws, const K* in, K* out, K* tmp, const V* vin, V
   const uint32_t tiles = (uint32_t)((n + OS_TILE - 1) / OS_TILE);
   if (os) LS_TRY(onesweep_prologue<K>(ws, in, n, lo, hi, bits, P, tiles, st));
   if (tp && bias) {
-    if constexpr (kCanBias) LS_TRY((tiles_prologue<K, BiasedDigit>(ws, in, n, lo, hi, bits, st, bias)));
+    if constexpr (kCanBias) LS_TRY((tiles_prologue<K, V, BiasedDigit>(ws, in, n, lo, hi, bits, st, bias)));
   } else if (tp) {
-    LS_TRY(tiles_prologue<K>(ws, in, n, lo, hi, bits, st));
+    LS_TRY((tiles_prologue<K, V>(ws, in, n, lo, hi, bits, st)));
   }
   for (int p = 0; p < P; ++p) {
     const int shift = lo + p * bits;
@@ -2452,7 +2513,7 @@ hipError_t partition_lut_impl(Workspace& ws, const K* in, K* out, const V* vin, 
   ws.part_pending.valid = false;
   {
     ScopedTimer tm("partition", st, n);
-    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(), K, V, false, LutDigit>), dim3(tiles), dim3(B), 0, st, in,
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(BITS), K, V, false, LutDigit>), dim3(tiles), dim3(B), 0, st, in,
                        out, vin, vout, (uint32_t)n, op, RadixDigit{0u, 1u}, ws.tc[0], (const uint32_t*)ws.tb,
                        (const uint32_t*)tiles_digit_starts(ws, tiles, BITS), ws.tc[1]);
     LS_TRY(hipGetLastError());
