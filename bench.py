@@ -215,7 +215,7 @@ def main():
     # live per-kernel durations (hipEvents on libsort's launch stream)
     kern = {}
     for name in ("whist", "onesweep", "upsweep", "scan", "downsweep", "tilecounts", "colscan", "tilepass",
-                 "partition", "histogram", "segcopy"):
+                 "hybplan", "bucketsort", "partition", "histogram", "segcopy"):
         launches, ms, kk = D.timing_query(name)
         if launches:
             kern[name] = {"launches": launches, "avg_us": 1e3 * ms / launches, "keys_per_launch": kk / launches}

@@ -330,6 +330,20 @@ static int env_boundary_mode() {
 }
 static std::atomic<int> g_boundary_mode{env_boundary_mode()};
 
+// MSD hybrid for full 32-bit key sorts (sort_hybrid_u32): 0 = off, 1 = auto
+// (2^27 <= n <= 2^28 + 2^24), 2 = every full sort of n >= 1024 keys (tests).
+// Initial value from LIBSORT_HYBRID (0 / 1 / 2; default 1).
+static int env_hybrid() {
+  const char* s = getenv("LIBSORT_HYBRID");
+  return (s && s[0] >= '0' && s[0] <= '2') ? s[0] - '0' : 1;
+}
+static std::atomic<int> g_hybrid{env_hybrid()};
+int get_hybrid_mode() { return g_hybrid.load(std::memory_order_relaxed); }
+int set_hybrid_mode(int m) {
+  if (m < 0 || m > 2) return -1;
+  return g_hybrid.exchange(m);
+}
+
 int get_algorithm() { return g_algorithm.load(std::memory_order_relaxed); }
 int set_algorithm(int a) {
   if (a < 0 || a > 3) return -1;
@@ -1025,6 +1039,7 @@ LIBSORT_EXPORT int libsortSetDigitBits(int bits) {
 LIBSORT_EXPORT int libsortGetDigitBits(void) { return g_digit_bits.load(); }
 
 LIBSORT_EXPORT int libsortSetAlgorithm(int algo) { return set_algorithm(algo); }
+LIBSORT_EXPORT int libsortSetHybrid(int mode) { return set_hybrid_mode(mode); }
 
 LIBSORT_EXPORT int libsortSetBoundaryMode(int mode) {
   if (mode != 0 && mode != 1) return -1;

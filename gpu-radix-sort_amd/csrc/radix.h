@@ -110,6 +110,14 @@ struct Workspace {
   PartToken part_pending{nullptr, nullptr, 0, nullptr, 0, 0, nullptr, false};
   hipError_t ensure_tiles(size_t count_words, size_t chunk_words);
 
+  // MSD hybrid (sort_hybrid_u32): tile tables, per-segment run bases and
+  // child tables of two depths, counters; a pinned mirror for the host checks
+  uint32_t* hyb = nullptr;
+  size_t hyb_cap = 0;  // words
+  uint32_t* hyb_host = nullptr;  // pinned, 256 words
+  hipEvent_t hyb_evt = nullptr;
+  hipError_t ensure_hybrid(size_t words);
+
   hipError_t ensure_counts(size_t m);
   hipError_t ensure_hbuf(size_t bytes);
   hipError_t ensure_bounds(size_t m);
@@ -153,6 +161,10 @@ hipError_t sort_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t
 // "rts" / "tiles").
 int get_algorithm();
 int set_algorithm(int algo);  // returns the previous value, -1 if invalid
+// MSD hybrid for full 32-bit key sorts: 0 = off, 1 = auto (2^27 <= n <=
+// 2^28 + 2^24), 2 = every full sort of n >= 1024 keys.  LIBSORT_HYBRID.
+int get_hybrid_mode();
+int set_hybrid_mode(int mode);
 
 // Host-side choice of the ping-pong pair for the host ABI: returns true when
 // the result of a `passes`-pass sort started from hbuf[0] lands in hbuf[1].

@@ -27,6 +27,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cmath>
 #include <type_traits>
 
 namespace lsort {
@@ -787,10 +788,14 @@ constexpr int col_chunk_rows(int radix) { return radix >= 256 ? LIBSORT_COL_ROWS
 
 // Per-tile digit counts of the first pass; also zeroes `zero_buf` (the
 // next-pass count buffer).  One block per tile.
-template <int BITS, int BLOCK, int ITEMS, typename K, typename Op = RadixDigit>
+// TAB: the tiles of an MSD hybrid depth (tiles[t] = first key, keys; rows of
+// blocks past *ntiles are written as zeros: the column scan covers the grid).
+template <int BITS, int BLOCK, int ITEMS, typename K, typename Op = RadixDigit, bool TAB = false>
 __global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ keys, uint32_t n, Op op_in,
                                                        uint32_t* __restrict__ counts,
-                                                       uint32_t* __restrict__ zero_buf, uint32_t zero_words) {
+                                                       uint32_t* __restrict__ zero_buf, uint32_t zero_words,
+                                                       const uint4* __restrict__ tiles,
+                                                       const uint32_t* __restrict__ ntiles) {
   constexpr int RADIX = 1 << BITS;
   constexpr int TILE = BLOCK * ITEMS;
   constexpr int COPIES = RADIX <= 16 ? 16 : 1;  // spread same-digit LDS atomics
@@ -803,11 +808,22 @@ __global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ key
     zero_buf[i] = 0u;
   __syncthreads();
   const uint32_t cp = tid % COPIES;
-  const uint64_t tile_base = (uint64_t)blockIdx.x * TILE;
-  const uint32_t valid = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tile_base);
+  uint64_t tile_base = (uint64_t)blockIdx.x * TILE;
+  uint32_t valid;
+  if constexpr (TAB) {
+    if (blockIdx.x < *ntiles) {
+      const uint4 te = tiles[blockIdx.x];
+      tile_base = te.x;
+      valid = te.y;
+    } else {
+      valid = 0;
+    }
+  } else {
+    valid = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tile_base);
+  }
   using VT = typename VecOf<K>::type;
   constexpr int PER = VecOf<K>::n;
-  if (valid == TILE && (reinterpret_cast<uintptr_t>(keys) % 16) == 0) {
+  if (valid == TILE && (reinterpret_cast<uintptr_t>(keys + tile_base) % 16) == 0) {
     const VT* vp = reinterpret_cast<const VT*>(keys + tile_base);
     VT v[ITEMS / PER];
 #pragma unroll
@@ -1008,6 +1024,19 @@ __device__ __forceinline__ uint32_t xcd_tile_of_block() {
   return x * q + min(x, r) + i;
 }
 
+// Tile geometry of the MSD hybrid (sort_hybrid_u32): at depth k >= 1 the
+// tiles are cut per segment (the keys sharing their top 4k or 8k bits), so
+// tile t = tiles[t] = (first key, keys, segment); the run offsets of segment s
+// are D[s * RADIX + d] + the column prefix; and the fused next-digit counts
+// go to the next depth's tiles, cut the same way per child (segment * RADIX +
+// digit): child c starts at ncstart[c] and its first tile is nctile0[c].
+struct HybridGeo {
+  const uint4* tiles;        // GEO & 1: this depth's tile table
+  const uint32_t* ntiles;    // GEO & 1: this depth's tile count (blocks past it exit)
+  const uint32_t* ncstart;   // GEO & 2: next depth's child starts
+  const uint32_t* nctile0;   // GEO & 2: next depth's first tile per child
+};
+
 // The pass kernel of the tile-offset path: the onesweep tile body with the
 // run offsets read from the scanned counts.  FUSE: also count the next digit
 // (op_next) of every written key per destination tile into C_next (4-bit
@@ -1023,12 +1052,13 @@ __device__ __forceinline__ uint32_t xcd_tile_of_block() {
 #define LS_TP_ATTR
 #endif
 template <int BITS, int BLOCK, int ITEMS, typename K, typename V, bool FUSE, typename Op = RadixDigit,
-          typename OpN = RadixDigit>
+          typename OpN = RadixDigit, int GEO = 0>
 __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restrict__ kin, K* __restrict__ kout,
                                                      const V* __restrict__ vin, V* __restrict__ vout,
                                                      uint32_t n, Op op_in, OpN op_next,
                                                      uint32_t* __restrict__ C, const uint32_t* __restrict__ B,
-                                                     const uint32_t* __restrict__ D, uint32_t* __restrict__ C_next) {
+                                                     const uint32_t* __restrict__ D, uint32_t* __restrict__ C_next,
+                                                     HybridGeo geo) {
   constexpr bool HAS_V = !std::is_same<V, NoValue>::value;
   using VS = typename std::conditional<HAS_V, V, uint8_t>::type;
   constexpr int RADIX = 1 << BITS;
@@ -1064,6 +1094,18 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   const int lane = tid & (kWave - 1);
   const int w = tid / kWave;
   const uint32_t t = xcd_tile_of_block();
+  uint64_t tile_base;
+  uint32_t valid, seg = 0;
+  if constexpr ((GEO & 1) != 0) {
+    if (t >= *geo.ntiles) return;  // past this depth's tiles (the grid is a bound)
+    const uint4 te = geo.tiles[t];
+    tile_base = te.x;
+    valid = te.y;
+    seg = te.z;
+  } else {
+    tile_base = (uint64_t)t * TILE;
+    valid = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tile_base);
+  }
   const Op op = bind_op(op_in, s_lut, tid, BLOCK);
   if constexpr (OpLds<Op>::bytes > 1) __syncthreads();
   for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0u;
@@ -1074,12 +1116,9 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   // this tile's run offsets (independent of every other tile)
   uint32_t gofs = 0;
   if (tid < RADIX) {
-    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid] + D[tid];
+    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid] + D[(size_t)seg * RADIX + tid];
     if constexpr (FUSE) C[(size_t)t * RADIX + tid] = 0u;  // the C_next of the pass after the next
   }
-
-  const uint64_t tile_base = (uint64_t)t * TILE;
-  const uint32_t valid = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tile_base);
   const bool full = valid == TILE;
   const uint32_t wbase = w * WSPAN;
 
@@ -1128,7 +1167,14 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
       run += c;
     }
     const uint32_t ob = gofs - excl;
-    if constexpr (FUSE) {
+    if constexpr (FUSE && (GEO & 2) != 0) {
+      // next depth's tiles are cut per child: position p of child c is in
+      // tile nctile0[c] + (p - ncstart[c]) / TILE
+      const uint32_t c = seg * RADIX + tid, cs = geo.ncstart[c];
+      const uint32_t tl = (gofs - cs) / TILE;
+      s_ob[tid] = make_uint2(ob, cs + (tl + 1) * TILE - ob);
+      s_tfirst[tid] = geo.nctile0[c] + tl;
+    } else if constexpr (FUSE) {
       const uint32_t tf = gofs / TILE;
       s_ob[tid] = make_uint2(ob, (tf + 1) * TILE - ob);
       s_tfirst[tid] = tf;
@@ -1236,6 +1282,220 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
       }
     }
   }
+}
+
+// ============================================================================
+// Bucket sort: the last level of the MSD hybrid (DESIGN.md §3 "MSD passes +
+// bucket sort").  Block b sorts bucket b (bstart[b], blen[b] <= BLOCK*ITEMS
+// keys that share every bit above `lbits`) entirely on chip: the keys are
+// loaded once into registers, then each BITS-bit LSD step over bits
+// [0, lbits) is a stable wave64 ballot rank (rank_items_t), a block scan of
+// the digit counts and an LDS scatter, read back in item order; the sorted
+// bucket is written out coalesced.  One HBM read and one write per key for
+// the low lbits bits instead of lbits/BITS digit passes.  Slots past the end
+// of the bucket hold 0xffffffff: they are last in item order and carry the
+// largest digit, so every step keeps them behind the real keys and the steps
+// run without predicates.  Grid: an upper bound of buckets; *nb is the
+// bucket count.  A bucket larger than the block is left alone and counted in
+// *oversized (the caller then sorts those keys another way).  in may equal
+// out (a block holds its whole bucket before it writes).
+template <int BITS, int BLOCK, int ITEMS>
+__global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* in, uint32_t* out,
+                                                       const uint32_t* __restrict__ bstart,
+                                                       const uint32_t* __restrict__ blen,
+                                                       const uint32_t* __restrict__ nb, uint32_t lbits,
+                                                       uint32_t* __restrict__ oversized) {
+  constexpr int RADIX = 1 << BITS;
+  constexpr int WAVES = BLOCK / kWave;
+  constexpr int CAP = BLOCK * ITEMS;
+  constexpr int WSPAN = ITEMS * kWave;
+  static_assert(RADIX <= BLOCK && CAP < 65536, "one digit per thread; 16-bit wave counters");
+  __shared__ uint32_t s_keys[CAP];
+  __shared__ WaveCount s_whist[WAVES][RADIX];
+  __shared__ WaveCount s_off[RADIX <= kWave ? WAVES : 1][RADIX];
+  __shared__ uint32_t s_wsum[WAVES];
+  if (blockIdx.x >= *nb) return;
+  const uint32_t start = bstart[blockIdx.x], len = blen[blockIdx.x];
+  if (len > (uint32_t)CAP) {
+    if (threadIdx.x == 0) atomicAdd(oversized, 1u);
+    return;
+  }
+  if (len == 0) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int w = tid / kWave;
+  const uint32_t wbase = w * WSPAN;
+  uint32_t k[ITEMS], rk[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t i = wbase + j * kWave + lane;
+    k[j] = i < len ? load_stream(&in[(size_t)start + i]) : 0xffffffffu;
+  }
+  for (uint32_t shift = 0; shift < lbits; shift += BITS) {
+    const uint32_t nbits = min((uint32_t)BITS, lbits - shift);
+    const RadixDigit op{shift, (1u << nbits) - 1u};
+    for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0;
+    rank_items_t<BITS, true, ITEMS>(k, rk, s_whist[w], 0u, wbase, lane, op);
+    __syncthreads();
+    if constexpr (RADIX <= kWave) {
+      // every wave derives its own run offsets (lane d: the digit-d keys of
+      // all waves for smaller digits, plus those of earlier waves): no
+      // block scan, two barriers per step
+      uint32_t col = 0, mine = 0;
+      if (lane < RADIX) {
+#pragma unroll
+        for (int i = 0; i < WAVES; ++i) {
+          const uint32_t c = s_whist[i][lane];
+          col += c;
+          mine += i < w ? c : 0u;
+        }
+      }
+      uint32_t x = col;
+#pragma unroll
+      for (int o = 1; o < RADIX; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, RADIX);
+        if ((lane & (RADIX - 1)) >= o) x += y;
+      }
+      if (lane < RADIX) s_off[w][lane] = (WaveCount)(x - col + mine);
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) s_keys[s_off[w][op(k[j])] + rk[j]] = k[j];
+    } else {
+      uint32_t cnt_d = 0;
+      if (tid < RADIX) {
+#pragma unroll
+        for (int i = 0; i < WAVES; ++i) cnt_d += s_whist[i][tid];
+      }
+      uint32_t total;
+      const uint32_t excl = block_exclusive_scan<BLOCK>(cnt_d, s_wsum, total);
+      if (tid < RADIX) {
+        uint32_t run = excl;
+#pragma unroll
+        for (int i = 0; i < WAVES; ++i) {
+          const uint32_t c = s_whist[i][tid];
+          s_whist[i][tid] = (WaveCount)run;
+          run += c;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) s_keys[s_whist[w][op(k[j])] + rk[j]] = k[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) k[j] = s_keys[wbase + j * kWave + lane];
+  }
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t i = wbase + j * kWave + lane;
+    if (i < len) out[(size_t)start + i] = k[j];
+  }
+}
+
+// MSD hybrid planning (sort_hybrid_u32).  After the column scan of depth k
+// (per-tile counts C' chunk-local, chunk prefixes B, digit starts D over all
+// `rows` scanned rows), one thread per child (segment s, digit d):
+//   P(t, d) = C'[t][d] + B[t / CH][d]  (the digit-d keys in tiles < t; the
+//             column total past the last row),
+//   size    = P(t1, d) - P(t0, d) over the segment's tiles [t0, t1),
+//   start   = cstart[s] + the sizes of digits < d in s,
+//   segbase[s][d] = start - P(t0, d)  (the pass adds P(t, d): the run of
+//             tile t lands at start + the digit-d keys of the earlier tiles
+//             of its segment),
+// and the child's start, size and tile count for the next depth.  Depth 0
+// (fixed tiles) has one segment, tiles [0, fixed_tiles), starting at 0.
+template <int RADIX, int TILE>
+__global__ __launch_bounds__(256) void k_hyb_children(const uint32_t* __restrict__ C, const uint32_t* __restrict__ B,
+                                                      const uint32_t* __restrict__ D, uint32_t rows, uint32_t nkeys,
+                                                      uint32_t nseg, const uint32_t* __restrict__ ctile0,
+                                                      const uint32_t* __restrict__ cstart, uint32_t fixed_tiles,
+                                                      uint32_t* __restrict__ segbase, uint32_t* __restrict__ ncstart,
+                                                      uint32_t* __restrict__ nsize, uint32_t* __restrict__ ntl) {
+  static_assert(RADIX == 16 || RADIX == 256, "4- or 8-bit digits");
+  constexpr int CH = col_chunk_rows(RADIX);
+  __shared__ uint32_t s_wsum[4];
+  const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+  const uint32_t seg = g / RADIX, d = g % RADIX;
+  const bool live = seg < nseg;
+  uint32_t t0 = 0, t1 = fixed_tiles, cs = 0;
+  if (ctile0 && live) {
+    t0 = ctile0[seg];
+    t1 = ctile0[seg + 1];
+    cs = cstart[seg];
+  }
+  const uint32_t total = (d + 1 < (uint32_t)RADIX ? D[d + 1] : nkeys) - D[d];
+  auto P = [&](uint32_t t) -> uint32_t {
+    return t < rows ? C[(size_t)t * RADIX + d] + B[(size_t)(t / CH) * RADIX + d] : total;
+  };
+  const uint32_t p0 = live ? P(t0) : 0u;
+  const uint32_t size = (live && t1 > t0) ? P(t1) - p0 : 0u;
+  uint32_t excl;
+  if constexpr (RADIX == 16) {
+    const uint32_t l = threadIdx.x & 15u;
+    uint32_t x = size;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 16);
+      if (l >= (uint32_t)o) x += y;
+    }
+    excl = x - size;
+  } else {
+    uint32_t tot;
+    excl = block_exclusive_scan<256>(size, s_wsum, tot);
+  }
+  if (!live) return;
+  const uint32_t start = cs + excl;
+  segbase[g] = start - p0;
+  ncstart[g] = start;
+  nsize[g] = size;
+  if (ntl) ntl[g] = (size + TILE - 1) / TILE;
+}
+
+// Exclusive scan of the children's tile counts (one block): ctile0[0..m],
+// ctile0[m] = *total = the next depth's tile count.
+__global__ __launch_bounds__(1024) void k_hyb_tile_prefix(const uint32_t* __restrict__ ntl, uint32_t m,
+                                                          uint32_t* __restrict__ ctile0, uint32_t* __restrict__ total) {
+  __shared__ uint32_t s_wsum[16];
+  const uint32_t per = (m + 1023) / 1024;
+  const uint32_t a = threadIdx.x * per, b = min(m, a + per);
+  uint32_t sum = 0;
+  for (uint32_t i = a; i < b; ++i) sum += ntl[i];
+  uint32_t tot;
+  uint32_t run = block_exclusive_scan<1024>(sum, s_wsum, tot);
+  for (uint32_t i = a; i < b; ++i) {
+    const uint32_t v = ntl[i];
+    ctile0[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 0) {
+    ctile0[m] = tot;
+    *total = tot;
+  }
+}
+
+// The next depth's tile table: tile t belongs to the child c with
+// ctile0[c] <= t < ctile0[c + 1] (binary search; empty children have no
+// tiles); rows [0, bound) of Czero (its fused counts) are zeroed.
+template <int RADIX, int TILE>
+__global__ __launch_bounds__(256) void k_hyb_expand(const uint32_t* __restrict__ ctile0, uint32_t m,
+                                                    const uint32_t* __restrict__ ncstart,
+                                                    const uint32_t* __restrict__ nsize,
+                                                    const uint32_t* __restrict__ ntiles, uint32_t bound,
+                                                    uint4* __restrict__ tiles, uint32_t* __restrict__ Czero) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= bound) return;
+  if (Czero) {
+#pragma unroll
+    for (int q = 0; q < RADIX; q += 4)
+      *reinterpret_cast<uint4*>(&Czero[(size_t)t * RADIX + q]) = make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (t >= *ntiles) return;
+  uint32_t lo = 0, hi = m;  // largest c with ctile0[c] <= t
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (ctile0[mid] <= t) lo = mid; else hi = mid;
+  }
+  const uint32_t k = t - ctile0[lo];
+  tiles[t] = make_uint4(ncstart[lo] + k * TILE, min((uint32_t)TILE, nsize[lo] - k * TILE), lo, 0u);
 }
 
 // bounds[g] = exclusive scan of window 0 (the whole group when width <= 8).
@@ -1952,6 +2212,17 @@ hipError_t Workspace::ensure_tiles(size_t count_words, size_t chunk_words) {
   return hipSuccess;
 }
 
+hipError_t Workspace::ensure_hybrid(size_t words) {
+  if (!hyb_evt) LS_TRY(hipEventCreateWithFlags(&hyb_evt, hipEventDisableTiming));
+  if (!hyb_host) LS_TRY(hipHostMalloc(&hyb_host, 256 * sizeof(uint32_t), hipHostMallocDefault));
+  if (words <= hyb_cap) return hipSuccess;
+  if (hyb) { (void)hipFree(hyb); hyb = nullptr; }
+  hyb_cap = 0;
+  LS_TRY(hipMalloc(&hyb, words * sizeof(uint32_t)));
+  hyb_cap = words;
+  return hipSuccess;
+}
+
 hipError_t Workspace::ensure_onesweep(size_t status_words) {
   if (!os_small) {
     LS_TRY(hipMalloc(&os_small, kOsSmallWords * sizeof(uint32_t)));
@@ -1983,6 +2254,10 @@ void Workspace::release() {
     if (p) (void)hipFree(p);
   tc[0] = tc[1] = tb = tticket = nullptr;
   tc_cap = tb_cap = 0;
+  if (hyb) (void)hipFree(hyb);
+  if (hyb_host) (void)hipHostFree(hyb_host);
+  hyb = hyb_host = nullptr;
+  hyb_cap = 0;
   os_status_cap = 0;
   if (seg_host) (void)hipHostFree(seg_host);
   if (copy_stream) (void)hipStreamSynchronize(copy_stream);
@@ -2124,7 +2399,7 @@ hipError_t tiles_counts(Workspace& ws, const K* in, size_t n, Op op, uint32_t ti
   static_assert(CB * CI == B * tp_items<K, V>(BITS), "count tiles = pass tiles");
   ScopedTimer tm("tilecounts", st, n);
   hipLaunchKernelGGL((k_tile_counts<BITS, CB, CI, K, Op>), dim3(tiles), dim3(CB), 0, st, in, (uint32_t)n, op, C, zero,
-                     zero_words);
+                     zero_words, nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -2190,11 +2465,11 @@ hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vou
   if (fuse)
     hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K, V>(BITS), K, V, BITS == 4, Op, Op>), dim3(tiles), dim3(B), 0, st,
                        kin, kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, tiles_digit_starts(ws, tiles, BITS),
-                       nxt);
+                       nxt, HybridGeo{});
   else
     hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K, V>(BITS), K, V, false, Op, Op>), dim3(tiles), dim3(B), 0, st, kin,
                        kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, tiles_digit_starts(ws, tiles, BITS),
-                       nxt);
+                       nxt, HybridGeo{});
   return hipGetLastError();
 }
 
@@ -2370,11 +2645,190 @@ hipError_t group_bounds(Workspace& ws, const uint32_t* sorted, size_t n, int lo,
   return hipGetLastError();
 }
 
+// ----------------------------------------------------------------------------
+// MSD hybrid for full 32-bit sorts of uint32 keys (DESIGN.md §3 "MSD passes +
+// bucket sort"): DEPTHS = 16 / BITS digit passes from the TOP digit down,
+// each a stable partition of every segment (keys sharing the digits above) by
+// its next digit, cut into segment-aligned tiles; then every one of the 2^16
+// buckets (keys sharing their top 16 bits, ~n / 65536 keys) is sorted on its
+// low 16 bits on chip by k_bucket_sort.  HBM passes: DEPTHS + 1 instead of
+// 32 / BITS.  Keys only: order among equal keys is not observable.
+// Buffers: depth k reads buf[k] and writes buf[k + 1] with buf[0] = in,
+// buf[odd] = tmp, buf[even > 0] = out; DEPTHS is even, so the buckets are
+// sorted in place in out.
+// Host checks (the stream is synchronised twice, without idling the GPU):
+// after the first column scan, a top digit holding more than 1.5 n / RADIX
+// keys (a skewed input, buckets would overflow) abandons the hybrid
+// (*handled = false: the caller runs the LSD sort; in is untouched); after
+// the bucket sort, buckets too large for a block (counted on the device) are
+// sorted by an LSD sort of out in place.
+constexpr size_t kHybMinKeys = 1ull << 27;
+constexpr size_t kHybMaxKeys = (1ull << 28) + (1ull << 24);
+
+
+template <int BITS>
+hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n, hipStream_t st,
+                           bool* handled) {
+  constexpr int RADIX = 1 << BITS;
+  constexpr int B = tp_block<uint32_t>(BITS);
+  constexpr int TILE = B * 16;
+  constexpr int DEPTHS = 16 / BITS;
+  static_assert(DEPTHS % 2 == 0, "the last depth writes out");
+  constexpr uint32_t NB = 1u << 16;  // buckets
+  *handled = false;
+  constexpr int kSmallItems = 10, kLargeItems = 19;  // bucket-sort blocks: 256 x items keys
+  const bool small = n <= (1ull << 27) + (1ull << 23);
+  const uint32_t cap = 256u * (small ? kSmallItems : kLargeItems);
+  const uint32_t T0 = (uint32_t)((n + TILE - 1) / TILE);
+  auto tbound = [&](int k) { return k == 0 ? T0 : T0 + (1u << (BITS * k)); };
+  const uint32_t TB = tbound(DEPTHS - 1);
+  LS_TRY(ws.ensure_tiles((size_t)TB * RADIX, ((size_t)tp_chunks(TB, BITS) + 1) * RADIX));
+  // hybrid block: tiles[2] | segbase | cstart[2] | nsize | ctile0[2] | ntl | counters
+  const size_t w_tiles = (size_t)TB * 4;
+  const size_t words = 2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16;
+  LS_TRY(ws.ensure_hybrid(words));
+  uint32_t* h = ws.hyb;
+  uint4* tiles[2] = {reinterpret_cast<uint4*>(h), reinterpret_cast<uint4*>(h + w_tiles)};
+  h += 2 * w_tiles;
+  uint32_t* segbase = h; h += NB;
+  uint32_t* cstart[2] = {h, h + NB}; h += 2 * (size_t)NB;
+  uint32_t* nsize = h; h += NB;
+  uint32_t* ctile0[2] = {h, h + NB + 1}; h += 2 * ((size_t)NB + 1);
+  uint32_t* ntl = h; h += NB;
+  uint32_t* ctr = h;  // [k] tiles of depth k, [8] oversized buckets, [9] bucket count
+  LS_TRY(hipMemsetAsync(ctr, 0, 16 * sizeof(uint32_t), st));
+  LS_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctr + 9), (int)NB, 1, st));
+  ws.part_pending.valid = false;
+
+  auto buf = [&](int k) -> uint32_t* { return k == 0 ? const_cast<uint32_t*>(in) : (k & 1) ? tmp : out; };
+  for (int k = 0; k < DEPTHS; ++k) {
+    const bool last = k == DEPTHS - 1;
+    const uint32_t rows = tbound(k);
+    const uint32_t nseg = 1u << (BITS * k);
+    const uint32_t m = nseg * RADIX;  // children
+    const RadixDigit op{(uint32_t)(32 - BITS * (k + 1)), (uint32_t)RADIX - 1u};
+    const RadixDigit op_next{(uint32_t)(last ? 0 : 32 - BITS * (k + 2)), (uint32_t)RADIX - 1u};
+    uint32_t* C = (BITS == 4) ? ws.tc[k & 1] : ws.tc[0];
+    uint32_t* Cn = ws.tc[(k + 1) & 1];
+    const uint32_t* src = buf(k);
+    uint32_t* dst = buf(k + 1);
+    // counts of this depth: depth 0 reads the keys; 4-bit deeper depths were
+    // counted by the previous pass (fused); 8-bit deeper depths read the keys
+    // tile by tile from the table
+    if (k == 0) {
+      LS_TRY((tiles_counts<BITS, uint32_t>(ws, src, n, op, T0, C, BITS == 4 ? Cn : nullptr,
+                                           BITS == 4 ? T0 * (uint32_t)RADIX : 0u, st)));
+    } else if (BITS == 8) {
+      ScopedTimer tm("tilecounts", st, n);
+      hipLaunchKernelGGL((k_tile_counts<BITS, B, 16, uint32_t, RadixDigit, true>), dim3(rows), dim3(B), 0, st, src,
+                         (uint32_t)n, op, C, nullptr, 0u, tiles[k & 1], ctr + k);
+      LS_TRY(hipGetLastError());
+    }
+    LS_TRY(tiles_colscan<BITS>(ws, C, rows, st));
+    const uint32_t* D = tiles_digit_starts(ws, rows, BITS);
+    if (k == 0) {
+      // the top digit's sizes, for the skew check below
+      LS_TRY(hipMemcpyAsync(ws.hyb_host, D, RADIX * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      LS_TRY(hipEventRecord(ws.hyb_evt, st));
+    }
+    {
+      ScopedTimer tm("hybplan", st, m);
+      hipLaunchKernelGGL((k_hyb_children<RADIX, TILE>), dim3((m + 255) / 256), dim3(256), 0, st, C, ws.tb, D, rows,
+                         (uint32_t)n, nseg, k == 0 ? nullptr : ctile0[k & 1], cstart[k & 1], T0, segbase,
+                         cstart[(k + 1) & 1], nsize, last ? nullptr : ntl);
+      LS_TRY(hipGetLastError());
+      if (!last) {
+        hipLaunchKernelGGL(k_hyb_tile_prefix, dim3(1), dim3(1024), 0, st, ntl, m, ctile0[(k + 1) & 1], ctr + k + 1);
+        LS_TRY(hipGetLastError());
+        const uint32_t nb_ = tbound(k + 1);
+        hipLaunchKernelGGL((k_hyb_expand<RADIX, TILE>), dim3((nb_ + 255) / 256), dim3(256), 0, st,
+                           ctile0[(k + 1) & 1], m, cstart[(k + 1) & 1], nsize, ctr + k + 1, nb_,
+                           tiles[(k + 1) & 1], BITS == 4 ? Cn : nullptr);
+        LS_TRY(hipGetLastError());
+      }
+    }
+    const HybridGeo geo{tiles[k & 1], ctr + k, cstart[(k + 1) & 1], ctile0[(k + 1) & 1]};
+    {
+      ScopedTimer tm("tilepass", st, n);
+      if (BITS == 4 && !last) {
+        if (k == 0)
+          hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, BITS == 4, RadixDigit, RadixDigit, 2>),
+                             dim3(rows), dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C,
+                             ws.tb, segbase, Cn, geo);
+        else
+          hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, BITS == 4, RadixDigit, RadixDigit, 3>),
+                             dim3(rows), dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C,
+                             ws.tb, segbase, Cn, geo);
+      } else if (k == 0) {
+        hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, false, RadixDigit, RadixDigit, 0>), dim3(rows),
+                           dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C, ws.tb, segbase,
+                           Cn, geo);
+      } else {
+        hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, false, RadixDigit, RadixDigit, 1>), dim3(rows),
+                           dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C, ws.tb, segbase,
+                           Cn, geo);
+      }
+      LS_TRY(hipGetLastError());
+    }
+    if (k == 0) {
+      // skew check (the pass above keeps the GPU busy meanwhile; it wrote
+      // only tmp, so abandoning here leaves in intact)
+      LS_TRY(hipEventSynchronize(ws.hyb_evt));
+      uint32_t mx = 0;
+      for (int d = 0; d < RADIX; ++d) {
+        const uint32_t e = d + 1 < RADIX ? ws.hyb_host[d + 1] : (uint32_t)n;
+        mx = std::max(mx, e - ws.hyb_host[d]);
+      }
+      // a top digit well above its share (beyond sampling noise), or one
+      // whose buckets would average > 0.9 of a block: the LSD sort instead
+      const double share = (double)n / RADIX;
+      if ((double)mx > 1.25 * share + 4.0 * std::sqrt(share) + 32.0 ||
+          (double)mx / (double)(NB / RADIX) > 0.9 * cap)
+        return hipSuccess;
+    }
+  }
+  // bucket sort of the 2^16 buckets in place in out (cstart/nsize of the
+  // last depth's children)
+  {
+    ScopedTimer tm("bucketsort", st, n);
+    const uint32_t* bstart = cstart[DEPTHS & 1];
+    if (small)
+      hipLaunchKernelGGL((k_bucket_sort<BITS, 256, kSmallItems>), dim3(NB), dim3(256), 0, st, out, out, bstart, nsize,
+                         ctr + 9, 16u, ctr + 8);
+    else
+      hipLaunchKernelGGL((k_bucket_sort<BITS, 256, kLargeItems>), dim3(NB), dim3(256), 0, st, out, out, bstart, nsize,
+                         ctr + 9, 16u, ctr + 8);
+    LS_TRY(hipGetLastError());
+  }
+  LS_TRY(hipMemcpyAsync(ws.hyb_host + 16, ctr + 8, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  LS_TRY(hipStreamSynchronize(st));
+  *handled = true;
+  if (ws.hyb_host[16] != 0) {
+    // buckets too large for one block: finish with the LSD sort of out
+    LS_TRY((sort_impl<uint32_t, NoValue>(ws, out, out, tmp, nullptr, nullptr, nullptr, n, 0, 32, BITS, st)));
+  }
+  return hipSuccess;
+}
+
 }  // namespace
 
 hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n, int lo,
                     int hi, int digit_bits, uint32_t* d_bounds, hipStream_t st, uint32_t bias) {
   if (bias && d_bounds) return hipErrorInvalidValue;
+  const int hyb = get_hybrid_mode();
+  if (!d_bounds && !bias && lo == 0 && hi == 32 && (digit_bits == 4 || digit_bits == 8) &&
+      ((hyb == 1 && n >= kHybMinKeys && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
+      (get_algorithm() == 0 || get_algorithm() == 3) && in != tmp) {
+    bool handled = false;
+    if (digit_bits == 4)
+      LS_TRY(sort_hybrid_u32<4>(ws, in, out, tmp, n, st, &handled));
+    else
+      LS_TRY(sort_hybrid_u32<8>(ws, in, out, tmp, n, st, &handled));
+    if (handled) {
+      ws.last_algo = 4;
+      return hipSuccess;
+    }
+  }
   LS_TRY((sort_impl<uint32_t, NoValue>(ws, in, out, tmp, nullptr, nullptr, nullptr, n, lo, hi,
                                       digit_bits, st, bias)));
   if (d_bounds) {
@@ -2515,7 +2969,7 @@ hipError_t partition_lut_impl(Workspace& ws, const K* in, K* out, const V* vin, 
     ScopedTimer tm("partition", st, n);
     hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(BITS), K, V, false, LutDigit>), dim3(tiles), dim3(B), 0, st, in,
                        out, vin, vout, (uint32_t)n, op, RadixDigit{0u, 1u}, ws.tc[0], (const uint32_t*)ws.tb,
-                       (const uint32_t*)tiles_digit_starts(ws, tiles, BITS), ws.tc[1]);
+                       (const uint32_t*)tiles_digit_starts(ws, tiles, BITS), ws.tc[1], HybridGeo{});
     LS_TRY(hipGetLastError());
   }
   return hipSuccess;

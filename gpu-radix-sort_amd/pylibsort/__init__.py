@@ -85,6 +85,7 @@ _SIGS = [
     ("libsortSetDigitBits", ctypes.c_int, [ctypes.c_int]),
     ("libsortGetDigitBits", ctypes.c_int, []),
     ("libsortSetAlgorithm", ctypes.c_int, [ctypes.c_int]),
+    ("libsortSetHybrid", ctypes.c_int, [ctypes.c_int]),
     ("libsortSetBoundaryMode", ctypes.c_int, [ctypes.c_int]),
     ("libsortTimingEnable", None, [ctypes.c_bool]),
     ("libsortTimingReset", None, []),

@@ -12,7 +12,7 @@ from . import _state, require_gpu
 __all__ = [
     "sortException", "sortResultException", "groupBits", "bytesToInts", "checkOrder",
     "checkSortFull", "checkPartial", "sortFull", "sortFullDistrib", "sortPartial", "generateInputs",
-    "boundariesToCaps", "setDigitBits", "getDigitBits", "setAlgorithm",
+    "boundariesToCaps", "setDigitBits", "getDigitBits", "setAlgorithm", "setHybrid",
 ]
 
 
@@ -163,6 +163,16 @@ def getDigitBits():
 
 
 _ALGOS = {"auto": 0, "onesweep": 1, "rts": 2, "tiles": 3}
+_HYBRID = {"off": 0, "auto": 1, "force": 2}
+
+
+def setHybrid(name):
+    """MSD hybrid for full 32-bit key sorts: "auto" (default), "off" or
+    "force" (every full sort of >= 1024 keys); returns the previous name."""
+    prev = _state.sortLib.libsortSetHybrid(_HYBRID[name])
+    if prev < 0:
+        raise ValueError(name)
+    return {v: k for k, v in _HYBRID.items()}[prev]
 
 
 def setAlgorithm(name):

@@ -263,6 +263,15 @@ LIBSORT_API int libsortGetDigitBits(void);
  * if `algo` is invalid. */
 LIBSORT_API int libsortSetAlgorithm(int algo);
 
+/* Full 32-bit sorts of uint32 keys (providedGpu, libsortSortKeysU32 with
+ * offset 0 / width 32): 1 (default) = for 2^27 <= n <= 2^28 + 2^24 keys the
+ * MSD hybrid (16 / digit-bits passes from the top digit down, then every
+ * bucket of keys sharing the top 16 bits sorted on chip; the call returns with
+ * the sort complete); 0 = always the LSD digit passes; 2 = the hybrid for
+ * every such sort of n >= 1024 keys (tests).  Initial value from
+ * LIBSORT_HYBRID.  Returns the previous value, or -1 if `mode` is invalid. */
+LIBSORT_API int libsortSetHybrid(int mode);
+
 /* Boundaries returned by gpuPartial / gpuPartialProfile / gpuPartialSort:
  * 0 (default) = for every group g the number of elements whose group is < g
  * (the exclusive prefix every reference caller and test expects:

@@ -1,0 +1,157 @@
+"""GPU parity of the MSD hybrid (sort_hybrid_u32: digit passes from the top
+digit down over segment-aligned tiles, then every bucket of keys sharing the
+top 16 bits sorted on chip), through the C ABI, against the oracle.
+
+The hybrid serves full 32-bit sorts of 2^27 .. 2^28 + 2^24 keys; "force"
+mode (libsortSetHybrid(2)) runs it for every full sort of >= 1024 keys, so
+ragged sizes, skewed and duplicate-heavy inputs are checked at sizes the
+oracle sorts in a moment.  Both fallbacks are covered: a skewed top digit
+abandons the hybrid after the first column scan (LSD sort of the untouched
+input), and buckets larger than a block are finished by an LSD sort of the
+output in place.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pylibsort
+    import pylibsort.device as D
+    assert pylibsort.gpu_ready(), pylibsort.last_error()
+    return D
+
+
+@pytest.fixture(params=[4, 8], ids=["digit4", "digit8"])
+def bits(request, dev):
+    import pylibsort
+    prev = pylibsort.setDigitBits(request.param)
+    yield request.param
+    pylibsort.setDigitBits(prev)
+
+
+@pytest.fixture
+def force(dev):
+    import pylibsort
+    prev = pylibsort.setHybrid("force")
+    yield
+    pylibsort.setHybrid(prev)
+
+
+def _u32(t):
+    return t.detach().cpu().numpy().view(np.uint32)
+
+
+def _tensor(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.uint32).view(np.int32)).cuda()
+
+
+def _sort_counting_buckets(dev, *args, **kw):
+    """dev.sort_keys_u32 with the per-kernel timing registry on: returns the
+    output and how many bucket-sort launches (the hybrid's last step) ran."""
+    dev.timing_enable(True)
+    dev.timing_reset()
+    try:
+        out = dev.sort_keys_u32(*args, **kw)
+        torch.cuda.synchronize()
+        return out, dev.timing_query("bucketsort")[0]
+    finally:
+        dev.timing_enable(False)
+
+
+def _inputs(kind, n, seed):
+    import oracle.oracle as o
+    x = o.pcg(n, first=seed)
+    rng = np.random.default_rng(seed)
+    if kind == "pcg":
+        return x
+    if kind == "top_skew":        # keys < 2^30: 4 of 16 top digits -> hybrid abandoned
+        return x >> 2
+    if kind == "deep_skew":       # top digit uniform, bits 16-27 zero -> buckets overflow
+        return x & np.uint32(0xF000FFFF)
+    if kind == "equal":
+        return np.full(n, 0x9E3779B9, dtype=np.uint32)
+    if kind == "four":
+        return rng.integers(0, 4, n, dtype=np.uint64).astype(np.uint32) * np.uint32(0x40000001)
+    if kind == "sorted":
+        return np.sort(x)
+    if kind == "reverse":
+        return np.sort(x)[::-1].copy()
+    if kind == "low16_const":     # every bucket all-equal keys
+        return x & np.uint32(0xFFFF0000)
+    if kind == "top16_dense":     # ~16 keys per bucket at 2^20
+        return x
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize("n", [1024, 1025, 4097, 65539, (1 << 20) + 3, (1 << 22) + 5])
+def test_hybrid_forced_sizes(dev, oracle_mod, bits, force, n):
+    x = oracle_mod.pcg(n, first=5 * n + bits)
+    out, nbs = _sort_counting_buckets(dev, _tensor(x))
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+    assert nbs == 1
+
+
+@pytest.mark.parametrize("kind", ["top_skew", "deep_skew", "equal", "four", "sorted", "reverse", "low16_const"])
+def test_hybrid_forced_distributions(dev, oracle_mod, bits, force, kind):
+    n = (1 << 22) + 17
+    x = _inputs(kind, n, 11 + bits)
+    out = dev.sort_keys_u32(_tensor(x))
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+
+
+def test_hybrid_forced_in_place(dev, oracle_mod, bits, force):
+    x = oracle_mod.pcg((1 << 21) + 9, first=77)
+    t = _tensor(x)
+    tmp = torch.empty_like(t)
+    dev.sort_keys_u32(t, out=t, tmp=tmp)
+    np.testing.assert_array_equal(_u32(t), oracle_mod.sort_u32(x))
+
+
+def test_hybrid_forced_host_abi(dev, oracle_mod, bits, force):
+    import pylibsort
+    x = oracle_mod.pcg(300007, first=91)
+    buf = bytearray(x.tobytes())
+    pylibsort.sortFull(buf)
+    np.testing.assert_array_equal(np.frombuffer(buf, dtype=np.uint32), oracle_mod.sort_u32(x))
+
+
+@pytest.mark.parametrize("n", [1 << 27, (1 << 27) + 12345, (1 << 28) + (1 << 24) - 3])
+def test_hybrid_auto_large(dev, oracle_mod, bits, n):
+    """The sizes the auto mode serves (the 2^28 reference hash is in
+    test_gpu_parity.test_reference_size_full_sort_sha): PCG keys sorted on
+    the device, sha256 against the oracle's counting-sort restatement."""
+    import hashlib
+    x = dev.populate_u32(n, first=n % 1000)
+    out, nbs = _sort_counting_buckets(dev, x)
+    assert nbs == 1
+    h = hashlib.sha256()
+    for i in range(0, n, 1 << 26):
+        h.update(out[i:i + (1 << 26)].cpu().numpy().view("<u4").tobytes())
+    assert h.hexdigest() == oracle_mod.sorted_pcg_sha256(n, first=n % 1000)
+
+
+def test_hybrid_auto_skewed_large(dev, oracle_mod, bits):
+    """2^27 keys that overflow the buckets (the bits below the top digit
+    down to bit 16 zero): the bucket sort
+    leaves them and the LSD sort of the output finishes; and a skewed top
+    digit (keys < 2^30) abandons the hybrid before it writes out."""
+    n = 1 << 27
+    x = dev.populate_u32(n, first=3)
+    for mask_kind in ("deep", "top"):
+        if mask_kind == "deep":
+            # the top digit uniform, the bits below it down to bit 16 zero
+            mask = 0xF000FFFF if bits == 4 else 0xFF00FFFF
+            y = torch.bitwise_and(x, torch.tensor(mask - (1 << 32), dtype=torch.int32, device=x.device))
+        else:
+            y = torch.bitwise_and(torch.bitwise_right_shift(x, 2), 0x3FFFFFFF)
+        out, nbs = _sort_counting_buckets(dev, y)
+        assert nbs == (1 if mask_kind == "deep" else 0)
+        host = y.cpu().numpy().view(np.uint32)
+        np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(host))

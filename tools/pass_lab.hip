@@ -17,6 +17,7 @@ namespace lsort {
 int timing_start(const char*, hipStream_t, uint64_t) { return -1; }
 void timing_stop(int, hipStream_t) {}
 int get_algorithm() { return 3; }
+int get_hybrid_mode() { return 0; }
 }  // namespace lsort
 
 using namespace lsort;
