@@ -34,16 +34,26 @@ KEYS = 1 << 28
 HEADLINE = "k_tile_pass<4, 256, 16, unsigned int, lsort::NoValue"
 
 
+def _groups(row):
+    gx = int(float(row.get("Grid_Size_X", row.get("Grid_Size", 0)) or 0))
+    wx = int(float(row.get("Workgroup_Size_X", row.get("Workgroup_Size", 256)) or 256))
+    return gx // wx if gx >= wx * 1024 else gx  # grid in work-items or in workgroups
+
+
 def headline(row):
     """The bench's headline pass: 4-bit keys-only RadixDigit k_tile_pass over
-    the 2^28-key workload (65536 tiles of 4096 keys)."""
+    the 2^28-key workload -- the MSD hybrid's four digit passes, whose grids
+    are the 65536 tiles plus at most one partial tile per segment (16, 256,
+    4096 segments at depths 1-3)."""
     name = row.get("Kernel_Name", "")
     if HEADLINE not in name or "BiasedDigit" in name or "LutDigit" in name:
         return False
-    gx = int(float(row.get("Grid_Size_X", row.get("Grid_Size", 0)) or 0))
-    wx = int(float(row.get("Workgroup_Size_X", row.get("Workgroup_Size", 256)) or 256))
-    groups = gx // wx if gx >= wx * 1024 else gx  # grid in work-items or in workgroups
-    return groups == KEYS // 4096
+    return KEYS // 4096 <= _groups(row) <= KEYS // 4096 + 4096
+
+
+def bucketsort(row):
+    name = row.get("Kernel_Name", "")
+    return "k_bucket_sort<4," in name and _groups(row) == 65536
 
 
 trace = sorted(glob.glob(str(src / "stats" / "**" / "*kernel_trace.csv"), recursive=True))
@@ -55,23 +65,24 @@ for f in trace:
 durs.sort()
 if durs:
     us = [d for _, d in durs]
-    steps, per = 20, 8  # the command's timed steps, passes per sort
+    steps, per = 20, 4  # the command's timed steps, digit passes per sort (MSD hybrid: 16 bits / 4)
     timed = us[-steps * per:]
-    rec = {"kernel": "k_tile_pass<4,...> (4-bit keys-only pass, 65536 tiles)", "cmd": cmd,
+    rec = {"kernel": "k_tile_pass<4,...> (4-bit keys-only digit pass of the MSD hybrid, 65536+ tiles)", "cmd": cmd,
            "launches": len(timed), "avg_launch_us": sum(timed) / len(timed),
            "all_launches": len(us), "avg_all_us": sum(us) / len(us),
            "min_us": min(us), "max_us": max(us),
-           "note": "avg_launch_us = the last 160 launches (the 20 timed sorts; the warm-up sorts come first in the "
+           "note": "avg_launch_us = the last 80 launches (the 20 timed sorts; the warm-up sorts come first in the "
                    "trace), avg_all_us includes the warm-up"}
     (dst / ("%s_rocprof_tilepass.json" % tag)).write_text(json.dumps(rec, indent=1) + "\n")
     print(json.dumps(rec))
 
 
-def pmc(counter):
+def pmc(counter, pick=None):
+    pick = pick or headline
     vals = []
     for f in glob.glob(str(src / ("pmc_" + counter) / "**" / "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if headline(r):
+            if pick(r):
                 vals.append(float(r["Counter_Value"]))
     return vals
 
@@ -86,4 +97,22 @@ if fetch and write:
                      "read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE; KiB -> bytes; headline pass launches only" % cmd,
            "round": tag}
     (dst / ("%s_pmc_tilepass.json" % tag)).write_text(json.dumps(rec, indent=1) + "\n")
+    print(json.dumps(rec))
+
+
+# the bucket sort (the MSD hybrid's last step: one HBM read and write per key)
+fetch, write = pmc("FETCH_SIZE", bucketsort), pmc("WRITE_SIZE", bucketsort)
+bs = []
+for f in trace:
+    for r in csv.DictReader(open(f)):
+        if bucketsort(r):
+            bs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+if fetch and write and bs:
+    fr = sum(fetch) / len(fetch) * 1024 * 2
+    wr = sum(write) / len(write) * 1024
+    rec = {"kernel": "k_bucket_sort<4, 256, 19> (2^16 buckets of the 2^28-key workload)", "cmd": cmd,
+           "launches": len(bs), "avg_launch_us": sum(bs) / len(bs), "read_bytes_per_launch": fr,
+           "write_bytes_per_launch": wr, "algorithmic_bytes_per_launch": 8.0 * KEYS,
+           "method": "same runs as %s_pmc_tilepass.json" % tag, "round": tag}
+    (dst / ("%s_bucketsort.json" % tag)).write_text(json.dumps(rec, indent=1) + "\n")
     print(json.dumps(rec))
