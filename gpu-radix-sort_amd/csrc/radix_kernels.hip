@@ -1114,10 +1114,16 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
     for (int q = 0; q < NEXT / BLOCK; ++q) s_next[tid + q * BLOCK] = 0u;
   }
   // this tile's run offsets (independent of every other tile)
-  uint32_t gofs = 0;
+  uint32_t gofs = 0, ncs = 0, nct = 0;
   if (tid < RADIX) {
     gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid] + D[(size_t)seg * RADIX + tid];
     if constexpr (FUSE) C[(size_t)t * RADIX + tid] = 0u;  // the C_next of the pass after the next
+    if constexpr (FUSE && (GEO & 2) != 0) {
+      // the next depth's child of digit tid (loaded with the offsets, not
+      // after the rank where the block would wait for it)
+      ncs = geo.ncstart[seg * RADIX + tid];
+      nct = geo.nctile0[seg * RADIX + tid];
+    }
   }
   const bool full = valid == TILE;
   const uint32_t wbase = w * WSPAN;
@@ -1170,10 +1176,9 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
     if constexpr (FUSE && (GEO & 2) != 0) {
       // next depth's tiles are cut per child: position p of child c is in
       // tile nctile0[c] + (p - ncstart[c]) / TILE
-      const uint32_t c = seg * RADIX + tid, cs = geo.ncstart[c];
-      const uint32_t tl = (gofs - cs) / TILE;
-      s_ob[tid] = make_uint2(ob, cs + (tl + 1) * TILE - ob);
-      s_tfirst[tid] = geo.nctile0[c] + tl;
+      const uint32_t tl = (gofs - ncs) / TILE;
+      s_ob[tid] = make_uint2(ob, ncs + (tl + 1) * TILE - ob);
+      s_tfirst[tid] = nct + tl;
     } else if constexpr (FUSE) {
       const uint32_t tf = gofs / TILE;
       s_ob[tid] = make_uint2(ob, (tf + 1) * TILE - ob);

@@ -42,11 +42,15 @@ int main(int argc, char** argv) {
   std::vector<uint32_t> h(n);
   struct V { std::string name; uint32_t S; std::function<void(uint32_t)> launch; };
   std::vector<V> vs;
-#define BV(BITS, B, I, S_)                                                                                        \
-  vs.push_back({#BITS "-bit " #B "x" #I " S=" #S_, S_, [&](uint32_t m) {                                          \
-                  hipLaunchKernelGGL((k_bucket_sort<BITS, B, I>), dim3(m), dim3(B), 0, st, in, out, bs, bl, nb, 16u, ov); \
+#define BVG(BITS, B, I, S_, LB, G)                                                                                \
+  vs.push_back({#BITS "-bit " #B "x" #I " S=" #S_ " lbits=" #LB " grid=" #G, S_, [&](uint32_t m) {               \
+                  hipLaunchKernelGGL((k_bucket_sort<BITS, B, I>), dim3(G ? std::min<uint32_t>(m, G) : m), dim3(B), 0, \
+                                     st, in, out, bs, bl, nb, LB##u, ov);                                           \
                 }});
-  BV(4, 256, 19, 4096) BV(4, 256, 16, 4096) BV(4, 256, 17, 4096) BV(8, 256, 19, 4096) BV(8, 256, 16, 4096)
+#define BVL(BITS, B, I, S_, LB) BVG(BITS, B, I, S_, LB, 0)
+#define BV(BITS, B, I, S_) BVL(BITS, B, I, S_, 16)
+  BV(4, 256, 19, 4096) BV(4, 256, 16, 4096) BVL(4, 256, 16, 4096, 0) BVL(4, 256, 16, 4096, 4)
+  BVL(4, 256, 16, 4096, 8) BV(8, 256, 19, 4096) BV(8, 256, 16, 4096)
   for (auto& v : vs) {
     const uint32_t m = (uint32_t)(n / v.S);
     hipLaunchKernelGGL(fill, dim3((n + 255) / 256), dim3(256), 0, st, in, n, v.S, 0u);
@@ -74,7 +78,7 @@ int main(int argc, char** argv) {
     std::sort(us.begin(), us.end());
     const float med = us[us.size() / 2];
     printf("%-26s 2^%d keys: median %7.1f us  best %7.1f  %5.0f GB/s (8 B/key)  %s\n", v.name.c_str(), lg, med, us[0],
-           8.0 * n / (med * 1e-6) / 1e9, (sorted && sum0 == sum1 && x0 == x1) ? "sorted" : "WRONG");
+           8.0 * n / (med * 1e-6) / 1e9, (sorted && sum0 == sum1 && x0 == x1) ? "sorted" : (sum0 == sum1 && x0 == x1 ? "permutation" : "WRONG"));
   }
   return 0;
 }
