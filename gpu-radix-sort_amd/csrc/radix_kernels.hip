@@ -65,11 +65,12 @@ struct BiasedDigit {
   __device__ __forceinline__ uint32_t operator()(uint64_t k) const { return (uint32_t)((k - bias) >> shift) & mask; }
 };
 
-template <typename Op> Op make_digit(uint32_t shift, uint32_t mask, uint32_t bias);
-template <> inline RadixDigit make_digit<RadixDigit>(uint32_t shift, uint32_t mask, uint32_t) {
+template <typename Op> __host__ __device__ Op make_digit(uint32_t shift, uint32_t mask, uint32_t bias);
+template <> __host__ __device__ inline RadixDigit make_digit<RadixDigit>(uint32_t shift, uint32_t mask, uint32_t) {
   return RadixDigit{shift, mask};
 }
-template <> inline BiasedDigit make_digit<BiasedDigit>(uint32_t shift, uint32_t mask, uint32_t bias) {
+template <> __host__ __device__ inline BiasedDigit make_digit<BiasedDigit>(uint32_t shift, uint32_t mask,
+                                                                            uint32_t bias) {
   return BiasedDigit{shift, mask, bias};
 }
 
@@ -1300,16 +1301,17 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 // the low lbits bits instead of lbits/BITS digit passes.  Slots past the end
 // of the bucket hold 0xffffffff: they are last in item order and carry the
 // largest digit, so every step keeps them behind the real keys and the steps
-// run without predicates.  Grid: an upper bound of buckets; *nb is the
+// run without predicates (range sorts, Op = BiasedDigit: digits of key -
+// bias, pads bias - 1).  Grid: an upper bound of buckets; *nb is the
 // bucket count.  A bucket larger than the block is left alone and counted in
 // *oversized (the caller then sorts those keys another way).  in may equal
 // out (a block holds its whole bucket before it writes).
-template <int BITS, int BLOCK, int ITEMS>
+template <int BITS, int BLOCK, int ITEMS, typename Op = RadixDigit>
 __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* in, uint32_t* out,
                                                        const uint32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ blen,
                                                        const uint32_t* __restrict__ nb, uint32_t lbits,
-                                                       uint32_t* __restrict__ oversized) {
+                                                       uint32_t bias, uint32_t* __restrict__ oversized) {
   constexpr int RADIX = 1 << BITS;
   constexpr int WAVES = BLOCK / kWave;
   constexpr int CAP = BLOCK * ITEMS;
@@ -1334,11 +1336,11 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* in, uint3
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t i = wbase + j * kWave + lane;
-    k[j] = i < len ? load_stream(&in[(size_t)start + i]) : 0xffffffffu;
+    k[j] = i < len ? load_stream(&in[(size_t)start + i]) : bias - 1u;  // pad: every digit of key - bias maximal
   }
   for (uint32_t shift = 0; shift < lbits; shift += BITS) {
     const uint32_t nbits = min((uint32_t)BITS, lbits - shift);
-    const RadixDigit op{shift, (1u << nbits) - 1u};
+    const Op op = make_digit<Op>(shift, (1u << nbits) - 1u, bias);
     for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0;
     rank_items_t<BITS, true, ITEMS>(k, rk, s_whist[w], 0u, wbase, lane, op);
     __syncthreads();
@@ -2651,12 +2653,13 @@ hipError_t group_bounds(Workspace& ws, const uint32_t* sorted, size_t n, int lo,
 }
 
 // ----------------------------------------------------------------------------
-// MSD hybrid for full 32-bit sorts of uint32 keys (DESIGN.md §3 "MSD passes +
-// bucket sort"): DEPTHS = 16 / BITS digit passes from the TOP digit down,
+// MSD hybrid for full sorts of uint32 keys (DESIGN.md §3 "MSD passes +
+// bucket sort"): all 32 bits, or a range sort's W bits of key - bias (keys in
+// [bias, bias + 2^W)).  DEPTHS = 16 / BITS digit passes from the TOP digit down,
 // each a stable partition of every segment (keys sharing the digits above) by
 // its next digit, cut into segment-aligned tiles; then every one of the 2^16
-// buckets (keys sharing their top 16 bits, ~n / 65536 keys) is sorted on its
-// low 16 bits on chip by k_bucket_sort.  HBM passes: DEPTHS + 1 instead of
+// buckets (keys sharing their top 16 of W bits, ~n / 65536 keys) is sorted
+// on its low W - 16 bits on chip by k_bucket_sort.  HBM passes: DEPTHS + 1 instead of
 // 32 / BITS.  Keys only: order among equal keys is not observable.
 // Buffers: depth k reads buf[k] and writes buf[k + 1] with buf[0] = in,
 // buf[odd] = tmp, buf[even > 0] = out; DEPTHS is even, so the buckets are
@@ -2671,9 +2674,9 @@ constexpr size_t kHybMinKeys = 1ull << 27;
 constexpr size_t kHybMaxKeys = (1ull << 28) + (1ull << 24);
 
 
-template <int BITS>
-hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n, hipStream_t st,
-                           bool* handled) {
+template <int BITS, typename Op>
+hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n, int W,
+                           uint32_t bias, hipStream_t st, bool* handled) {
   constexpr int RADIX = 1 << BITS;
   constexpr int B = tp_block<uint32_t>(BITS);
   constexpr int TILE = B * 16;
@@ -2711,8 +2714,8 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
     const uint32_t rows = tbound(k);
     const uint32_t nseg = 1u << (BITS * k);
     const uint32_t m = nseg * RADIX;  // children
-    const RadixDigit op{(uint32_t)(32 - BITS * (k + 1)), (uint32_t)RADIX - 1u};
-    const RadixDigit op_next{(uint32_t)(last ? 0 : 32 - BITS * (k + 2)), (uint32_t)RADIX - 1u};
+    const Op op = make_digit<Op>((uint32_t)(W - BITS * (k + 1)), (uint32_t)RADIX - 1u, bias);
+    const Op op_next = make_digit<Op>((uint32_t)(last ? 0 : W - BITS * (k + 2)), (uint32_t)RADIX - 1u, bias);
     uint32_t* C = (BITS == 4) ? ws.tc[k & 1] : ws.tc[0];
     uint32_t* Cn = ws.tc[(k + 1) & 1];
     const uint32_t* src = buf(k);
@@ -2721,11 +2724,11 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
     // counted by the previous pass (fused); 8-bit deeper depths read the keys
     // tile by tile from the table
     if (k == 0) {
-      LS_TRY((tiles_counts<BITS, uint32_t>(ws, src, n, op, T0, C, BITS == 4 ? Cn : nullptr,
+      LS_TRY((tiles_counts<BITS, uint32_t, Op>(ws, src, n, op, T0, C, BITS == 4 ? Cn : nullptr,
                                            BITS == 4 ? T0 * (uint32_t)RADIX : 0u, st)));
     } else if (BITS == 8) {
       ScopedTimer tm("tilecounts", st, n);
-      hipLaunchKernelGGL((k_tile_counts<BITS, B, 16, uint32_t, RadixDigit, true>), dim3(rows), dim3(B), 0, st, src,
+      hipLaunchKernelGGL((k_tile_counts<BITS, B, 16, uint32_t, Op, true>), dim3(rows), dim3(B), 0, st, src,
                          (uint32_t)n, op, C, nullptr, 0u, tiles[k & 1], ctr + k);
       LS_TRY(hipGetLastError());
     }
@@ -2757,19 +2760,19 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
       ScopedTimer tm("tilepass", st, n);
       if (BITS == 4 && !last) {
         if (k == 0)
-          hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, BITS == 4, RadixDigit, RadixDigit, 2>),
+          hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, BITS == 4, Op, Op, 2>),
                              dim3(rows), dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C,
                              ws.tb, segbase, Cn, geo);
         else
-          hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, BITS == 4, RadixDigit, RadixDigit, 3>),
+          hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, BITS == 4, Op, Op, 3>),
                              dim3(rows), dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C,
                              ws.tb, segbase, Cn, geo);
       } else if (k == 0) {
-        hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, false, RadixDigit, RadixDigit, 0>), dim3(rows),
+        hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, false, Op, Op, 0>), dim3(rows),
                            dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C, ws.tb, segbase,
                            Cn, geo);
       } else {
-        hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, false, RadixDigit, RadixDigit, 1>), dim3(rows),
+        hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, false, Op, Op, 1>), dim3(rows),
                            dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C, ws.tb, segbase,
                            Cn, geo);
       }
@@ -2797,12 +2800,13 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   {
     ScopedTimer tm("bucketsort", st, n);
     const uint32_t* bstart = cstart[DEPTHS & 1];
+    const uint32_t lbits = (uint32_t)(W - 16);
     if (small)
-      hipLaunchKernelGGL((k_bucket_sort<BITS, 256, kSmallItems>), dim3(NB), dim3(256), 0, st, out, out, bstart, nsize,
-                         ctr + 9, 16u, ctr + 8);
+      hipLaunchKernelGGL((k_bucket_sort<BITS, 256, kSmallItems, Op>), dim3(NB), dim3(256), 0, st, out, out, bstart,
+                         nsize, ctr + 9, lbits, bias, ctr + 8);
     else
-      hipLaunchKernelGGL((k_bucket_sort<BITS, 256, kLargeItems>), dim3(NB), dim3(256), 0, st, out, out, bstart, nsize,
-                         ctr + 9, 16u, ctr + 8);
+      hipLaunchKernelGGL((k_bucket_sort<BITS, 256, kLargeItems, Op>), dim3(NB), dim3(256), 0, st, out, out, bstart,
+                         nsize, ctr + 9, lbits, bias, ctr + 8);
     LS_TRY(hipGetLastError());
   }
   LS_TRY(hipMemcpyAsync(ws.hyb_host + 16, ctr + 8, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -2810,7 +2814,7 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   *handled = true;
   if (ws.hyb_host[16] != 0) {
     // buckets too large for one block: finish with the LSD sort of out
-    LS_TRY((sort_impl<uint32_t, NoValue>(ws, out, out, tmp, nullptr, nullptr, nullptr, n, 0, 32, BITS, st)));
+    LS_TRY((sort_impl<uint32_t, NoValue>(ws, out, out, tmp, nullptr, nullptr, nullptr, n, 0, W, BITS, st, bias)));
   }
   return hipSuccess;
 }
@@ -2818,17 +2822,24 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
 }  // namespace
 
 hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n, int lo,
-                    int hi, int digit_bits, uint32_t* d_bounds, hipStream_t st, uint32_t bias) {
+                    int hi, int digit_bits, uint32_t* d_bounds, hipStream_t st, uint32_t bias, bool range) {
   if (bias && d_bounds) return hipErrorInvalidValue;
   const int hyb = get_hybrid_mode();
-  if (!d_bounds && !bias && lo == 0 && hi == 32 && (digit_bits == 4 || digit_bits == 8) &&
+  // the hybrid needs the sorted bits to determine the key: a full 32-bit
+  // sort, or a range sort (keys in [bias, bias + 2^hi)) of >= 20 bits
+  const bool whole = !d_bounds && lo == 0 && ((hi == 32 && !bias) || (range && hi >= 20));
+  if (whole && (digit_bits == 4 || digit_bits == 8) &&
       ((hyb == 1 && n >= kHybMinKeys && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
       (get_algorithm() == 0 || get_algorithm() == 3) && in != tmp) {
     bool handled = false;
-    if (digit_bits == 4)
-      LS_TRY(sort_hybrid_u32<4>(ws, in, out, tmp, n, st, &handled));
+    if (bias && digit_bits == 4)
+      LS_TRY((sort_hybrid_u32<4, BiasedDigit>(ws, in, out, tmp, n, hi, bias, st, &handled)));
+    else if (bias)
+      LS_TRY((sort_hybrid_u32<8, BiasedDigit>(ws, in, out, tmp, n, hi, bias, st, &handled)));
+    else if (digit_bits == 4)
+      LS_TRY((sort_hybrid_u32<4, RadixDigit>(ws, in, out, tmp, n, hi, 0u, st, &handled)));
     else
-      LS_TRY(sort_hybrid_u32<8>(ws, in, out, tmp, n, st, &handled));
+      LS_TRY((sort_hybrid_u32<8, RadixDigit>(ws, in, out, tmp, n, hi, 0u, st, &handled)));
     if (handled) {
       ws.last_algo = 4;
       return hipSuccess;

@@ -155,3 +155,45 @@ def test_hybrid_auto_skewed_large(dev, oracle_mod, bits):
         assert nbs == (1 if mask_kind == "deep" else 0)
         host = y.cpu().numpy().view(np.uint32)
         np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(host))
+
+
+@pytest.mark.parametrize("lo,width", [(0x12300000, 27), (0, 24), (0xFFF00000, 20), (7, 31)])
+@pytest.mark.parametrize("n", [4099, (1 << 21) + 11])
+def test_hybrid_forced_range_sorts(dev, oracle_mod, bits, force, lo, width, n):
+    """Range-restricted sorts (libsortSortKeysRangeU32: keys in [lo, lo +
+    2^width), the multi-GPU round sorts) take the hybrid over the width bits
+    of key - lo: digit passes over the top 16 of them, buckets sorted on the
+    rest (pads lo - 1)."""
+    hi = lo + (1 << width)
+    x = (oracle_mod.pcg(n, first=n + width).astype(np.uint64) % (hi - lo) + lo).astype(np.uint32)
+    x[:5] = [lo, hi - 1, lo, hi - 1, lo + 1]
+    dev.timing_enable(True)
+    dev.timing_reset()
+    try:
+        out = dev.sort_keys_range_u32(_tensor(x), lo, hi)
+        torch.cuda.synchronize()
+        nbs = dev.timing_query("bucketsort")[0]
+    finally:
+        dev.timing_enable(False)
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+    assert nbs == 1
+
+
+def test_hybrid_auto_range_large(dev, oracle_mod, bits):
+    """The size of a multi-GPU round sort at 8 GPUs (2^27 keys spanning
+    2^27 values): the auto mode takes the hybrid."""
+    import hashlib
+    n, lo = 1 << 27, 0x40000000
+    x = dev.populate_u32(n, first=5)
+    y = torch.bitwise_or(torch.bitwise_and(x, (1 << 27) - 1), lo)
+    dev.timing_enable(True)
+    dev.timing_reset()
+    try:
+        out = dev.sort_keys_range_u32(y, lo, lo + (1 << 27))
+        torch.cuda.synchronize()
+        nbs = dev.timing_query("bucketsort")[0]
+    finally:
+        dev.timing_enable(False)
+    assert nbs == 1
+    host = y.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(host))
