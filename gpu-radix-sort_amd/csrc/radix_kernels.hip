@@ -1302,16 +1302,19 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 // of the bucket hold 0xffffffff: they are last in item order and carry the
 // largest digit, so every step keeps them behind the real keys and the steps
 // run without predicates (range sorts, Op = BiasedDigit: digits of key -
-// bias, pads bias - 1).  Grid: an upper bound of buckets; *nb is the
-// bucket count.  A bucket larger than the block is left alone and counted in
-// *oversized (the caller then sorts those keys another way).  in may equal
+// bias, pads bias - 1).  Grid: an upper bound of buckets; min(*nb, nb_cap)
+// is the bucket count; bucket = ilist[block] when a list is given.  A bucket
+// larger than the block is left alone, counted in *oversized and (when olist
+// is given, up to olist_cap) listed for a block of the next size.  in may equal
 // out (a block holds its whole bucket before it writes).
 template <int BITS, int BLOCK, int ITEMS, typename Op = RadixDigit>
 __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* in, uint32_t* out,
                                                        const uint32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ blen,
-                                                       const uint32_t* __restrict__ nb, uint32_t lbits,
-                                                       uint32_t bias, uint32_t* __restrict__ oversized) {
+                                                       const uint32_t* __restrict__ nb, uint32_t nb_cap,
+                                                       const uint32_t* __restrict__ ilist, uint32_t lbits,
+                                                       uint32_t bias, uint32_t* __restrict__ oversized,
+                                                       uint32_t* __restrict__ olist, uint32_t olist_cap) {
   constexpr int RADIX = 1 << BITS;
   constexpr int WAVES = BLOCK / kWave;
   constexpr int CAP = BLOCK * ITEMS;
@@ -1321,10 +1324,14 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* in, uint3
   __shared__ WaveCount s_whist[WAVES][RADIX];
   __shared__ WaveCount s_off[RADIX <= kWave ? WAVES : 1][RADIX];
   __shared__ uint32_t s_wsum[WAVES];
-  if (blockIdx.x >= *nb) return;
-  const uint32_t start = bstart[blockIdx.x], len = blen[blockIdx.x];
+  if (blockIdx.x >= min(*nb, nb_cap)) return;
+  const uint32_t b = ilist ? ilist[blockIdx.x] : blockIdx.x;
+  const uint32_t start = bstart[b], len = blen[b];
   if (len > (uint32_t)CAP) {
-    if (threadIdx.x == 0) atomicAdd(oversized, 1u);
+    if (threadIdx.x == 0) {
+      const uint32_t slot = atomicAdd(oversized, 1u);
+      if (olist && slot < olist_cap) olist[slot] = b;
+    }
     return;
   }
   if (len == 0) return;
@@ -2684,16 +2691,19 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   static_assert(DEPTHS % 2 == 0, "the last depth writes out");
   constexpr uint32_t NB = 1u << 16;  // buckets
   *handled = false;
-  constexpr int kSmallItems = 10, kLargeItems = 19;  // bucket-sort blocks: 256 x items keys
+  // bucket-sort blocks (256 x items keys): the first size fits all but ~1 in
+  // 10^5 buckets of uniform keys (n / 65536 + 4 sigma); those go to the second
+  constexpr int kSmallItems = 9, kSmallItems2 = 12, kLargeItems = 17, kLargeItems2 = 24;
+  constexpr uint32_t kListCap = 1024;
   const bool small = n <= (1ull << 27) + (1ull << 23);
-  const uint32_t cap = 256u * (small ? kSmallItems : kLargeItems);
+  const uint32_t cap = 256u * (small ? kSmallItems2 : kLargeItems2);
   const uint32_t T0 = (uint32_t)((n + TILE - 1) / TILE);
   auto tbound = [&](int k) { return k == 0 ? T0 : T0 + (1u << (BITS * k)); };
   const uint32_t TB = tbound(DEPTHS - 1);
   LS_TRY(ws.ensure_tiles((size_t)TB * RADIX, ((size_t)tp_chunks(TB, BITS) + 1) * RADIX));
   // hybrid block: tiles[2] | segbase | cstart[2] | nsize | ctile0[2] | ntl | counters
   const size_t w_tiles = (size_t)TB * 4;
-  const size_t words = 2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16;
+  const size_t words = 2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16 + kListCap;
   LS_TRY(ws.ensure_hybrid(words));
   uint32_t* h = ws.hyb;
   uint4* tiles[2] = {reinterpret_cast<uint4*>(h), reinterpret_cast<uint4*>(h + w_tiles)};
@@ -2703,7 +2713,9 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   uint32_t* nsize = h; h += NB;
   uint32_t* ctile0[2] = {h, h + NB + 1}; h += 2 * ((size_t)NB + 1);
   uint32_t* ntl = h; h += NB;
-  uint32_t* ctr = h;  // [k] tiles of depth k, [8] oversized buckets, [9] bucket count
+  uint32_t* ctr = h;  // [k] tiles of depth k, [8] buckets over the first block, [9] bucket count, [10] over the second
+  h += 16;
+  uint32_t* olist = h;  // the buckets over the first block (kListCap)
   LS_TRY(hipMemsetAsync(ctr, 0, 16 * sizeof(uint32_t), st));
   LS_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctr + 9), (int)NB, 1, st));
   ws.part_pending.valid = false;
@@ -2801,18 +2813,25 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
     ScopedTimer tm("bucketsort", st, n);
     const uint32_t* bstart = cstart[DEPTHS & 1];
     const uint32_t lbits = (uint32_t)(W - 16);
-    if (small)
-      hipLaunchKernelGGL((k_bucket_sort<BITS, 256, kSmallItems, Op>), dim3(NB), dim3(256), 0, st, out, out, bstart,
-                         nsize, ctr + 9, lbits, bias, ctr + 8);
-    else
-      hipLaunchKernelGGL((k_bucket_sort<BITS, 256, kLargeItems, Op>), dim3(NB), dim3(256), 0, st, out, out, bstart,
-                         nsize, ctr + 9, lbits, bias, ctr + 8);
+#define LS_BS(I, G, NBP, CAPN, IL, OV, OL)                                                                          \
+  hipLaunchKernelGGL((k_bucket_sort<BITS, 256, I, Op>), dim3(G), dim3(256), 0, st, out, out, bstart, nsize, NBP, CAPN, \
+                     IL, lbits, bias, OV, OL, kListCap)
+    if (small) {
+      LS_BS(kSmallItems, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
+      LS_TRY(hipGetLastError());
+      LS_BS(kSmallItems2, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+    } else {
+      LS_BS(kLargeItems, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
+      LS_TRY(hipGetLastError());
+      LS_BS(kLargeItems2, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+    }
+#undef LS_BS
     LS_TRY(hipGetLastError());
   }
-  LS_TRY(hipMemcpyAsync(ws.hyb_host + 16, ctr + 8, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  LS_TRY(hipMemcpyAsync(ws.hyb_host + 16, ctr + 8, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   LS_TRY(hipStreamSynchronize(st));
   *handled = true;
-  if (ws.hyb_host[16] != 0) {
+  if (ws.hyb_host[16] > kListCap || ws.hyb_host[18] != 0) {
     // buckets too large for one block: finish with the LSD sort of out
     LS_TRY((sort_impl<uint32_t, NoValue>(ws, out, out, tmp, nullptr, nullptr, nullptr, n, 0, W, BITS, st, bias)));
   }

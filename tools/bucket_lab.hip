@@ -45,7 +45,7 @@ int main(int argc, char** argv) {
 #define BVG(BITS, B, I, S_, LB, G)                                                                                \
   vs.push_back({#BITS "-bit " #B "x" #I " S=" #S_ " lbits=" #LB " grid=" #G, S_, [&](uint32_t m) {               \
                   hipLaunchKernelGGL((k_bucket_sort<BITS, B, I>), dim3(G ? std::min<uint32_t>(m, G) : m), dim3(B), 0, \
-                                     st, in, out, bs, bl, nb, LB##u, ov);                                           \
+                                     st, in, out, bs, bl, nb, 1u << 30, nullptr, LB##u, 0u, ov, nullptr, 0u);                                           \
                 }});
 #define BVL(BITS, B, I, S_, LB) BVG(BITS, B, I, S_, LB, 0)
 #define BV(BITS, B, I, S_) BVL(BITS, B, I, S_, 16)
