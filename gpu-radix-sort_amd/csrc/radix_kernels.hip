@@ -2691,12 +2691,16 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   static_assert(DEPTHS % 2 == 0, "the last depth writes out");
   constexpr uint32_t NB = 1u << 16;  // buckets
   *handled = false;
-  // bucket-sort blocks (256 x items keys): the first size fits all but ~1 in
-  // 10^5 buckets of uniform keys (n / 65536 + 4 sigma); those go to the second
-  constexpr int kSmallItems = 9, kSmallItems2 = 12, kLargeItems = 17, kLargeItems2 = 24;
+  // bucket-sort blocks (256 x items keys), in two sizes: the first holds the
+  // mean bucket of uniform keys + 3.5 sigma (all but a few of the 65536
+  // buckets), those few are listed for the second, 6 x 256 keys larger.
+  // Classes: first size 9 / 13 / 17 / 19 keys per thread.
   constexpr uint32_t kListCap = 1024;
-  const bool small = n <= (1ull << 27) + (1ull << 23);
-  const uint32_t cap = 256u * (small ? kSmallItems2 : kLargeItems2);
+  const double mean = (double)n / NB;
+  const double need = mean + 3.5 * std::sqrt(mean);
+  const int cls = need <= 256.0 * 9 ? 0 : need <= 256.0 * 13 ? 1 : need <= 256.0 * 17 ? 2 : 3;
+  static constexpr int kItems1[4] = {9, 13, 17, 19};
+  const uint32_t cap = 256u * (uint32_t)(kItems1[cls] + 6);
   const uint32_t T0 = (uint32_t)((n + TILE - 1) / TILE);
   auto tbound = [&](int k) { return k == 0 ? T0 : T0 + (1u << (BITS * k)); };
   const uint32_t TB = tbound(DEPTHS - 1);
@@ -2816,15 +2820,17 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
 #define LS_BS(I, G, NBP, CAPN, IL, OV, OL)                                                                          \
   hipLaunchKernelGGL((k_bucket_sort<BITS, 256, I, Op>), dim3(G), dim3(256), 0, st, out, out, bstart, nsize, NBP, CAPN, \
                      IL, lbits, bias, OV, OL, kListCap)
-    if (small) {
-      LS_BS(kSmallItems, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
-      LS_TRY(hipGetLastError());
-      LS_BS(kSmallItems2, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
-    } else {
-      LS_BS(kLargeItems, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
-      LS_TRY(hipGetLastError());
-      LS_BS(kLargeItems2, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+#define LS_BS2(I)                                          \
+  LS_BS(I, NB, ctr + 9, NB, nullptr, ctr + 8, olist);      \
+  LS_TRY(hipGetLastError());                               \
+  LS_BS(I + 6, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr)
+    switch (cls) {
+      case 0: LS_BS2(9); break;
+      case 1: LS_BS2(13); break;
+      case 2: LS_BS2(17); break;
+      default: LS_BS2(19); break;
     }
+#undef LS_BS2
 #undef LS_BS
     LS_TRY(hipGetLastError());
   }

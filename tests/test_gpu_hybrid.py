@@ -55,12 +55,19 @@ def _tensor(a):
 def _sort_counting_buckets(dev, *args, **kw):
     """dev.sort_keys_u32 with the per-kernel timing registry on: returns the
     output and how many bucket-sort launches (the hybrid's last step) ran."""
+    out, nbs, _ = _sort_counting(dev, *args, **kw)
+    return out, nbs
+
+
+def _sort_counting(dev, *args, **kw):
+    """... and how many digit passes ran (16 / bits when the hybrid needed no
+    fallback)."""
     dev.timing_enable(True)
     dev.timing_reset()
     try:
         out = dev.sort_keys_u32(*args, **kw)
         torch.cuda.synchronize()
-        return out, dev.timing_query("bucketsort")[0]
+        return out, dev.timing_query("bucketsort")[0], dev.timing_query("tilepass")[0]
     finally:
         dev.timing_enable(False)
 
@@ -129,8 +136,9 @@ def test_hybrid_auto_large(dev, oracle_mod, bits, n):
     the device, sha256 against the oracle's counting-sort restatement."""
     import hashlib
     x = dev.populate_u32(n, first=n % 1000)
-    out, nbs = _sort_counting_buckets(dev, x)
+    out, nbs, npass = _sort_counting(dev, x)
     assert nbs == 1
+    assert npass == 16 // bits, "uniform keys must not need the LSD fallback"
     h = hashlib.sha256()
     for i in range(0, n, 1 << 26):
         h.update(out[i:i + (1 << 26)].cpu().numpy().view("<u4").tobytes())
