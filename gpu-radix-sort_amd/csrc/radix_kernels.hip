@@ -1307,20 +1307,23 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 // larger than the block is left alone, counted in *oversized and (when olist
 // is given, up to olist_cap) listed for a block of the next size.  in may equal
 // out (a block holds its whole bucket before it writes).
-template <int BITS, int BLOCK, int ITEMS, typename Op = RadixDigit>
-__global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* in, uint32_t* out,
+template <int BITS, int BLOCK, int ITEMS, typename Op = RadixDigit, typename K = uint32_t, typename V = NoValue>
+__global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, const V* vin, V* vout,
                                                        const uint32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ blen,
                                                        const uint32_t* __restrict__ nb, uint32_t nb_cap,
                                                        const uint32_t* __restrict__ ilist, uint32_t lbits,
                                                        uint32_t bias, uint32_t* __restrict__ oversized,
                                                        uint32_t* __restrict__ olist, uint32_t olist_cap) {
+  constexpr bool HAS_V = !std::is_same<V, NoValue>::value;
+  using VS = typename std::conditional<HAS_V, V, uint8_t>::type;
   constexpr int RADIX = 1 << BITS;
   constexpr int WAVES = BLOCK / kWave;
   constexpr int CAP = BLOCK * ITEMS;
   constexpr int WSPAN = ITEMS * kWave;
   static_assert(RADIX <= BLOCK && CAP < 65536, "one digit per thread; 16-bit wave counters");
-  __shared__ uint32_t s_keys[CAP];
+  __shared__ K s_keys[CAP];
+  __shared__ VS s_vals[HAS_V ? CAP : 1];
   __shared__ WaveCount s_whist[WAVES][RADIX];
   __shared__ WaveCount s_off[RADIX <= kWave ? WAVES : 1][RADIX];
   __shared__ uint32_t s_wsum[WAVES];
@@ -1339,11 +1342,15 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* in, uint3
   const int lane = tid & (kWave - 1);
   const int w = tid / kWave;
   const uint32_t wbase = w * WSPAN;
-  uint32_t k[ITEMS], rk[ITEMS];
+  const K pad = (K)bias - (K)1;  // every digit of key - bias maximal
+  K k[ITEMS];
+  VS v[ITEMS];
+  uint32_t rk[ITEMS];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t i = wbase + j * kWave + lane;
-    k[j] = i < len ? load_stream(&in[(size_t)start + i]) : bias - 1u;  // pad: every digit of key - bias maximal
+    k[j] = i < len ? load_stream(&in[(size_t)start + i]) : pad;
+    if constexpr (HAS_V) v[j] = i < len ? load_stream(&vin[(size_t)start + i]) : (VS)0;
   }
   for (uint32_t shift = 0; shift < lbits; shift += BITS) {
     const uint32_t nbits = min((uint32_t)BITS, lbits - shift);
@@ -1372,7 +1379,11 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* in, uint3
       }
       if (lane < RADIX) s_off[w][lane] = (WaveCount)(x - col + mine);
 #pragma unroll
-      for (int j = 0; j < ITEMS; ++j) s_keys[s_off[w][op(k[j])] + rk[j]] = k[j];
+      for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t pos = s_off[w][op(k[j])] + rk[j];
+        s_keys[pos] = k[j];
+        if constexpr (HAS_V) s_vals[pos] = v[j];
+      }
     } else {
       uint32_t cnt_d = 0;
       if (tid < RADIX) {
@@ -1392,16 +1403,26 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint32_t* in, uint3
       }
       __syncthreads();
 #pragma unroll
-      for (int j = 0; j < ITEMS; ++j) s_keys[s_whist[w][op(k[j])] + rk[j]] = k[j];
+      for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t pos = s_whist[w][op(k[j])] + rk[j];
+        s_keys[pos] = k[j];
+        if constexpr (HAS_V) s_vals[pos] = v[j];
+      }
     }
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) k[j] = s_keys[wbase + j * kWave + lane];
+    for (int j = 0; j < ITEMS; ++j) {
+      k[j] = s_keys[wbase + j * kWave + lane];
+      if constexpr (HAS_V) v[j] = s_vals[wbase + j * kWave + lane];
+    }
   }
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t i = wbase + j * kWave + lane;
-    if (i < len) out[(size_t)start + i] = k[j];
+    if (i < len) {
+      out[(size_t)start + i] = k[j];
+      if constexpr (HAS_V) vout[(size_t)start + i] = v[j];
+    }
   }
 }
 
@@ -2681,12 +2702,13 @@ constexpr size_t kHybMinKeys = 1ull << 27;
 constexpr size_t kHybMaxKeys = (1ull << 28) + (1ull << 24);
 
 
-template <int BITS, typename Op>
-hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n, int W,
-                           uint32_t bias, hipStream_t st, bool* handled) {
+template <int BITS, typename Op, typename K = uint32_t, typename V = NoValue>
+hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin, V* vout, V* vtmp, size_t n, int W,
+                       uint32_t bias, hipStream_t st, bool* handled) {
   constexpr int RADIX = 1 << BITS;
-  constexpr int B = tp_block<uint32_t>(BITS);
-  constexpr int TILE = B * 16;
+  constexpr int B = tp_block<K>(BITS);
+  constexpr int ITEMS = tp_items<K, V>(BITS);
+  constexpr int TILE = B * ITEMS;
   constexpr int DEPTHS = 16 / BITS;
   static_assert(DEPTHS % 2 == 0, "the last depth writes out");
   constexpr uint32_t NB = 1u << 16;  // buckets
@@ -2724,7 +2746,8 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   LS_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctr + 9), (int)NB, 1, st));
   ws.part_pending.valid = false;
 
-  auto buf = [&](int k) -> uint32_t* { return k == 0 ? const_cast<uint32_t*>(in) : (k & 1) ? tmp : out; };
+  auto buf = [&](int k) -> K* { return k == 0 ? const_cast<K*>(in) : (k & 1) ? tmp : out; };
+  auto vbuf = [&](int k) -> V* { return k == 0 ? const_cast<V*>(vin) : (k & 1) ? vtmp : vout; };
   for (int k = 0; k < DEPTHS; ++k) {
     const bool last = k == DEPTHS - 1;
     const uint32_t rows = tbound(k);
@@ -2734,17 +2757,19 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
     const Op op_next = make_digit<Op>((uint32_t)(last ? 0 : W - BITS * (k + 2)), (uint32_t)RADIX - 1u, bias);
     uint32_t* C = (BITS == 4) ? ws.tc[k & 1] : ws.tc[0];
     uint32_t* Cn = ws.tc[(k + 1) & 1];
-    const uint32_t* src = buf(k);
-    uint32_t* dst = buf(k + 1);
+    const K* src = buf(k);
+    K* dst = buf(k + 1);
+    const V* vsrc = vbuf(k);
+    V* vdst = vbuf(k + 1);
     // counts of this depth: depth 0 reads the keys; 4-bit deeper depths were
     // counted by the previous pass (fused); 8-bit deeper depths read the keys
     // tile by tile from the table
     if (k == 0) {
-      LS_TRY((tiles_counts<BITS, uint32_t, Op>(ws, src, n, op, T0, C, BITS == 4 ? Cn : nullptr,
+      LS_TRY((tiles_counts<BITS, K, Op, V>(ws, src, n, op, T0, C, BITS == 4 ? Cn : nullptr,
                                            BITS == 4 ? T0 * (uint32_t)RADIX : 0u, st)));
     } else if (BITS == 8) {
       ScopedTimer tm("tilecounts", st, n);
-      hipLaunchKernelGGL((k_tile_counts<BITS, B, 16, uint32_t, Op, true>), dim3(rows), dim3(B), 0, st, src,
+      hipLaunchKernelGGL((k_tile_counts<BITS, B, ITEMS, K, Op, true>), dim3(rows), dim3(B), 0, st, src,
                          (uint32_t)n, op, C, nullptr, 0u, tiles[k & 1], ctr + k);
       LS_TRY(hipGetLastError());
     }
@@ -2776,20 +2801,20 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
       ScopedTimer tm("tilepass", st, n);
       if (BITS == 4 && !last) {
         if (k == 0)
-          hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, BITS == 4, Op, Op, 2>),
-                             dim3(rows), dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C,
+          hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 2>),
+                             dim3(rows), dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C,
                              ws.tb, segbase, Cn, geo);
         else
-          hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, BITS == 4, Op, Op, 3>),
-                             dim3(rows), dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C,
+          hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 3>),
+                             dim3(rows), dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C,
                              ws.tb, segbase, Cn, geo);
       } else if (k == 0) {
-        hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, false, Op, Op, 0>), dim3(rows),
-                           dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C, ws.tb, segbase,
+        hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, false, Op, Op, 0>), dim3(rows),
+                           dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase,
                            Cn, geo);
       } else {
-        hipLaunchKernelGGL((k_tile_pass<BITS, B, 16, uint32_t, NoValue, false, Op, Op, 1>), dim3(rows),
-                           dim3(B), 0, st, src, dst, nullptr, nullptr, (uint32_t)n, op, op_next, C, ws.tb, segbase,
+        hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, false, Op, Op, 1>), dim3(rows),
+                           dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase,
                            Cn, geo);
       }
       LS_TRY(hipGetLastError());
@@ -2818,8 +2843,8 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
     const uint32_t* bstart = cstart[DEPTHS & 1];
     const uint32_t lbits = (uint32_t)(W - 16);
 #define LS_BS(I, G, NBP, CAPN, IL, OV, OL)                                                                          \
-  hipLaunchKernelGGL((k_bucket_sort<BITS, 256, I, Op>), dim3(G), dim3(256), 0, st, out, out, bstart, nsize, NBP, CAPN, \
-                     IL, lbits, bias, OV, OL, kListCap)
+  hipLaunchKernelGGL((k_bucket_sort<BITS, 256, I, Op, K, V>), dim3(G), dim3(256), 0, st, out, out, vout, vout, bstart, \
+                     nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
 #define LS_BS2(I)                                          \
   LS_BS(I, NB, ctr + 9, NB, nullptr, ctr + 8, olist);      \
   LS_TRY(hipGetLastError());                               \
@@ -2839,7 +2864,7 @@ hipError_t sort_hybrid_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   *handled = true;
   if (ws.hyb_host[16] > kListCap || ws.hyb_host[18] != 0) {
     // buckets too large for one block: finish with the LSD sort of out
-    LS_TRY((sort_impl<uint32_t, NoValue>(ws, out, out, tmp, nullptr, nullptr, nullptr, n, 0, W, BITS, st, bias)));
+    LS_TRY((sort_impl<K, V>(ws, out, out, tmp, vout, vout, vtmp, n, 0, W, BITS, st, bias)));
   }
   return hipSuccess;
 }
@@ -2857,14 +2882,15 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
       ((hyb == 1 && n >= kHybMinKeys && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
       (get_algorithm() == 0 || get_algorithm() == 3) && in != tmp) {
     bool handled = false;
+    NoValue* nv = nullptr;
     if (bias && digit_bits == 4)
-      LS_TRY((sort_hybrid_u32<4, BiasedDigit>(ws, in, out, tmp, n, hi, bias, st, &handled)));
+      LS_TRY((sort_hybrid<4, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, bias, st, &handled)));
     else if (bias)
-      LS_TRY((sort_hybrid_u32<8, BiasedDigit>(ws, in, out, tmp, n, hi, bias, st, &handled)));
+      LS_TRY((sort_hybrid<8, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, bias, st, &handled)));
     else if (digit_bits == 4)
-      LS_TRY((sort_hybrid_u32<4, RadixDigit>(ws, in, out, tmp, n, hi, 0u, st, &handled)));
+      LS_TRY((sort_hybrid<4, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, 0u, st, &handled)));
     else
-      LS_TRY((sort_hybrid_u32<8, RadixDigit>(ws, in, out, tmp, n, hi, 0u, st, &handled)));
+      LS_TRY((sort_hybrid<8, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, 0u, st, &handled)));
     if (handled) {
       ws.last_algo = 4;
       return hipSuccess;
@@ -2909,20 +2935,44 @@ hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t
   return sort_impl<uint32_t, uint32_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, lo, hi, digit_bits, st);
 }
 
+// 64-bit keys (alone or with u32 payloads), full-width sorts with 8-bit
+// digits: the MSD hybrid (two digit passes over the top 16 bits, buckets
+// sorted on chip on the low 48 bits, stable: the passes and the on-chip steps
+// keep the order of equal keys, so a payload keeps its input order).
+template <typename V>
+hipError_t sort_64_hybrid_or_lsd(Workspace& ws, const uint64_t* kin, uint64_t* kout, uint64_t* ktmp, const V* vin,
+                                 V* vout, V* vtmp, size_t n, int lo, int hi, int digit_bits, hipStream_t st) {
+  const int hyb = get_hybrid_mode();
+  if (lo == 0 && hi == 64 && digit_bits == 8 &&
+      ((hyb == 1 && n >= kHybMinKeys && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
+      (get_algorithm() == 0 || get_algorithm() == 3) && (const void*)kin != (const void*)ktmp) {
+    bool handled = false;
+    LS_TRY((sort_hybrid<8, RadixDigit, uint64_t, V>(ws, kin, kout, ktmp, vin, vout, vtmp, n, 64, 0u, st, &handled)));
+    if (handled) {
+      ws.last_algo = 4;
+      return hipSuccess;
+    }
+  }
+  return sort_impl<uint64_t, V>(ws, kin, kout, ktmp, vin, vout, vtmp, n, lo, hi, digit_bits, st);
+}
+
 hipError_t sort_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
                               uint32_t* vout, uint64_t* ktmp, uint32_t* vtmp, size_t n, int lo, int hi,
                               int digit_bits, hipStream_t st) {
-  return sort_impl<uint64_t, uint32_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, lo, hi, digit_bits, st);
+  return sort_64_hybrid_or_lsd<uint32_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, lo, hi, digit_bits, st);
 }
 
 hipError_t sort_u64(Workspace& ws, const uint64_t* in, uint64_t* out, uint64_t* tmp, size_t n, int lo, int hi,
                     int digit_bits, hipStream_t st) {
-  return sort_impl<uint64_t, NoValue>(ws, in, out, tmp, nullptr, nullptr, nullptr, n, lo, hi, digit_bits, st);
+  NoValue* nv = nullptr;
+  return sort_64_hybrid_or_lsd<NoValue>(ws, in, out, tmp, nv, nv, nv, n, lo, hi, digit_bits, st);
 }
 
 hipError_t sort_pairs_u64_u64(Workspace& ws, const uint64_t* kin, const uint64_t* vin, uint64_t* kout,
                               uint64_t* vout, uint64_t* ktmp, uint64_t* vtmp, size_t n, int lo, int hi,
                               int digit_bits, hipStream_t st) {
+  // (u64, u64) pairs stay LSD: through the hybrid, 2^27 pairs took 10.66 ms
+  // against 9.46 (16 bytes per pair through LDS in each of 6 on-chip steps)
   return sort_impl<uint64_t, uint64_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, lo, hi, digit_bits, st);
 }
 

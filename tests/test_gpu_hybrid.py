@@ -205,3 +205,76 @@ def test_hybrid_auto_range_large(dev, oracle_mod, bits):
     assert nbs == 1
     host = y.cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(host))
+
+
+def _pairs_counting(dev, kt, vt):
+    dev.timing_enable(True)
+    dev.timing_reset()
+    try:
+        ok_, ov = dev.sort_pairs_u64_u32(kt, vt)
+        torch.cuda.synchronize()
+        return ok_, ov, dev.timing_query("bucketsort")[0], dev.timing_query("tilepass")[0]
+    finally:
+        dev.timing_enable(False)
+
+
+@pytest.fixture
+def bits8(dev):
+    import pylibsort
+    prev = pylibsort.setDigitBits(8)
+    yield 8
+    pylibsort.setDigitBits(prev)
+
+
+@pytest.mark.parametrize("kind", ["uniform", "dups", "top_skew", "deep_skew", "equal"])
+@pytest.mark.parametrize("n", [1024, 65539, (1 << 21) + 7])
+def test_hybrid_forced_pairs_u64_u32(dev, oracle_mod, bits8, force, kind, n):
+    """(u64 key, u32 payload) pairs (configs[4]'s record) through the hybrid:
+    two digit passes over the top 16 key bits, buckets sorted on chip on the
+    low 48 bits; stable (payload = input index, ties keep it increasing)."""
+    rng = np.random.default_rng(n + len(kind))
+    k = rng.integers(0, 1 << 63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+    if kind == "dups":
+        k = rng.integers(0, 1 << 10, n, dtype=np.uint64) * np.uint64(0x0040000100000001)
+    elif kind == "top_skew":
+        k >>= np.uint64(4)
+    elif kind == "deep_skew":
+        k &= np.uint64(0xFF00FFFFFFFFFFFF)
+    elif kind == "equal":
+        k[:] = np.uint64(0x123456789ABCDEF0)
+    v = np.arange(n, dtype=np.uint32)
+    kt = torch.from_numpy(k.view(np.int64)).cuda()
+    vt = torch.from_numpy(v.view(np.int32)).cuda()
+    ok_, ov, nbs, _ = _pairs_counting(dev, kt, vt)
+    rk, rv = oracle_mod.stable_sort_kv64(k, v)
+    np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), rk)
+    np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint32), rv)
+    if kind in ("uniform", "dups", "deep_skew"):
+        assert nbs == 1
+
+
+@pytest.mark.parametrize("n", [4097, (1 << 21) + 7])
+def test_hybrid_forced_keys_u64(dev, oracle_mod, bits8, force, n):
+    rng = np.random.default_rng(n)
+    k = rng.integers(0, 1 << 63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+    k[: n // 5] &= np.uint64(0xFFFF0000FFFF)
+    kt = torch.from_numpy(k.view(np.int64)).cuda()
+    out = dev.sort_keys_u64(kt)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), oracle_mod.sort_u64(k))
+
+
+def test_hybrid_auto_pairs_large(dev, oracle_mod, bits8):
+    """configs[4]'s per-GPU record at 2^27 pairs (key = two consecutive PCG
+    draws, payload = index) through the auto mode: no fallback, and equal to
+    the oracle's stable sort."""
+    n = 1 << 27
+    d = dev.populate_u32(2 * n, first=11).to(torch.int64) & 0xFFFFFFFF
+    kt = (d[0::2] << 32) | d[1::2]
+    vt = torch.arange(n, dtype=torch.int32, device="cuda")
+    ok_, ov, nbs, npass = _pairs_counting(dev, kt, vt)
+    assert nbs == 1 and npass == 2
+    k = kt.cpu().numpy().view(np.uint64)
+    rk, rv = oracle_mod.stable_sort_kv64(k, np.arange(n, dtype=np.uint32))
+    np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), rk)
+    np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint32), rv)
+
