@@ -2698,6 +2698,9 @@ hipError_t group_bounds(Workspace& ws, const uint32_t* sorted, size_t n, int lo,
 // (*handled = false: the caller runs the LSD sort; in is untouched); after
 // the bucket sort, buckets too large for a block (counted on the device) are
 // sorted by an LSD sort of out in place.
+#ifndef LIBSORT_BUCKET64_BLOCK
+#define LIBSORT_BUCKET64_BLOCK 512
+#endif
 constexpr size_t kHybMinKeys = 1ull << 27;
 constexpr size_t kHybMaxKeys = (1ull << 28) + (1ull << 24);
 
@@ -2842,9 +2845,12 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     ScopedTimer tm("bucketsort", st, n);
     const uint32_t* bstart = cstart[DEPTHS & 1];
     const uint32_t lbits = (uint32_t)(W - 16);
-#define LS_BS(I, G, NBP, CAPN, IL, OV, OL)                                                                          \
-  hipLaunchKernelGGL((k_bucket_sort<BITS, 256, I, Op, K, V>), dim3(G), dim3(256), 0, st, out, out, vout, vout, bstart, \
-                     nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
+    // 64-bit keys: 512-thread blocks (the same slots in half the keys per
+    // thread: 152 -> ~90 VGPRs for (u64, u32) pairs at 17 slots per 256)
+    constexpr int BB = sizeof(K) == 8 ? LIBSORT_BUCKET64_BLOCK : 256;
+#define LS_BS(I, G, NBP, CAPN, IL, OV, OL)                                                                     \
+  hipLaunchKernelGGL((k_bucket_sort<BITS, BB, (I * 256 + BB - 1) / BB, Op, K, V>), dim3(G), dim3(BB), 0, st, out, \
+                     out, vout, vout, bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
 #define LS_BS2(I)                                          \
   LS_BS(I, NB, ctr + 9, NB, nullptr, ctr + 8, olist);      \
   LS_TRY(hipGetLastError());                               \
