@@ -1307,7 +1307,15 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 // larger than the block is left alone, counted in *oversized and (when olist
 // is given, up to olist_cap) listed for a block of the next size.  in may equal
 // out (a block holds its whole bucket before it writes).
-template <int BITS, int BLOCK, int ITEMS, typename Op = RadixDigit, typename K = uint32_t, typename V = NoValue>
+// FIX > 0 (64-bit keys, whose buckets keep 48 bits to sort): the on-chip LSD
+// steps cover only the top FIX of the lbits bits; keys then equal in all
+// their higher bits form runs (4096 uniform keys over 2^16 values of the top
+// FIX = 16 bits: ~128 runs of 2, a few of 3), which are insertion-sorted on
+// the whole key in LDS by the thread holding the run's first key -- stable,
+// since only larger keys move.  A bucket with a run longer than 64 reloads
+// its keys and runs every step instead.
+template <int BITS, int BLOCK, int ITEMS, typename Op = RadixDigit, typename K = uint32_t, typename V = NoValue,
+          int FIX = 0>
 __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, const V* vin, V* vout,
                                                        const uint32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ blen,
@@ -1321,7 +1329,9 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
   constexpr int WAVES = BLOCK / kWave;
   constexpr int CAP = BLOCK * ITEMS;
   constexpr int WSPAN = ITEMS * kWave;
+  constexpr uint32_t kMaxRun = 64;
   static_assert(RADIX <= BLOCK && CAP < 65536, "one digit per thread; 16-bit wave counters");
+  static_assert(FIX == 0 || (sizeof(K) == 8 && FIX % BITS == 0), "tie fix-up: 64-bit keys");
   __shared__ K s_keys[CAP];
   __shared__ VS s_vals[HAS_V ? CAP : 1];
   __shared__ WaveCount s_whist[WAVES][RADIX];
@@ -1346,75 +1356,154 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
   K k[ITEMS];
   VS v[ITEMS];
   uint32_t rk[ITEMS];
+  auto load = [&]() {
 #pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {
-    const uint32_t i = wbase + j * kWave + lane;
-    k[j] = i < len ? load_stream(&in[(size_t)start + i]) : pad;
-    if constexpr (HAS_V) v[j] = i < len ? load_stream(&vin[(size_t)start + i]) : (VS)0;
-  }
-  for (uint32_t shift = 0; shift < lbits; shift += BITS) {
-    const uint32_t nbits = min((uint32_t)BITS, lbits - shift);
-    const Op op = make_digit<Op>(shift, (1u << nbits) - 1u, bias);
-    for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0;
-    rank_items_t<BITS, true, ITEMS>(k, rk, s_whist[w], 0u, wbase, lane, op);
-    __syncthreads();
-    if constexpr (RADIX <= kWave) {
-      // every wave derives its own run offsets (lane d: the digit-d keys of
-      // all waves for smaller digits, plus those of earlier waves): no
-      // block scan, two barriers per step
-      uint32_t col = 0, mine = 0;
-      if (lane < RADIX) {
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t i = wbase + j * kWave + lane;
+      k[j] = i < len ? load_stream(&in[(size_t)start + i]) : pad;
+      if constexpr (HAS_V) v[j] = i < len ? load_stream(&vin[(size_t)start + i]) : (VS)0;
+    }
+  };
+  // LSD steps over bits [lo_bit, hi_bit) of (key - bias); on return k, v hold
+  // the bucket in that order (slot j of wave w = position wbase + j*64 + lane)
+  // and s_keys / s_vals the same
+  auto steps = [&](uint32_t lo_bit, uint32_t hi_bit) {
+    for (uint32_t shift = lo_bit; shift < hi_bit; shift += BITS) {
+      const uint32_t nbits = min((uint32_t)BITS, hi_bit - shift);
+      const Op op = make_digit<Op>(shift, (1u << nbits) - 1u, bias);
+      for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0;
+      rank_items_t<BITS, true, ITEMS>(k, rk, s_whist[w], 0u, wbase, lane, op);
+      __syncthreads();
+      if constexpr (RADIX <= kWave) {
+        // every wave derives its own run offsets (lane d: the digit-d keys of
+        // all waves for smaller digits, plus those of earlier waves): no
+        // block scan, two barriers per step
+        uint32_t col = 0, mine = 0;
+        if (lane < RADIX) {
 #pragma unroll
-        for (int i = 0; i < WAVES; ++i) {
-          const uint32_t c = s_whist[i][lane];
-          col += c;
-          mine += i < w ? c : 0u;
+          for (int i = 0; i < WAVES; ++i) {
+            const uint32_t c = s_whist[i][lane];
+            col += c;
+            mine += i < w ? c : 0u;
+          }
         }
-      }
-      uint32_t x = col;
+        uint32_t x = col;
 #pragma unroll
-      for (int o = 1; o < RADIX; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, RADIX);
-        if ((lane & (RADIX - 1)) >= o) x += y;
-      }
-      if (lane < RADIX) s_off[w][lane] = (WaveCount)(x - col + mine);
+        for (int o = 1; o < RADIX; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o, RADIX);
+          if ((lane & (RADIX - 1)) >= o) x += y;
+        }
+        if (lane < RADIX) s_off[w][lane] = (WaveCount)(x - col + mine);
 #pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        const uint32_t pos = s_off[w][op(k[j])] + rk[j];
-        s_keys[pos] = k[j];
-        if constexpr (HAS_V) s_vals[pos] = v[j];
-      }
-    } else {
-      uint32_t cnt_d = 0;
-      if (tid < RADIX) {
+        for (int j = 0; j < ITEMS; ++j) {
+          const uint32_t pos = s_off[w][op(k[j])] + rk[j];
+          s_keys[pos] = k[j];
+          if constexpr (HAS_V) s_vals[pos] = v[j];
+        }
+      } else {
+        uint32_t cnt_d = 0;
+        if (tid < RADIX) {
 #pragma unroll
-        for (int i = 0; i < WAVES; ++i) cnt_d += s_whist[i][tid];
-      }
-      uint32_t total;
-      const uint32_t excl = block_exclusive_scan<BLOCK>(cnt_d, s_wsum, total);
-      if (tid < RADIX) {
-        uint32_t run = excl;
+          for (int i = 0; i < WAVES; ++i) cnt_d += s_whist[i][tid];
+        }
+        uint32_t total;
+        const uint32_t excl = block_exclusive_scan<BLOCK>(cnt_d, s_wsum, total);
+        if (tid < RADIX) {
+          uint32_t run = excl;
 #pragma unroll
-        for (int i = 0; i < WAVES; ++i) {
-          const uint32_t c = s_whist[i][tid];
-          s_whist[i][tid] = (WaveCount)run;
-          run += c;
+          for (int i = 0; i < WAVES; ++i) {
+            const uint32_t c = s_whist[i][tid];
+            s_whist[i][tid] = (WaveCount)run;
+            run += c;
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+          const uint32_t pos = s_whist[w][op(k[j])] + rk[j];
+          s_keys[pos] = k[j];
+          if constexpr (HAS_V) s_vals[pos] = v[j];
         }
       }
       __syncthreads();
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
-        const uint32_t pos = s_whist[w][op(k[j])] + rk[j];
-        s_keys[pos] = k[j];
-        if constexpr (HAS_V) s_vals[pos] = v[j];
+        k[j] = s_keys[wbase + j * kWave + lane];
+        if constexpr (HAS_V) v[j] = s_vals[wbase + j * kWave + lane];
       }
     }
-    __syncthreads();
+  };
+  load();
+  if constexpr (FIX > 0) {
+    const uint32_t fs = lbits > (uint32_t)FIX ? lbits - FIX : 0u;  // keys equal above fs form the runs
+    steps(fs, lbits);
+    if (fs > 0) {
+      // ties from registers: position p = wbase + j*64 + lane holds k[j]; its
+      // neighbours are the adjacent lanes (the adjacent items across lanes 63
+      // and 0, LDS across waves)
+      auto hi = [&](K x) -> K { return (K)(x - bias) >> fs; };
+      auto shfl64 = [](K x, int src) -> K {
+        const uint32_t lo = __shfl((uint32_t)x, src), up = __shfl((uint32_t)(x >> 32), src);
+        return ((K)up << 32) | lo;
+      };
+      uint32_t long_run = 0;
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-      k[j] = s_keys[wbase + j * kWave + lane];
-      if constexpr (HAS_V) v[j] = s_vals[wbase + j * kWave + lane];
+      for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t p = wbase + j * kWave + lane;
+        K prev = shfl64(k[j], (lane + kWave - 1) & (kWave - 1));
+        K next = shfl64(k[j], (lane + 1) & (kWave - 1));
+        if (j > 0) {
+          const K last_prev = shfl64(k[j - 1], kWave - 1);
+          if (lane == 0) prev = last_prev;
+        } else if (lane == 0 && wbase > 0) {
+          prev = s_keys[wbase - 1];
+        }
+        if (j + 1 < ITEMS) {
+          const K first_next = shfl64(k[j + 1], 0);
+          if (lane == kWave - 1) next = first_next;
+        } else if (lane == kWave - 1 && p + 1 < len) {
+          next = s_keys[p + 1];
+        }
+        const bool tie_prev = p > 0 && p < len && hi(prev) == hi(k[j]);
+        const bool tie_next = p + 1 < len && hi(next) == hi(k[j]);
+        if (tie_next && !tie_prev) {
+          // a run starts here: its length from LDS, then a stable insertion
+          // sort of s_keys[p, p + L) on key - bias
+          uint32_t L = 2;
+          while (L <= kMaxRun && p + L < len && hi(s_keys[p + L]) == hi(k[j])) ++L;
+          if (L > kMaxRun) {
+            long_run = 1;
+          } else {
+            for (uint32_t a = 1; a < L; ++a) {
+              const K x = s_keys[p + a];
+              VS xv;
+              if constexpr (HAS_V) xv = s_vals[p + a];
+              uint32_t c = a;
+              while (c > 0 && (K)(s_keys[p + c - 1] - bias) > (K)(x - bias)) {
+                s_keys[p + c] = s_keys[p + c - 1];
+                if constexpr (HAS_V) s_vals[p + c] = s_vals[p + c - 1];
+                --c;
+              }
+              s_keys[p + c] = x;
+              if constexpr (HAS_V) s_vals[p + c] = xv;
+            }
+          }
+        }
+      }
+      if (__syncthreads_or((int)long_run)) {
+        // a long run of equal high bits: every step from the input order
+        load();
+        steps(0, lbits);
+      } else {
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+          k[j] = s_keys[wbase + j * kWave + lane];
+          if constexpr (HAS_V) v[j] = s_vals[wbase + j * kWave + lane];
+        }
+      }
     }
+  } else {
+    steps(0, lbits);
   }
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
@@ -2698,6 +2787,9 @@ hipError_t group_bounds(Workspace& ws, const uint32_t* sorted, size_t n, int lo,
 // (*handled = false: the caller runs the LSD sort; in is untouched); after
 // the bucket sort, buckets too large for a block (counted on the device) are
 // sorted by an LSD sort of out in place.
+#ifndef LIBSORT_BUCKET64_FIX
+#define LIBSORT_BUCKET64_FIX 16
+#endif
 #ifndef LIBSORT_BUCKET64_BLOCK
 #define LIBSORT_BUCKET64_BLOCK 512
 #endif
@@ -2848,8 +2940,11 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     // 64-bit keys: 512-thread blocks (the same slots in half the keys per
     // thread: 152 -> ~90 VGPRs for (u64, u32) pairs at 17 slots per 256)
     constexpr int BB = sizeof(K) == 8 ? LIBSORT_BUCKET64_BLOCK : 256;
+    // 64-bit keys: on-chip steps over the top 16 of the 48 bucket bits, then
+    // the tie fix-up (k_bucket_sort FIX)
+    constexpr int FIXB = sizeof(K) == 8 ? LIBSORT_BUCKET64_FIX : 0;
 #define LS_BS(I, G, NBP, CAPN, IL, OV, OL)                                                                     \
-  hipLaunchKernelGGL((k_bucket_sort<BITS, BB, (I * 256 + BB - 1) / BB, Op, K, V>), dim3(G), dim3(BB), 0, st, out, \
+  hipLaunchKernelGGL((k_bucket_sort<BITS, BB, (I * 256 + BB - 1) / BB, Op, K, V, FIXB>), dim3(G), dim3(BB), 0, st, out, \
                      out, vout, vout, bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
 #define LS_BS2(I)                                          \
   LS_BS(I, NB, ctr + 9, NB, nullptr, ctr + 8, olist);      \

@@ -45,12 +45,12 @@ int main(int argc, char** argv) {
 #define BVG(BITS, B, I, S_, LB, G)                                                                                \
   vs.push_back({#BITS "-bit " #B "x" #I " S=" #S_ " lbits=" #LB " grid=" #G, S_, [&](uint32_t m) {               \
                   hipLaunchKernelGGL((k_bucket_sort<BITS, B, I>), dim3(G ? std::min<uint32_t>(m, G) : m), dim3(B), 0, \
-                                     st, in, out, bs, bl, nb, 1u << 30, nullptr, LB##u, 0u, ov, nullptr, 0u);                                           \
+                                     st, in, out, (const NoValue*)nullptr, (NoValue*)nullptr, bs, bl, nb, 1u << 30,  \
+                                     nullptr, LB##u, 0u, ov, nullptr, 0u);                                           \
                 }});
 #define BVL(BITS, B, I, S_, LB) BVG(BITS, B, I, S_, LB, 0)
 #define BV(BITS, B, I, S_) BVL(BITS, B, I, S_, 16)
-  BV(4, 256, 19, 4096) BV(4, 256, 16, 4096) BVL(4, 256, 16, 4096, 0) BVL(4, 256, 16, 4096, 4)
-  BVL(4, 256, 16, 4096, 8) BV(8, 256, 19, 4096) BV(8, 256, 16, 4096)
+  BV(4, 256, 16, 4096)
   for (auto& v : vs) {
     const uint32_t m = (uint32_t)(n / v.S);
     hipLaunchKernelGGL(fill, dim3((n + 255) / 256), dim3(256), 0, st, in, n, v.S, 0u);
@@ -79,6 +79,47 @@ int main(int argc, char** argv) {
     const float med = us[us.size() / 2];
     printf("%-26s 2^%d keys: median %7.1f us  best %7.1f  %5.0f GB/s (8 B/key)  %s\n", v.name.c_str(), lg, med, us[0],
            8.0 * n / (med * 1e-6) / 1e9, (sorted && sum0 == sum1 && x0 == x1) ? "sorted" : (sum0 == sum1 && x0 == x1 ? "permutation" : "WRONG"));
+  }
+  // (u64 key, u32 value) buckets: key = bucket << 48 | 48 random bits
+  {
+    const size_t np = n / 2;
+    uint64_t *k64, *o64;
+    uint32_t *vv, *ov32;
+    CK(hipMalloc(&k64, np * 8)); CK(hipMalloc(&o64, np * 8)); CK(hipMalloc(&vv, np * 4)); CK(hipMalloc(&ov32, np * 4));
+    std::vector<uint64_t> hk(np);
+    const uint32_t S = 4096, m = (uint32_t)(np / S);
+    for (size_t i = 0; i < np; ++i) {
+      uint64_t x = (i + 1) * 0x9E3779B97F4A7C15ull;
+      x ^= x >> 29; x *= 0xBF58476D1CE4E5B9ull; x ^= x >> 32;
+      hk[i] = ((uint64_t)(i / S) << 48) | (x & 0xFFFFFFFFFFFFull);
+    }
+    CK(hipMemcpy(k64, hk.data(), np * 8, hipMemcpyHostToDevice));
+    std::vector<uint32_t> hs(m), hl(m, S), hv(np);
+    for (uint32_t b = 0; b < m; ++b) hs[b] = b * S;
+    for (size_t i = 0; i < np; ++i) hv[i] = (uint32_t)i;
+    CK(hipMemcpy(vv, hv.data(), np * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(bs, hs.data(), m * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(bl, hl.data(), m * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(nb, &m, 4, hipMemcpyHostToDevice));
+    auto run = [&](const char* name, std::function<void()> f) {
+      std::vector<float> us;
+      for (int r = 0; r < 12; ++r) {
+        CK(hipEventRecord(e0, st)); f(); CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
+        float ms; CK(hipEventElapsedTime(&ms, e0, e1)); if (r >= 2) us.push_back(ms * 1e3f);
+      }
+      std::sort(us.begin(), us.end());
+      std::vector<uint64_t> ok(np);
+      CK(hipMemcpy(ok.data(), o64, np * 8, hipMemcpyDeviceToHost));
+      bool sorted = true;
+      for (size_t i = 1; i < np; ++i) if (ok[i - 1] > ok[i]) { sorted = false; break; }
+      printf("pairs %-34s 2^%d pairs: median %7.1f us  %s\n", name, lg - 1, us[us.size() / 2], sorted ? "sorted" : "not sorted");
+    };
+#define PV(B, I, LB, FX)                                                                                         \
+    run(#B "x" #I " lbits=" #LB " fix=" #FX, [&] {                                                             \
+      hipLaunchKernelGGL((k_bucket_sort<8, B, I, RadixDigit, uint64_t, uint32_t, FX>), dim3(m), dim3(B), 0, st, k64, o64, \
+                         vv, ov32, bs, bl, nb, 1u << 30, nullptr, LB##u, 0u, ov, nullptr, 0u);                        \
+    });
+    PV(512, 9, 0, 0) PV(512, 9, 8, 0) PV(512, 9, 16, 0) PV(512, 9, 48, 0) PV(512, 9, 48, 16) PV(256, 17, 48, 16)
   }
   return 0;
 }
