@@ -278,3 +278,61 @@ def test_hybrid_auto_pairs_large(dev, oracle_mod, bits8):
     np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), rk)
     np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint32), rv)
 
+
+
+def test_hybrid_forced_second_block(dev, oracle_mod, bits, force):
+    """One bucket of 3000 keys (above the first block's slots, within the
+    second's): sorted by the second bucket-sort launch, no LSD fallback."""
+    n = 1 << 22
+    rng = np.random.default_rng(5)
+    x = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    x[:3000] = np.uint32(0x12340000) | rng.integers(0, 1 << 16, 3000, dtype=np.uint64).astype(np.uint32)
+    out, nbs, npass = _sort_counting(dev, _tensor(x))
+    assert nbs == 1
+    assert npass == 16 // bits, "a bucket within the second block must not need the LSD fallback"
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+
+
+def test_hybrid_forced_second_block_pairs(dev, oracle_mod, bits8, force):
+    """The same for stable (u64, u32) pairs (512-thread blocks)."""
+    n = 1 << 22
+    rng = np.random.default_rng(6)
+    k = rng.integers(0, 1 << 63, n, dtype=np.uint64) * np.uint64(2)
+    k[:3000] = np.uint64(0x1234 << 48) | (k[:3000] & np.uint64((1 << 48) - 1))
+    k[3000:3100] = k[:100]  # equal keys: the payload order must hold
+    kt = torch.from_numpy(k.view(np.int64)).cuda()
+    vt = torch.arange(n, dtype=torch.int32, device="cuda")
+    ok_, ov, nbs, npass = _pairs_counting(dev, kt, vt)
+    assert nbs == 1 and npass == 2, "a bucket within the second block must not need the LSD fallback"
+    rk, rv = oracle_mod.stable_sort_kv64(k, np.arange(n, dtype=np.uint32))
+    np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), rk)
+    np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint32), rv)
+
+
+@pytest.mark.parametrize("n", [1 << 28])
+def test_hybrid_auto_bench_size(dev, bits, n):
+    """The bench's size (2^28 keys, where ~2 buckets outgrow the first block):
+    no LSD fallback, output sorted (checked on the device)."""
+    x = dev.populate_u32(n)
+    out, nbs, npass = _sort_counting(dev, x)
+    assert nbs == 1
+    assert npass == 16 // bits, "uniform keys must not need the LSD fallback"
+    o = out.view(torch.int32) ^ torch.iinfo(torch.int32).min  # unsigned order as signed
+    assert bool((o[1:] >= o[:-1]).all())
+
+
+def test_hybrid_auto_pairs_bench_size(dev, bits8):
+    """configs[4]'s per-GPU share (2^28 pairs, random 64-bit keys, payload =
+    index): no LSD fallback; keys sorted and the payloads a permutation that
+    follows them (checked on the device)."""
+    n = 1 << 28
+    d = dev.populate_u32(2 * n, first=3).to(torch.int64) & 0xFFFFFFFF
+    kt = (d[0::2] << 32) | d[1::2]
+    del d
+    vt = torch.arange(n, dtype=torch.int32, device="cuda")
+    ok_, ov, nbs, npass = _pairs_counting(dev, kt, vt)
+    assert nbs == 1 and npass == 2, "uniform keys must not need the LSD fallback"
+    o = ok_ ^ torch.iinfo(torch.int64).min
+    assert bool((o[1:] >= o[:-1]).all())
+    assert bool((kt[ov.to(torch.int64)] == ok_).all())
+    assert bool((torch.sort(ov)[0] == vt).all())
