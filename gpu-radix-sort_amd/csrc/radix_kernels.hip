@@ -1330,13 +1330,15 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
   constexpr int CAP = BLOCK * ITEMS;
   constexpr int WSPAN = ITEMS * kWave;
   constexpr uint32_t kMaxRun = 64;
+  constexpr uint32_t kRunList = FIX > 0 ? 2 * kWave : 1;  // run starts listed per wave (FIX)
   static_assert(RADIX <= BLOCK && CAP < 65536, "one digit per thread; 16-bit wave counters");
-  static_assert(FIX == 0 || (sizeof(K) == 8 && FIX % BITS == 0), "tie fix-up: 64-bit keys");
+  static_assert(FIX == 0 || (sizeof(K) == 8 && FIX % BITS == 0 && FIX <= 32), "tie fix-up: 64-bit keys");
   __shared__ K s_keys[CAP];
   __shared__ VS s_vals[HAS_V ? CAP : 1];
   __shared__ WaveCount s_whist[WAVES][RADIX];
   __shared__ WaveCount s_off[RADIX <= kWave ? WAVES : 1][RADIX];
   __shared__ uint32_t s_wsum[WAVES];
+  __shared__ uint16_t s_runs[FIX > 0 ? WAVES : 1][kRunList];
   if (blockIdx.x >= min(*nb, nb_cap)) return;
   const uint32_t b = ilist ? ilist[blockIdx.x] : blockIdx.x;
   const uint32_t start = bstart[b], len = blen[b];
@@ -1438,54 +1440,73 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
     const uint32_t fs = lbits > (uint32_t)FIX ? lbits - FIX : 0u;  // keys equal above fs form the runs
     steps(fs, lbits);
     if (fs > 0) {
-      // ties from registers: position p = wbase + j*64 + lane holds k[j]; its
-      // neighbours are the adjacent lanes (the adjacent items across lanes 63
-      // and 0, LDS across waves)
-      auto hi = [&](K x) -> K { return (K)(x - bias) >> fs; };
-      auto shfl64 = [](K x, int src) -> K {
-        const uint32_t lo = __shfl((uint32_t)x, src), up = __shfl((uint32_t)(x >> 32), src);
-        return ((K)up << 32) | lo;
+      // run starts (a key whose bits above fs equal the next position's but
+      // not the previous one's) from registers: position p = wbase + j*64 +
+      // lane holds k[j]; its neighbours are the adjacent lanes (DPP wave
+      // shifts), the adjacent items across lanes 63 / 0 (readlane) and LDS
+      // across waves.  The starts are listed per wave, then one lane per run
+      // sorts it (the divergent work once per wave, not once per item).
+      // (the bits above lbits are the bucket's, so 32 bits from fs decide a
+      // tie: FIX <= 32)
+      auto hi = [&](K x) -> uint32_t { return (uint32_t)((K)(x - bias) >> fs); };
+      auto dpp = [](uint32_t x, uint32_t old, auto ctrl) -> uint32_t {
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, decltype(ctrl)::value, 0xf, 0xf, false);
       };
-      uint32_t long_run = 0;
+      auto readlane = [](uint32_t x, int l) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)x, l); };
+      using WaveShr1 = std::integral_constant<int, 0x138>;  // lane i <- lane i - 1
+      using WaveShl1 = std::integral_constant<int, 0x130>;  // lane i <- lane i + 1
+      uint32_t h[ITEMS];
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) h[j] = hi(k[j]);
+      uint32_t nruns = 0;
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
         const uint32_t p = wbase + j * kWave + lane;
-        K prev = shfl64(k[j], (lane + kWave - 1) & (kWave - 1));
-        K next = shfl64(k[j], (lane + 1) & (kWave - 1));
-        if (j > 0) {
-          const K last_prev = shfl64(k[j - 1], kWave - 1);
-          if (lane == 0) prev = last_prev;
-        } else if (lane == 0 && wbase > 0) {
-          prev = s_keys[wbase - 1];
+        const uint32_t before = j > 0 ? readlane(h[j - 1], kWave - 1) : (wbase > 0 ? hi(s_keys[wbase - 1]) : 0u);
+        const uint32_t after = j + 1 < ITEMS ? readlane(h[j + 1], 0)
+                                             : (wbase + WSPAN < len ? hi(s_keys[wbase + WSPAN]) : 0u);
+        // (the shifts run with every lane active: a DPP source lane that is
+        // off in EXEC reads as invalid)
+        const uint32_t hp = dpp(h[j], before, WaveShr1{});
+        const uint32_t hn = dpp(h[j], after, WaveShl1{});
+        const bool tie_prev = (p > 0) & (p < len) & (hp == h[j]);
+        const bool tie_next = (p + 1 < len) & (hn == h[j]);
+        const bool st = tie_next && !tie_prev;
+        const uint64_t m = __ballot(st);
+        if (st) {
+          const uint32_t idx = nruns + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          if (idx < kRunList) s_runs[w][idx] = (uint16_t)p;
         }
-        if (j + 1 < ITEMS) {
-          const K first_next = shfl64(k[j + 1], 0);
-          if (lane == kWave - 1) next = first_next;
-        } else if (lane == kWave - 1 && p + 1 < len) {
-          next = s_keys[p + 1];
-        }
-        const bool tie_prev = p > 0 && p < len && hi(prev) == hi(k[j]);
-        const bool tie_next = p + 1 < len && hi(next) == hi(k[j]);
-        if (tie_next && !tie_prev) {
-          // a run starts here: its length from LDS, then a stable insertion
-          // sort of s_keys[p, p + L) on key - bias
-          uint32_t L = 2;
-          while (L <= kMaxRun && p + L < len && hi(s_keys[p + L]) == hi(k[j])) ++L;
-          if (L > kMaxRun) {
-            long_run = 1;
-          } else {
-            for (uint32_t a = 1; a < L; ++a) {
-              const K x = s_keys[p + a];
-              VS xv;
-              if constexpr (HAS_V) xv = s_vals[p + a];
-              uint32_t c = a;
-              while (c > 0 && (K)(s_keys[p + c - 1] - bias) > (K)(x - bias)) {
-                s_keys[p + c] = s_keys[p + c - 1];
-                if constexpr (HAS_V) s_vals[p + c] = s_vals[p + c - 1];
-                --c;
+        nruns += (uint32_t)__popcll(m);
+      }
+      uint32_t long_run = nruns > kRunList ? 1u : 0u;
+      if (!long_run) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t r0 = 0; r0 < nruns; r0 += kWave) {
+          if (r0 + lane < nruns) {
+            // a stable insertion sort of s_keys[p, p + L) on key - bias
+            const uint32_t p = s_runs[w][r0 + lane];
+            const uint32_t h0 = hi(s_keys[p]);
+            uint32_t L = 2;
+            while (L <= kMaxRun && p + L < len && hi(s_keys[p + L]) == h0) ++L;
+            if (L > kMaxRun) {
+              long_run = 1;
+            } else {
+              for (uint32_t a = 1; a < L; ++a) {
+                const K x = s_keys[p + a];
+                VS xv;
+                if constexpr (HAS_V) xv = s_vals[p + a];
+                uint32_t c = a;
+                while (c > 0 && (K)(s_keys[p + c - 1] - bias) > (K)(x - bias)) {
+                  s_keys[p + c] = s_keys[p + c - 1];
+                  if constexpr (HAS_V) s_vals[p + c] = s_vals[p + c - 1];
+                  --c;
+                }
+                s_keys[p + c] = x;
+                if constexpr (HAS_V) s_vals[p + c] = xv;
               }
-              s_keys[p + c] = x;
-              if constexpr (HAS_V) s_vals[p + c] = xv;
             }
           }
         }

@@ -50,7 +50,7 @@ int main(int argc, char** argv) {
                 }});
 #define BVL(BITS, B, I, S_, LB) BVG(BITS, B, I, S_, LB, 0)
 #define BV(BITS, B, I, S_) BVL(BITS, B, I, S_, 16)
-  BV(4, 256, 16, 4096)
+  BV(4, 256, 17, 4096)
   for (auto& v : vs) {
     const uint32_t m = (uint32_t)(n / v.S);
     hipLaunchKernelGGL(fill, dim3((n + 255) / 256), dim3(256), 0, st, in, n, v.S, 0u);
