@@ -3057,7 +3057,7 @@ hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t
   return sort_impl<uint32_t, uint32_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, lo, hi, digit_bits, st);
 }
 
-// 64-bit keys (alone or with u32 payloads), full-width sorts with 8-bit
+// 64-bit keys (alone or with u32 / u64 payloads), full-width sorts with 8-bit
 // digits: the MSD hybrid (two digit passes over the top 16 bits, buckets
 // sorted on chip on the low 48 bits, stable: the passes and the on-chip steps
 // keep the order of equal keys, so a payload keeps its input order).
@@ -3065,11 +3065,14 @@ template <typename V>
 hipError_t sort_64_hybrid_or_lsd(Workspace& ws, const uint64_t* kin, uint64_t* kout, uint64_t* ktmp, const V* vin,
                                  V* vout, V* vtmp, size_t n, int lo, int hi, int digit_bits, hipStream_t st) {
   const int hyb = get_hybrid_mode();
-  if (lo == 0 && hi == 64 && digit_bits == 8 &&
+  if (lo == 0 && hi == 64 && (digit_bits == 8 || digit_bits == 4) &&
       ((hyb == 1 && n >= kHybMinKeys && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
       (get_algorithm() == 0 || get_algorithm() == 3) && (const void*)kin != (const void*)ktmp) {
     bool handled = false;
-    LS_TRY((sort_hybrid<8, RadixDigit, uint64_t, V>(ws, kin, kout, ktmp, vin, vout, vtmp, n, 64, 0u, st, &handled)));
+    if (digit_bits == 8)
+      LS_TRY((sort_hybrid<8, RadixDigit, uint64_t, V>(ws, kin, kout, ktmp, vin, vout, vtmp, n, 64, 0u, st, &handled)));
+    else
+      LS_TRY((sort_hybrid<4, RadixDigit, uint64_t, V>(ws, kin, kout, ktmp, vin, vout, vtmp, n, 64, 0u, st, &handled)));
     if (handled) {
       ws.last_algo = 4;
       return hipSuccess;
@@ -3093,10 +3096,7 @@ hipError_t sort_u64(Workspace& ws, const uint64_t* in, uint64_t* out, uint64_t* 
 hipError_t sort_pairs_u64_u64(Workspace& ws, const uint64_t* kin, const uint64_t* vin, uint64_t* kout,
                               uint64_t* vout, uint64_t* ktmp, uint64_t* vtmp, size_t n, int lo, int hi,
                               int digit_bits, hipStream_t st) {
-  // (u64, u64) pairs stay LSD: through the hybrid (with the top-16-bit steps
-  // and the run fix-up), 2^27 pairs took 10.47 ms against 9.33 (16 bytes per
-  // pair through LDS in every on-chip step, half the blocks per CU)
-  return sort_impl<uint64_t, uint64_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, lo, hi, digit_bits, st);
+  return sort_64_hybrid_or_lsd<uint64_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, lo, hi, digit_bits, st);
 }
 
 hipError_t histogram_u32(Workspace& ws, const uint32_t* keys, size_t n, int shift, int bits,

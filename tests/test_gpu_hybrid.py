@@ -226,12 +226,14 @@ def bits8(dev):
     pylibsort.setDigitBits(prev)
 
 
-@pytest.mark.parametrize("kind", ["uniform", "dups", "top_skew", "deep_skew", "equal"])
-@pytest.mark.parametrize("n", [1024, 65539, (1 << 21) + 7])
-def test_hybrid_forced_pairs_u64_u32(dev, oracle_mod, bits8, force, kind, n):
-    """(u64 key, u32 payload) pairs (configs[4]'s record) through the hybrid:
-    two digit passes over the top 16 key bits, buckets sorted on chip on the
-    low 48 bits; stable (payload = input index, ties keep it increasing)."""
+KINDS64 = ["uniform", "dups", "top_skew", "deep_skew", "equal", "runs", "long_runs"]
+
+
+def _keys64(kind, n):
+    """64-bit key sets for the hybrid: uniform; few distinct values; skewed
+    top digit (abandons); skewed second byte (oversized buckets); all equal;
+    runs of keys sharing their top 32 bits (the bucket sort's tie fix-up:
+    insertion-sorted runs, and past 64 keys the reload with every step)."""
     rng = np.random.default_rng(n + len(kind))
     k = rng.integers(0, 1 << 63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
     if kind == "dups":
@@ -242,6 +244,21 @@ def test_hybrid_forced_pairs_u64_u32(dev, oracle_mod, bits8, force, kind, n):
         k &= np.uint64(0xFF00FFFFFFFFFFFF)
     elif kind == "equal":
         k[:] = np.uint64(0x123456789ABCDEF0)
+    elif kind == "runs":          # bits 32-47 from 4 values: runs of a quarter bucket
+        k = (k & np.uint64(0xFFFF0000FFFFFFFF)) | (rng.integers(0, 4, n, dtype=np.uint64) << np.uint64(32))
+    elif kind == "long_runs":     # 4096 buckets, bits 32-47 zero: a run is the whole bucket
+        top = rng.integers(0, 4096, n, dtype=np.uint64) * np.uint64(16)
+        k = (top << np.uint64(48)) | (k & np.uint64(0xFFFFFFFF))
+    return k
+
+
+@pytest.mark.parametrize("kind", KINDS64)
+@pytest.mark.parametrize("n", [1024, 65539, (1 << 21) + 7])
+def test_hybrid_forced_pairs_u64_u32(dev, oracle_mod, bits, force, kind, n):
+    """(u64 key, u32 payload) pairs (configs[4]'s record) through the hybrid:
+    two digit passes over the top 16 key bits, buckets sorted on chip on the
+    low 48 bits; stable (payload = input index, ties keep it increasing)."""
+    k = _keys64(kind, n)
     v = np.arange(n, dtype=np.uint32)
     kt = torch.from_numpy(k.view(np.int64)).cuda()
     vt = torch.from_numpy(v.view(np.int32)).cuda()
@@ -249,12 +266,59 @@ def test_hybrid_forced_pairs_u64_u32(dev, oracle_mod, bits8, force, kind, n):
     rk, rv = oracle_mod.stable_sort_kv64(k, v)
     np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), rk)
     np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint32), rv)
-    if kind in ("uniform", "dups", "deep_skew"):
+    if kind in ("uniform", "dups", "deep_skew", "runs", "long_runs"):
         assert nbs == 1
 
 
+@pytest.mark.parametrize("kind", KINDS64)
 @pytest.mark.parametrize("n", [4097, (1 << 21) + 7])
-def test_hybrid_forced_keys_u64(dev, oracle_mod, bits8, force, n):
+def test_hybrid_forced_pairs_u64_u64(dev, oracle_mod, bits, force, kind, n):
+    """(u64 key, u64 payload) pairs through the hybrid, stable."""
+    k = _keys64(kind, n)
+    v = np.arange(n, dtype=np.uint64) * np.uint64(0x100000001)
+    kt = torch.from_numpy(k.view(np.int64)).cuda()
+    vt = torch.from_numpy(v.view(np.int64)).cuda()
+    dev.timing_enable(True)
+    dev.timing_reset()
+    try:
+        ok_, ov = dev.sort_pairs_u64_u64(kt, vt)
+        torch.cuda.synchronize()
+        nbs = dev.timing_query("bucketsort")[0]
+    finally:
+        dev.timing_enable(False)
+    rk, rv = oracle_mod.stable_sort_kv64v64(k, v)
+    np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), rk)
+    np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint64), rv)
+    if kind in ("uniform", "dups", "deep_skew", "runs", "long_runs"):
+        assert nbs == 1
+
+
+def test_hybrid_auto_pairs_u64_u64_large(dev, oracle_mod, bits8):
+    """2^27 (u64, u64) pairs (uniform keys, 1/64 of them repeated) through
+    the auto mode: no fallback, equal to the oracle's stable sort."""
+    n = 1 << 27
+    d = dev.populate_u32(2 * n, first=17).to(torch.int64) & 0xFFFFFFFF
+    kt = (d[0::2] << 32) | d[1::2]
+    del d
+    kt[n // 64: n // 32] = kt[: n // 64]
+    vt = torch.arange(n, dtype=torch.int64, device="cuda")
+    dev.timing_enable(True)
+    dev.timing_reset()
+    try:
+        ok_, ov = dev.sort_pairs_u64_u64(kt, vt)
+        torch.cuda.synchronize()
+        nbs, npass = dev.timing_query("bucketsort")[0], dev.timing_query("tilepass")[0]
+    finally:
+        dev.timing_enable(False)
+    assert nbs == 1 and npass == 2, "uniform keys must not need the LSD fallback"
+    k = kt.cpu().numpy().view(np.uint64)
+    rk, rv = oracle_mod.stable_sort_kv64v64(k, np.arange(n, dtype=np.uint64))
+    np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), rk)
+    np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint64), rv)
+
+
+@pytest.mark.parametrize("n", [4097, (1 << 21) + 7])
+def test_hybrid_forced_keys_u64(dev, oracle_mod, bits, force, n):
     rng = np.random.default_rng(n)
     k = rng.integers(0, 1 << 63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
     k[: n // 5] &= np.uint64(0xFFFF0000FFFF)
@@ -263,7 +327,7 @@ def test_hybrid_forced_keys_u64(dev, oracle_mod, bits8, force, n):
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint64), oracle_mod.sort_u64(k))
 
 
-def test_hybrid_auto_pairs_large(dev, oracle_mod, bits8):
+def test_hybrid_auto_pairs_large(dev, oracle_mod, bits):
     """configs[4]'s per-GPU record at 2^27 pairs (key = two consecutive PCG
     draws, payload = index) through the auto mode: no fallback, and equal to
     the oracle's stable sort."""
@@ -272,7 +336,7 @@ def test_hybrid_auto_pairs_large(dev, oracle_mod, bits8):
     kt = (d[0::2] << 32) | d[1::2]
     vt = torch.arange(n, dtype=torch.int32, device="cuda")
     ok_, ov, nbs, npass = _pairs_counting(dev, kt, vt)
-    assert nbs == 1 and npass == 2
+    assert nbs == 1 and npass == 16 // bits
     k = kt.cpu().numpy().view(np.uint64)
     rk, rv = oracle_mod.stable_sort_kv64(k, np.arange(n, dtype=np.uint32))
     np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), rk)
