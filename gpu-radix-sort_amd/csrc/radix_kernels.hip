@@ -3054,6 +3054,23 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
 hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
                               uint32_t* vout, uint32_t* ktmp, uint32_t* vtmp, size_t n, int lo, int hi,
                               int digit_bits, hipStream_t st) {
+  // full-width sorts: the MSD hybrid (stable; the payloads travel with the keys)
+  const int hyb = get_hybrid_mode();
+  if (lo == 0 && hi == 32 && (digit_bits == 8 || digit_bits == 4) &&
+      ((hyb == 1 && n >= kHybMinKeys && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
+      (get_algorithm() == 0 || get_algorithm() == 3) && kin != ktmp) {
+    bool handled = false;
+    if (digit_bits == 8)
+      LS_TRY((sort_hybrid<8, RadixDigit, uint32_t, uint32_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, 32, 0u, st,
+                                                              &handled)));
+    else
+      LS_TRY((sort_hybrid<4, RadixDigit, uint32_t, uint32_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, 32, 0u, st,
+                                                              &handled)));
+    if (handled) {
+      ws.last_algo = 4;
+      return hipSuccess;
+    }
+  }
   return sort_impl<uint32_t, uint32_t>(ws, kin, kout, ktmp, vin, vout, vtmp, n, lo, hi, digit_bits, st);
 }
 

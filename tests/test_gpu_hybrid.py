@@ -400,3 +400,44 @@ def test_hybrid_auto_pairs_bench_size(dev, bits8):
     assert bool((o[1:] >= o[:-1]).all())
     assert bool((kt[ov.to(torch.int64)] == ok_).all())
     assert bool((torch.sort(ov)[0] == vt).all())
+
+
+@pytest.mark.parametrize("kind", ["pcg", "low16_const", "four", "top_skew", "deep_skew", "equal"])
+@pytest.mark.parametrize("n", [1024, 65539, (1 << 21) + 7])
+def test_hybrid_forced_pairs_u32_u32(dev, oracle_mod, bits, force, kind, n):
+    """(u32 key, u32 payload) pairs through the hybrid, stable."""
+    k = _inputs(kind, n, n + len(kind))
+    v = np.arange(n, dtype=np.uint32)
+    dev.timing_enable(True)
+    dev.timing_reset()
+    try:
+        ok_, ov = dev.sort_pairs_u32_u32(_tensor(k), _tensor(v))
+        torch.cuda.synchronize()
+        nbs = dev.timing_query("bucketsort")[0]
+    finally:
+        dev.timing_enable(False)
+    rk, rv = oracle_mod.stable_sort_kv32(k, v)
+    np.testing.assert_array_equal(_u32(ok_), rk)
+    np.testing.assert_array_equal(_u32(ov), rv)
+    if kind in ("pcg", "low16_const"):
+        assert nbs == 1
+
+
+def test_hybrid_auto_pairs_u32_u32_large(dev, oracle_mod, bits):
+    """2^27 PCG keys with index payloads through the auto mode: no fallback,
+    equal to the oracle's stable sort."""
+    n = 1 << 27
+    kt = dev.populate_u32(n, first=29)
+    vt = torch.arange(n, dtype=torch.int32, device="cuda")
+    dev.timing_enable(True)
+    dev.timing_reset()
+    try:
+        ok_, ov = dev.sort_pairs_u32_u32(kt, vt)
+        torch.cuda.synchronize()
+        nbs, npass = dev.timing_query("bucketsort")[0], dev.timing_query("tilepass")[0]
+    finally:
+        dev.timing_enable(False)
+    assert nbs == 1 and npass == 16 // bits, "uniform keys must not need the LSD fallback"
+    rk, rv = oracle_mod.stable_sort_kv32(_u32(kt), np.arange(n, dtype=np.uint32))
+    np.testing.assert_array_equal(_u32(ok_), rk)
+    np.testing.assert_array_equal(_u32(ov), rv)

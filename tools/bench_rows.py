@@ -64,6 +64,28 @@ def row4():
               "sorted+stable=%s" % (bits, t * 1e3, m / t / 1e9, 32.0 * m * passes / t / 1e9, ok))
 
 
+def rowp():
+    """(u32 key, u32 payload) stable pairs, 2^28, PCG keys, LSD vs the MSD hybrid."""
+    import torch
+    import pylibsort
+    import pylibsort.device as D
+    n = 1 << 28
+    k = D.populate_u32(n)
+    v = torch.arange(n, dtype=torch.int32, device="cuda")
+    ok_, ov, tk, tv = (torch.empty_like(k), torch.empty_like(v), torch.empty_like(k), torch.empty_like(v))
+    flip = torch.tensor(-(1 << 31), dtype=torch.int32, device="cuda")
+    for bits in (4, 8):
+        pylibsort.setDigitBits(bits)
+        for mode in ("off", "auto"):
+            prev = pylibsort.setHybrid(mode)
+            t = timed(lambda: D.sort_pairs_u32_u32(k, v, out_keys=ok_, out_vals=ov, tmp_keys=tk, tmp_vals=tv))
+            pylibsort.setHybrid(prev)
+            s = torch.bitwise_xor(ok_, flip)
+            ok = bool((s[1:] >= s[:-1]).all()) and bool((k[ov.to(torch.int64)] == ok_).all())
+            print("u32+u32 pairs 2^28, %d-bit digits, hybrid %s: %.3f ms = %.2f Gpairs/s sorted+paired=%s"
+                  % (bits, mode, t * 1e3, n / t / 1e9, ok))
+
+
 def row3():
     import numpy as np
     from pylibsort import data, faas
@@ -106,3 +128,5 @@ if __name__ == "__main__":
         row4()
     if "3" in rows:
         row3()
+    if "p" in rows:
+        rowp()
