@@ -123,54 +123,60 @@ struct TimingRec {
 };
 static std::atomic<bool> g_timing_on{false};
 static std::mutex g_tmu;
-static std::vector<TimingRec> g_recs;
+static std::vector<TimingRec> g_recs;  // [0, g_nrec) recorded since the last reset; the rest keep their events
+static size_t g_nrec = 0;
+static std::string g_filter;  // ",name,name," (empty: every kernel)
 
 bool timing_enabled() { return g_timing_on.load(std::memory_order_relaxed); }
 void timing_enable(bool on) { g_timing_on.store(on); }
 
 void timing_reset() {
   std::lock_guard<std::mutex> lk(g_tmu);
-  for (auto& r : g_recs) {
-    if (r.a) (void)hipEventDestroy(r.a);
-    if (r.b) (void)hipEventDestroy(r.b);
-  }
-  g_recs.clear();
+  g_nrec = 0;
+}
+
+void timing_filter(const char* csv) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_filter = (csv && *csv) ? "," + std::string(csv) + "," : std::string();
 }
 
 int timing_start(const char* name, hipStream_t st, uint64_t keys) {
   if (!timing_enabled()) return -1;
-  TimingRec r;
+  std::lock_guard<std::mutex> lk(g_tmu);
+  if (!g_filter.empty() && g_filter.find("," + std::string(name) + ",") == std::string::npos) return -1;
+  if (g_nrec == g_recs.size()) {
+    // Timestamps only: no system-scope fence at record time.  A default
+    // event writes back and invalidates L2 when it is recorded (~3 us each
+    // between the kernels of a sort, and the pass kernel's L2-merged output
+    // lines flushed early); these events are never used to order memory.
+    TimingRec r;
+    if (hipEventCreateWithFlags(&r.a, hipEventDisableSystemFence) != hipSuccess) return -1;
+    if (hipEventCreateWithFlags(&r.b, hipEventDisableSystemFence) != hipSuccess) {
+      (void)hipEventDestroy(r.a);
+      return -1;
+    }
+    g_recs.push_back(r);
+  }
+  TimingRec& r = g_recs[g_nrec];
   r.name = name;
   r.keys = keys;
-  // Timestamps only: no system-scope fence at record time.  A default event
-  // writes back and invalidates L2 when it is recorded (~3 us each between the
-  // kernels of a sort, and the pass kernel's L2-merged output lines flushed
-  // early); these events are never used to order memory.
-  if (hipEventCreateWithFlags(&r.a, hipEventDisableSystemFence) != hipSuccess ||
-      hipEventCreateWithFlags(&r.b, hipEventDisableSystemFence) != hipSuccess)
-    return -1;
   if (hipEventRecord(r.a, st) != hipSuccess) return -1;
-  std::lock_guard<std::mutex> lk(g_tmu);
-  g_recs.push_back(r);
-  return (int)g_recs.size() - 1;
+  return (int)g_nrec++;
 }
 
 void timing_stop(int tok, hipStream_t st) {
   if (tok < 0) return;
-  hipEvent_t b;
-  {
-    std::lock_guard<std::mutex> lk(g_tmu);
-    if ((size_t)tok >= g_recs.size()) return;
-    b = g_recs[tok].b;
-  }
-  (void)hipEventRecord(b, st);
+  std::lock_guard<std::mutex> lk(g_tmu);
+  if ((size_t)tok >= g_nrec) return;
+  (void)hipEventRecord(g_recs[tok].b, st);
 }
 
 bool timing_query(const char* name, uint64_t* launches, double* total_ms, uint64_t* total_keys) {
   std::lock_guard<std::mutex> lk(g_tmu);
   uint64_t cnt = 0, keys = 0;
   double ms = 0.0;
-  for (auto& r : g_recs) {
+  for (size_t i = 0; i < g_nrec; ++i) {
+    const TimingRec& r = g_recs[i];
     if (r.name != name) continue;
     if (hipEventSynchronize(r.b) != hipSuccess) return false;
     float t = 0.f;
@@ -1048,6 +1054,7 @@ LIBSORT_EXPORT int libsortSetBoundaryMode(int mode) {
 
 LIBSORT_EXPORT void libsortTimingEnable(bool on) { timing_enable(on); }
 LIBSORT_EXPORT void libsortTimingReset(void) { timing_reset(); }
+LIBSORT_EXPORT void libsortTimingFilter(const char* kernels) { timing_filter(kernels); }
 LIBSORT_EXPORT int libsortTimingQuery(const char* kernel, uint64_t* launches, double* total_ms,
                                       uint64_t* total_keys) {
   return timing_query(kernel, launches, total_ms, total_keys) ? 1 : 0;

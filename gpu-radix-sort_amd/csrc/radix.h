@@ -163,8 +163,9 @@ hipError_t sort_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t
 // "rts" / "tiles").
 int get_algorithm();
 int set_algorithm(int algo);  // returns the previous value, -1 if invalid
-// MSD hybrid for full 32-bit key sorts: 0 = off, 1 = auto (2^27 <= n <=
-// 2^28 + 2^24), 2 = every full sort of n >= 1024 keys.  LIBSORT_HYBRID.
+// MSD hybrid for full-width sorts: 0 = off, 1 = auto (2^27 <= n <= 2^28 +
+// 2^24; 2^25 <= n for 64-bit keys), 2 = every full sort of n >= 1024 keys.
+// LIBSORT_HYBRID.
 int get_hybrid_mode();
 int set_hybrid_mode(int mode);
 
@@ -239,6 +240,8 @@ void distrib_release();
 bool timing_enabled();
 void timing_enable(bool on);
 void timing_reset();
+// Records only the kernels named in `csv` ("tilepass,bucketsort"); null or "" = all.
+void timing_filter(const char* csv);
 bool timing_query(const char* name, uint64_t* launches, double* total_ms, uint64_t* total_keys);
 // Records a start event; returns a token (or -1 when timing is off).
 int timing_start(const char* name, hipStream_t stream, uint64_t keys);

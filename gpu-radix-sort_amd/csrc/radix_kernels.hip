@@ -2815,6 +2815,9 @@ hipError_t group_bounds(Workspace& ws, const uint32_t* sorted, size_t n, int lo,
 #define LIBSORT_BUCKET64_BLOCK 512
 #endif
 constexpr size_t kHybMinKeys = 1ull << 27;
+// 64-bit keys: the LSD sort needs 8 (16) passes, so the hybrid pays from 2^25
+// keys (tools/hyb_sizes.py: (u64, u32) pairs 2^24 0.91x, 2^25 1.41x, 2^26 2.14x)
+constexpr size_t kHybMinKeys64 = 1ull << 25;
 constexpr size_t kHybMaxKeys = (1ull << 28) + (1ull << 24);
 
 
@@ -3083,7 +3086,7 @@ hipError_t sort_64_hybrid_or_lsd(Workspace& ws, const uint64_t* kin, uint64_t* k
                                  V* vout, V* vtmp, size_t n, int lo, int hi, int digit_bits, hipStream_t st) {
   const int hyb = get_hybrid_mode();
   if (lo == 0 && hi == 64 && (digit_bits == 8 || digit_bits == 4) &&
-      ((hyb == 1 && n >= kHybMinKeys && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
+      ((hyb == 1 && n >= kHybMinKeys64 && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
       (get_algorithm() == 0 || get_algorithm() == 3) && (const void*)kin != (const void*)ktmp) {
     bool handled = false;
     if (digit_bits == 8)

@@ -89,6 +89,7 @@ _SIGS = [
     ("libsortSetBoundaryMode", ctypes.c_int, [ctypes.c_int]),
     ("libsortTimingEnable", None, [ctypes.c_bool]),
     ("libsortTimingReset", None, []),
+    ("libsortTimingFilter", None, [ctypes.c_char_p]),
     ("libsortTimingQuery", ctypes.c_int,
      [ctypes.c_char_p, _u64p, ctypes.POINTER(ctypes.c_double), _u64p]),
     ("libsortReleaseWorkspace", ctypes.c_int, []),

@@ -407,6 +407,13 @@ def timing_reset():
     _lib().libsortTimingReset()
 
 
+def timing_filter(kernels=None):
+    """Record only the named kernels (a list or comma-separated string); None = all."""
+    if kernels is not None and not isinstance(kernels, str):
+        kernels = ",".join(kernels)
+    _lib().libsortTimingFilter(kernels.encode() if kernels else None)
+
+
 def timing_query(kernel):
     """(launches, total_ms, total_keys) of the recorded launches of `kernel`."""
     n = ctypes.c_uint64()

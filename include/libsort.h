@@ -263,13 +263,15 @@ LIBSORT_API int libsortGetDigitBits(void);
  * if `algo` is invalid. */
 LIBSORT_API int libsortSetAlgorithm(int algo);
 
-/* Full 32-bit sorts of uint32 keys (providedGpu, libsortSortKeysU32 with
- * offset 0 / width 32): 1 (default) = for 2^27 <= n <= 2^28 + 2^24 keys the
- * MSD hybrid (16 / digit-bits passes from the top digit down, then every
- * bucket of keys sharing the top 16 bits sorted on chip; the call returns with
- * the sort complete); 0 = always the LSD digit passes; 2 = the hybrid for
- * every such sort of n >= 1024 keys (tests).  Initial value from
- * LIBSORT_HYBRID.  Returns the previous value, or -1 if `mode` is invalid. */
+/* Full-width sorts (providedGpu, libsortSortKeysU32 with offset 0 / width 32,
+ * libsortSortKeysRangeU32 over >= 20 bits, libsortSortPairsU32U32 and the
+ * 64-bit key sorts at full width; 4- or 8-bit digits): 1 (default) = for
+ * 2^27 <= n <= 2^28 + 2^24 keys (2^25 <= n for 64-bit keys) the MSD hybrid
+ * (16 / digit-bits passes from the top digit down, then every bucket of keys
+ * sharing the top 16 bits sorted on chip, stable; the call returns with the
+ * sort complete); 0 = always the LSD digit passes; 2 = the hybrid for every
+ * such sort of n >= 1024 keys (tests).  Initial value from LIBSORT_HYBRID.
+ * Returns the previous value, or -1 if `mode` is invalid. */
 LIBSORT_API int libsortSetHybrid(int mode);
 
 /* Boundaries returned by gpuPartial / gpuPartialProfile / gpuPartialSort:
@@ -284,11 +286,14 @@ LIBSORT_API int libsortSetHybrid(int mode);
  * previous mode, or -1 if `mode` is invalid. */
 LIBSORT_API int libsortSetBoundaryMode(int mode);
 
-/* Per-kernel timing with hipEvents on the launch stream.  Names: "whist",
- * "onesweep", "upsweep", "scan", "downsweep", "bounds", "histogram",
- * "populate", "segcopy". */
+/* Per-kernel timing with hipEvents on the launch stream.  Names: "tilecounts",
+ * "colscan", "tilepass", "hybplan", "bucketsort", "whist", "onesweep",
+ * "upsweep", "scan", "downsweep", "bounds", "histogram", "populate",
+ * "segcopy".  libsortTimingFilter: record only the listed kernels
+ * (comma-separated, e.g. "tilepass"); NULL or "" = all. */
 LIBSORT_API void libsortTimingEnable(bool on);
 LIBSORT_API void libsortTimingReset(void);
+LIBSORT_API void libsortTimingFilter(const char* kernels);
 LIBSORT_API bool libsortTimingQuery(const char* kernel, uint64_t* launches, double* total_ms,
                                     uint64_t* total_keys);
 
