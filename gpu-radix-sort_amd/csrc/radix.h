@@ -118,6 +118,13 @@ struct Workspace {
   hipEvent_t hyb_evt = nullptr;
   hipError_t ensure_hybrid(size_t words);
 
+  // 8-bit digit passes: the next pass's digit of every key, one byte at the
+  // key's output position (written by the pass, read by the next pass's count
+  // kernel: 1 B per key instead of the key)
+  uint8_t* dstream = nullptr;
+  size_t dstream_cap = 0;  // bytes
+  hipError_t ensure_dstream(size_t bytes);
+
   hipError_t ensure_counts(size_t m);
   hipError_t ensure_hbuf(size_t bytes);
   hipError_t ensure_bounds(size_t m);

@@ -845,6 +845,63 @@ __global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ key
   }
 }
 
+// Per-tile 8-bit digit counts from the digit stream the previous pass wrote
+// (k_tile_pass geo.dout): one byte per key instead of the key (u32: 4 B, u64:
+// 8 B).  The tile's bytes are read as the 16-byte words that cover them (any
+// alignment: the hybrid's tiles start anywhere); bytes outside the tile are
+// masked.  TAB / rows past *ntiles as k_tile_counts.
+template <int BLOCK, int TILE, bool TAB = false>
+__global__ __launch_bounds__(BLOCK) void k_tile_counts_u8(const uint8_t* __restrict__ dig, uint32_t n,
+                                                          uint32_t* __restrict__ counts,
+                                                          const uint4* __restrict__ tiles,
+                                                          const uint32_t* __restrict__ ntiles) {
+  constexpr int RADIX = 256;
+  constexpr int COPIES = 2;  // halves the same-bin LDS atomics of a wave's neighbours
+  __shared__ uint32_t s_h[COPIES][RADIX];
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < COPIES * RADIX; i += BLOCK) (&s_h[0][0])[i] = 0u;
+  __syncthreads();
+  uint64_t tile_base = (uint64_t)blockIdx.x * TILE;
+  uint32_t valid;
+  if constexpr (TAB) {
+    if (blockIdx.x < *ntiles) {
+      const uint4 te = tiles[blockIdx.x];
+      tile_base = te.x;
+      valid = te.y;
+    } else {
+      valid = 0;
+    }
+  } else {
+    valid = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tile_base);
+  }
+  uint32_t* h = s_h[(tid / kWave) % COPIES];
+  const uint64_t end = tile_base + valid;
+  if (valid == TILE && (tile_base & 15u) == 0) {
+    for (uint32_t q = tid; q < TILE / 16; q += BLOCK) {
+      const uint4 x = load_count_vec(reinterpret_cast<const uint4*>(dig + tile_base) + q);
+      const uint32_t wd[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int c = 0; c < 16; ++c) atomicAdd(&h[(wd[c >> 2] >> (8 * (c & 3))) & 0xffu], 1u);
+    }
+  } else if (valid) {
+    const uint64_t a0 = tile_base & ~(uint64_t)15;
+    for (uint64_t a = a0 + 16ull * tid; a < end; a += 16ull * BLOCK) {
+      const uint4 x = load_count_vec(reinterpret_cast<const uint4*>(dig + a));
+      const uint32_t wd[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if (a + c >= tile_base && a + c < end) atomicAdd(&h[(wd[c >> 2] >> (8 * (c & 3))) & 0xffu], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t d = tid; d < RADIX; d += BLOCK) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int c = 0; c < COPIES; ++c) s += s_h[c][d];
+    counts[(size_t)blockIdx.x * RADIX + d] = s;
+  }
+}
+
 // The column scan turns the per-tile counts C[tile][RADIX] into each tile's
 // run offsets: offset(t, d) = C'[t][d] + B[t / CH][d] + D[d] with C' the
 // chunk-local exclusive scan (chunks of CH = col_chunk_rows(RADIX)
@@ -1036,6 +1093,7 @@ struct HybridGeo {
   const uint32_t* ntiles;    // GEO & 1: this depth's tile count (blocks past it exit)
   const uint32_t* ncstart;   // GEO & 2: next depth's child starts
   const uint32_t* nctile0;   // GEO & 2: next depth's first tile per child
+  uint8_t* dout;             // 8-bit passes (any GEO): op_next of every written key at its output position, or null
 };
 
 // The pass kernel of the tile-offset path: the onesweep tile body with the
@@ -1128,6 +1186,10 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   }
   const bool full = valid == TILE;
   const uint32_t wbase = w * WSPAN;
+  // the next 8-bit pass's digit stream (geo.dout)
+  constexpr bool DOUT = !FUSE && BITS == 8 &&
+                        (std::is_same<OpN, RadixDigit>::value || std::is_same<OpN, BiasedDigit>::value);
+  uint8_t* const dout = geo.dout;
 
   K k[ITEMS];
   VS v[ITEMS];
@@ -1213,6 +1275,8 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
         const K kk = s_keys[i];
         obk[j] = ob_base(s_ob[op(kk)]);
         kout[obk[j] + i] = kk;
+        if constexpr (DOUT)
+          if (dout) dout[obk[j] + i] = (uint8_t)op_next(kk);
       }
     }
     __syncthreads();
@@ -1245,6 +1309,8 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
         const uint32_t i = tid + (h * SP + j) * BLOCK;
         kout[ob_base(ob[j]) + i] = kk[j];
         if constexpr (HAS_V) vout[ob_base(ob[j]) + i] = s_vals[i];
+        if constexpr (DOUT)
+          if (dout) dout[ob_base(ob[j]) + i] = (uint8_t)op_next(kk[j]);
       }
       if constexpr (FUSE) {
 #pragma unroll
@@ -1270,6 +1336,8 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
       const OB ob = s_ob[d];
       kout[ob_base(ob) + i] = kk;
       if constexpr (HAS_V) vout[ob_base(ob) + i] = s_vals[i];
+      if constexpr (DOUT)
+        if (dout) dout[ob_base(ob) + i] = (uint8_t)op_next(kk);
       if constexpr (FUSE) {
         const uint32_t slot = i >= ob.y ? (uint32_t)(RADIX * RADIX) : 0u;
         atomicAdd(&s_next[slot + d * RADIX + op_next(kk)], 1u);
@@ -2368,6 +2436,16 @@ hipError_t Workspace::ensure_hybrid(size_t words) {
   return hipSuccess;
 }
 
+hipError_t Workspace::ensure_dstream(size_t bytes) {
+  bytes = (bytes + 64) & ~(size_t)15;  // the count kernel reads whole 16-byte words
+  if (bytes <= dstream_cap) return hipSuccess;
+  if (dstream) { (void)hipFree(dstream); dstream = nullptr; }
+  dstream_cap = 0;
+  LS_TRY(hipMalloc(&dstream, bytes));
+  dstream_cap = bytes;
+  return hipSuccess;
+}
+
 hipError_t Workspace::ensure_onesweep(size_t status_words) {
   if (!os_small) {
     LS_TRY(hipMalloc(&os_small, kOsSmallWords * sizeof(uint32_t)));
@@ -2400,6 +2478,9 @@ void Workspace::release() {
   tc[0] = tc[1] = tb = tticket = nullptr;
   tc_cap = tb_cap = 0;
   if (hyb) (void)hipFree(hyb);
+  if (dstream) (void)hipFree(dstream);
+  dstream = nullptr;
+  dstream_cap = 0;
   if (hyb_host) (void)hipHostFree(hyb_host);
   hyb = hyb_host = nullptr;
   hyb_cap = 0;
@@ -2569,6 +2650,19 @@ hipError_t tiles_colscan(Workspace& ws, uint32_t* C, uint32_t tiles, hipStream_t
   return hipGetLastError();
 }
 
+// 8-bit passes over 64-bit keys hand the next pass its digits as a byte
+// stream (k_tile_pass geo.dout -> k_tile_counts_u8): the next count reads 1 B
+// per key instead of 8 (c5: 5.21 -> 5.02 ms).  Not for 32-bit keys: the byte
+// stores beside 4-byte keys made the u32 pass 1716 -> 2557 us at 2^30 (c3
+// 10.03 -> 12.29 ms).  LIBSORT_DSTREAM=0 turns it off (A/B).
+inline bool dstream_on() {
+  static const bool on = [] {
+    const char* s = getenv("LIBSORT_DSTREAM");
+    return !(s && s[0] == '0');
+  }();
+  return on;
+}
+
 // Sort prologue of the tile path: buffers, and (4-bit) the pass-0 counts.
 template <typename K, typename V, typename Op = RadixDigit>
 hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, int bits, hipStream_t st,
@@ -2576,10 +2670,24 @@ hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, 
   const uint32_t tiles = tp_tiles<K, V>(n, bits);
   const uint32_t radix = 1u << bits;
   LS_TRY(ws.ensure_tiles((size_t)tiles * radix, ((size_t)tp_chunks(tiles, bits) + 1) * radix));
+  if (bits == 8 && sizeof(K) == 8 && dstream_on() && num_passes(hi - lo, 8) > 1) LS_TRY(ws.ensure_dstream(n));
   if (bits != 4) return hipSuccess;
   const int nb = std::min(4, hi - lo);
   return tiles_counts<4, K, Op, V>(ws, in, n, make_digit<Op>((uint32_t)lo, (1u << nb) - 1u, bias), tiles, ws.tc[0],
                                 ws.tc[1], tiles * 16u, st);
+}
+
+// Counts of an 8-bit pass from the digit stream (tiles: the pass's tiles, or
+// a hybrid depth's table when tab != null).
+template <typename K, typename V, bool TAB = false>
+hipError_t tiles_counts_u8(Workspace& ws, size_t n, uint32_t rows, uint32_t* C, const uint4* tab,
+                           const uint32_t* ntab, hipStream_t st) {
+  constexpr int B = tp_block<K>(8);
+  constexpr int TILE = B * tp_items<K, V>(8);
+  ScopedTimer tm("tilecounts", st, n);
+  hipLaunchKernelGGL((k_tile_counts_u8<B, TILE, TAB>), dim3(rows), dim3(B), 0, st, ws.dstream, (uint32_t)n, C, tab,
+                     ntab);
+  return hipGetLastError();
 }
 
 template <int BITS, typename K, typename V, typename Op = RadixDigit>
@@ -2600,12 +2708,20 @@ hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vou
   const bool fused_counts = BITS == 4 && fuse_on;
   uint32_t* cur = fused_counts ? ws.tc[p & 1] : ws.tc[0];
   uint32_t* nxt = ws.tc[(p + 1) & 1];
-  if (!fused_counts && !(BITS == 4 && p == 0))
+  // 8-bit: pass p >= 1 counts the digit stream pass p - 1 wrote; pass p
+  // writes one for pass p + 1
+  const bool dstream = BITS == 8 && sizeof(K) == 8 && dstream_on() && ws.dstream_cap >= n;
+  if (dstream && p >= 1)
+    LS_TRY((tiles_counts_u8<K, V>(ws, n, tiles, cur, nullptr, nullptr, st)));
+  else if (!fused_counts && !(BITS == 4 && p == 0))
     LS_TRY((tiles_counts<BITS, K, Op, V>(ws, kin, n, op, tiles, cur, nullptr, 0, st)));
   LS_TRY(tiles_colscan<BITS>(ws, cur, tiles, st));
   const bool fuse = fused_counts && p + 1 < P;
-  const int nb2 = fuse ? std::min(BITS, hi - shift - BITS) : 1;
-  const Op op_next = make_digit<Op>((uint32_t)(fuse ? shift + BITS : 0), (1u << nb2) - 1u, bias);
+  const bool dnext = dstream && p + 1 < P;
+  const int nb2 = (fuse || dnext) ? std::min(BITS, hi - shift - BITS) : 1;
+  const Op op_next = make_digit<Op>((uint32_t)((fuse || dnext) ? shift + BITS : 0), (1u << nb2) - 1u, bias);
+  HybridGeo geo{};
+  geo.dout = dnext ? ws.dstream : nullptr;
   ScopedTimer tm("tilepass", st, n);
   if (fuse)
     hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K, V>(BITS), K, V, BITS == 4, Op, Op>), dim3(tiles), dim3(B), 0, st,
@@ -2614,7 +2730,7 @@ hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vou
   else
     hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K, V>(BITS), K, V, false, Op, Op>), dim3(tiles), dim3(B), 0, st, kin,
                        kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, tiles_digit_starts(ws, tiles, BITS),
-                       nxt, HybridGeo{});
+                       nxt, geo);
   return hipGetLastError();
 }
 
@@ -2863,6 +2979,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   uint32_t* olist = h;  // the buckets over the first block (kListCap)
   LS_TRY(hipMemsetAsync(ctr, 0, 16 * sizeof(uint32_t), st));
   LS_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctr + 9), (int)NB, 1, st));
+  const bool dstream = BITS == 8 && sizeof(K) == 8 && dstream_on();
+  if (dstream) LS_TRY(ws.ensure_dstream(n));
   ws.part_pending.valid = false;
 
   auto buf = [&](int k) -> K* { return k == 0 ? const_cast<K*>(in) : (k & 1) ? tmp : out; };
@@ -2886,6 +3004,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     if (k == 0) {
       LS_TRY((tiles_counts<BITS, K, Op, V>(ws, src, n, op, T0, C, BITS == 4 ? Cn : nullptr,
                                            BITS == 4 ? T0 * (uint32_t)RADIX : 0u, st)));
+    } else if (BITS == 8 && dstream) {
+      // the digits depth k - 1 wrote (1 B per key)
+      LS_TRY((tiles_counts_u8<K, V, true>(ws, n, rows, C, tiles[k & 1], ctr + k, st)));
     } else if (BITS == 8) {
       ScopedTimer tm("tilecounts", st, n);
       hipLaunchKernelGGL((k_tile_counts<BITS, B, ITEMS, K, Op, true>), dim3(rows), dim3(B), 0, st, src,
@@ -2915,7 +3036,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
         LS_TRY(hipGetLastError());
       }
     }
-    const HybridGeo geo{tiles[k & 1], ctr + k, cstart[(k + 1) & 1], ctile0[(k + 1) & 1]};
+    HybridGeo geo{tiles[k & 1], ctr + k, cstart[(k + 1) & 1], ctile0[(k + 1) & 1], nullptr};
+    if (BITS == 8 && dstream && !last) geo.dout = ws.dstream;  // the next depth's digits
     {
       ScopedTimer tm("tilepass", st, n);
       if (BITS == 4 && !last) {
