@@ -1622,7 +1622,8 @@ __global__ __launch_bounds__(256) void k_hyb_children(const uint32_t* __restrict
                                                       uint32_t nseg, const uint32_t* __restrict__ ctile0,
                                                       const uint32_t* __restrict__ cstart, uint32_t fixed_tiles,
                                                       uint32_t* __restrict__ segbase, uint32_t* __restrict__ ncstart,
-                                                      uint32_t* __restrict__ nsize, uint32_t* __restrict__ ntl) {
+                                                      uint32_t* __restrict__ nsize, uint32_t* __restrict__ ntl,
+                                                      uint32_t* __restrict__ stats, uint32_t cap1) {
   static_assert(RADIX == 16 || RADIX == 256, "4- or 8-bit digits");
   constexpr int CH = col_chunk_rows(RADIX);
   __shared__ uint32_t s_wsum[4];
@@ -1655,12 +1656,26 @@ __global__ __launch_bounds__(256) void k_hyb_children(const uint32_t* __restrict
     uint32_t tot;
     excl = block_exclusive_scan<256>(size, s_wsum, tot);
   }
+  if (stats) {
+    // the last depth: the largest bucket (stats[0]) and the buckets over the
+    // first bucket-sort block (stats[1])
+    uint32_t mx = size;
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
+    if ((threadIdx.x & (kWave - 1)) == 0 && mx) atomicMax(&stats[0], mx);
+    if (size > cap1) atomicAdd(&stats[1], 1u);
+  }
   if (!live) return;
   const uint32_t start = cs + excl;
   segbase[g] = start - p0;
   ncstart[g] = start;
   nsize[g] = size;
   if (ntl) ntl[g] = (size + TILE - 1) / TILE;
+}
+
+// The hybrid's counter words: zero, and [9] = the bucket count.
+__global__ void k_hyb_init(uint32_t* __restrict__ ctr, uint32_t nb) {
+  if (threadIdx.x < 16) ctr[threadIdx.x] = threadIdx.x == 9 ? nb : 0u;
 }
 
 // Exclusive scan of the children's tile counts (one block): ctile0[0..m],
@@ -2957,7 +2972,11 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   const double need = mean + 3.5 * std::sqrt(mean);
   const int cls = need <= 256.0 * 9 ? 0 : need <= 256.0 * 13 ? 1 : need <= 256.0 * 17 ? 2 : 3;
   static constexpr int kItems1[4] = {9, 13, 17, 19};
-  const uint32_t cap = 256u * (uint32_t)(kItems1[cls] + 6);
+  // the two blocks' slots (64-bit keys: 512-thread blocks, keys per thread
+  // rounded up)
+  constexpr int BB = sizeof(K) == 8 ? LIBSORT_BUCKET64_BLOCK : 256;
+  const uint32_t cap1 = (uint32_t)BB * (((uint32_t)kItems1[cls] * 256u + BB - 1) / BB);
+  const uint32_t cap = (uint32_t)BB * (((uint32_t)(kItems1[cls] + 6) * 256u + BB - 1) / BB);
   const uint32_t T0 = (uint32_t)((n + TILE - 1) / TILE);
   auto tbound = [&](int k) { return k == 0 ? T0 : T0 + (1u << (BITS * k)); };
   const uint32_t TB = tbound(DEPTHS - 1);
@@ -2974,11 +2993,12 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   uint32_t* nsize = h; h += NB;
   uint32_t* ctile0[2] = {h, h + NB + 1}; h += 2 * ((size_t)NB + 1);
   uint32_t* ntl = h; h += NB;
-  uint32_t* ctr = h;  // [k] tiles of depth k, [8] buckets over the first block, [9] bucket count, [10] over the second
+  uint32_t* ctr = h;  // [k] tiles of depth k, [8] buckets over the first block, [9] bucket count, [10] over the
+                      // second, [11] largest bucket, [12] buckets over the first block (planning)
   h += 16;
   uint32_t* olist = h;  // the buckets over the first block (kListCap)
-  LS_TRY(hipMemsetAsync(ctr, 0, 16 * sizeof(uint32_t), st));
-  LS_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctr + 9), (int)NB, 1, st));
+  hipLaunchKernelGGL(k_hyb_init, dim3(1), dim3(64), 0, st, ctr, NB);  // one launch, not two memsets (4 fills)
+  LS_TRY(hipGetLastError());
   const bool dstream = BITS == 8 && sizeof(K) == 8 && dstream_on();
   if (dstream) LS_TRY(ws.ensure_dstream(n));
   ws.part_pending.valid = false;
@@ -3024,8 +3044,13 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       ScopedTimer tm("hybplan", st, m);
       hipLaunchKernelGGL((k_hyb_children<RADIX, TILE>), dim3((m + 255) / 256), dim3(256), 0, st, C, ws.tb, D, rows,
                          (uint32_t)n, nseg, k == 0 ? nullptr : ctile0[k & 1], cstart[k & 1], T0, segbase,
-                         cstart[(k + 1) & 1], nsize, last ? nullptr : ntl);
+                         cstart[(k + 1) & 1], nsize, last ? nullptr : ntl, last ? ctr + 11 : nullptr, cap1);
       LS_TRY(hipGetLastError());
+      if (last) {
+        // the bucket sizes, read back while the last pass runs
+        LS_TRY(hipMemcpyAsync(ws.hyb_host + 20, ctr + 11, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        LS_TRY(hipEventRecord(ws.hyb_evt, st));
+      }
       if (!last) {
         hipLaunchKernelGGL(k_hyb_tile_prefix, dim3(1), dim3(1024), 0, st, ntl, m, ctile0[(k + 1) & 1], ctr + k + 1);
         LS_TRY(hipGetLastError());
@@ -3077,15 +3102,21 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
         return hipSuccess;
     }
   }
+  // the bucket sizes (read back while the last pass runs): a bucket larger
+  // than the second block, or more buckets over the first than its list
+  // holds -> the LSD sort of out (any order sorts) instead of the bucket sort
+  LS_TRY(hipEventSynchronize(ws.hyb_evt));
+  *handled = true;
+  if (ws.hyb_host[21] > kListCap || ws.hyb_host[20] > cap)
+    return sort_impl<K, V>(ws, out, out, tmp, vout, vout, vtmp, n, 0, W, BITS, st, bias);
   // bucket sort of the 2^16 buckets in place in out (cstart/nsize of the
   // last depth's children)
   {
     ScopedTimer tm("bucketsort", st, n);
     const uint32_t* bstart = cstart[DEPTHS & 1];
     const uint32_t lbits = (uint32_t)(W - 16);
-    // 64-bit keys: 512-thread blocks (the same slots in half the keys per
+    // 64-bit keys: 512-thread blocks (BB; the same slots in half the keys per
     // thread: 152 -> ~90 VGPRs for (u64, u32) pairs at 17 slots per 256)
-    constexpr int BB = sizeof(K) == 8 ? LIBSORT_BUCKET64_BLOCK : 256;
     // 64-bit keys: on-chip steps over the top 16 of the 48 bucket bits, then
     // the tie fix-up (k_bucket_sort FIX)
     constexpr int FIXB = sizeof(K) == 8 ? LIBSORT_BUCKET64_FIX : 0;
@@ -3105,13 +3136,6 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
 #undef LS_BS2
 #undef LS_BS
     LS_TRY(hipGetLastError());
-  }
-  LS_TRY(hipMemcpyAsync(ws.hyb_host + 16, ctr + 8, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  LS_TRY(hipStreamSynchronize(st));
-  *handled = true;
-  if (ws.hyb_host[16] > kListCap || ws.hyb_host[18] != 0) {
-    // buckets too large for one block: finish with the LSD sort of out
-    LS_TRY((sort_impl<K, V>(ws, out, out, tmp, vout, vout, vtmp, n, 0, W, BITS, st, bias)));
   }
   return hipSuccess;
 }

@@ -268,8 +268,10 @@ LIBSORT_API int libsortSetAlgorithm(int algo);
  * 64-bit key sorts at full width; 4- or 8-bit digits): 1 (default) = for
  * 2^27 <= n <= 2^28 + 2^24 keys (2^25 <= n for 64-bit keys) the MSD hybrid
  * (16 / digit-bits passes from the top digit down, then every bucket of keys
- * sharing the top 16 bits sorted on chip, stable; the call returns with the
- * sort complete); 0 = always the LSD digit passes; 2 = the hybrid for every
+ * sharing the top 16 bits sorted on chip, stable; the host waits twice
+ * inside the call for small read-backs while passes run, and the call returns
+ * with the bucket sort queued like any other sort); 0 = always the LSD digit
+ * passes; 2 = the hybrid for every
  * such sort of n >= 1024 keys (tests).  Initial value from LIBSORT_HYBRID.
  * Returns the previous value, or -1 if `mode` is invalid. */
 LIBSORT_API int libsortSetHybrid(int mode);

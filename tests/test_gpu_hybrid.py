@@ -147,9 +147,10 @@ def test_hybrid_auto_large(dev, oracle_mod, bits, n):
 
 def test_hybrid_auto_skewed_large(dev, oracle_mod, bits):
     """2^27 keys that overflow the buckets (the bits below the top digit
-    down to bit 16 zero): the bucket sort
-    leaves them and the LSD sort of the output finishes; and a skewed top
-    digit (keys < 2^30) abandons the hybrid before it writes out."""
+    down to bit 16 zero): the planning of the last depth sees the bucket
+    sizes, the bucket sort is not launched and the LSD sort of the output
+    finishes; and a skewed top digit (keys < 2^30) abandons the hybrid after
+    its first pass (which wrote only tmp)."""
     n = 1 << 27
     x = dev.populate_u32(n, first=3)
     for mask_kind in ("deep", "top"):
@@ -159,8 +160,9 @@ def test_hybrid_auto_skewed_large(dev, oracle_mod, bits):
             y = torch.bitwise_and(x, torch.tensor(mask - (1 << 32), dtype=torch.int32, device=x.device))
         else:
             y = torch.bitwise_and(torch.bitwise_right_shift(x, 2), 0x3FFFFFFF)
-        out, nbs = _sort_counting_buckets(dev, y)
-        assert nbs == (1 if mask_kind == "deep" else 0)
+        out, nbs, npass = _sort_counting(dev, y)
+        assert nbs == 0
+        assert npass == (16 // bits if mask_kind == "deep" else 1) + 32 // bits
         host = y.cpu().numpy().view(np.uint32)
         np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(host))
 
@@ -266,8 +268,8 @@ def test_hybrid_forced_pairs_u64_u32(dev, oracle_mod, bits, force, kind, n):
     rk, rv = oracle_mod.stable_sort_kv64(k, v)
     np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), rk)
     np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint32), rv)
-    if kind in ("uniform", "dups", "deep_skew", "runs", "long_runs"):
-        assert nbs == 1
+    if kind in ("uniform", "dups", "runs", "long_runs") or (kind == "deep_skew" and n < 1 << 20):
+        assert nbs == 1  # (deep_skew at 2^21: buckets of 8192 -> the LSD sort, no bucket sort)
 
 
 @pytest.mark.parametrize("kind", KINDS64)
@@ -289,8 +291,8 @@ def test_hybrid_forced_pairs_u64_u64(dev, oracle_mod, bits, force, kind, n):
     rk, rv = oracle_mod.stable_sort_kv64v64(k, v)
     np.testing.assert_array_equal(ok_.cpu().numpy().view(np.uint64), rk)
     np.testing.assert_array_equal(ov.cpu().numpy().view(np.uint64), rv)
-    if kind in ("uniform", "dups", "deep_skew", "runs", "long_runs"):
-        assert nbs == 1
+    if kind in ("uniform", "dups", "runs", "long_runs") or (kind == "deep_skew" and n < 1 << 20):
+        assert nbs == 1  # (deep_skew at 2^21: buckets of 8192 -> the LSD sort, no bucket sort)
 
 
 def test_hybrid_auto_pairs_u64_u64_large(dev, oracle_mod, bits8):
