@@ -555,7 +555,7 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
         return finish(false);
       }
       if (!ok_hip(sort_u32(*s.d->ws, s.recv.u32() + a, s.outb.u32() + a, s.d->tmp.u32(), z - a, 0,
-                           span_bits(lo, hi), bits, nullptr, s.d->st, (uint32_t)lo, true),
+                           span_bits(lo, hi), bits, nullptr, s.d->st, (uint32_t)lo, true, hi - lo),
                   "round sort"))
         return finish(false);
     }

@@ -765,7 +765,8 @@ LIBSORT_EXPORT int libsortSortKeysRangeU32(const uint32_t* d_in, uint32_t* d_out
   while (width < 32 && (span >> width) != 0) ++width;
   hipStream_t st = as_stream(stream);
   return with_current_ws(st, [&](Workspace& ws) {
-           return hip_ok(sort_u32(ws, d_in, d_out, d_tmp, n, 0, width, g_digit_bits.load(), nullptr, st, lo, true),
+           return hip_ok(sort_u32(ws, d_in, d_out, d_tmp, n, 0, width, g_digit_bits.load(), nullptr, st, lo, true,
+                                  hi - lo),
                          "libsortSortKeysRangeU32");
          })
              ? 1

@@ -149,10 +149,11 @@ inline int num_passes(int width, int bits) { return width <= 0 ? 0 : (width + bi
 // keys in [bias, bias + 2^hi); no boundaries).
 // All work is enqueued on `stream`; nothing synchronises.
 // range: the keys are known to lie in [bias, bias + 2^hi) (libsortSortKeysRangeU32), so the
-// hi sorted bits determine a key and the MSD hybrid may serve the sort.
+// hi sorted bits determine a key and the MSD hybrid may serve the sort; span (when
+// nonzero): they lie in [bias, bias + span), span <= 2^hi (sizes the hybrid's buckets).
 hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n,
                     int lo, int hi, int digit_bits, uint32_t* d_bounds, hipStream_t stream,
-                    uint32_t bias = 0, bool range = false);
+                    uint32_t bias = 0, bool range = false, uint64_t span = 0);
 hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t* vin,
                               uint32_t* kout, uint32_t* vout, uint32_t* ktmp, uint32_t* vtmp,
                               size_t n, int lo, int hi, int digit_bits, hipStream_t stream);

@@ -803,12 +803,6 @@ __global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ key
   __shared__ uint32_t s_h[COPIES][RADIX];
   __shared__ __attribute__((aligned(16))) uint8_t s_lut[OpLds<Op>::bytes];
   const uint32_t tid = threadIdx.x;
-  const Op op = bind_op(op_in, s_lut, tid, BLOCK);
-  for (uint32_t i = tid; i < COPIES * RADIX; i += BLOCK) (&s_h[0][0])[i] = 0u;
-  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + tid; i < zero_words; i += (uint64_t)gridDim.x * BLOCK)
-    zero_buf[i] = 0u;
-  __syncthreads();
-  const uint32_t cp = tid % COPIES;
   uint64_t tile_base = (uint64_t)blockIdx.x * TILE;
   uint32_t valid;
   if constexpr (TAB) {
@@ -824,11 +818,22 @@ __global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ key
   }
   using VT = typename VecOf<K>::type;
   constexpr int PER = VecOf<K>::n;
-  if (valid == TILE && (reinterpret_cast<uintptr_t>(keys + tile_base) % 16) == 0) {
+  const bool vec = valid == TILE && (reinterpret_cast<uintptr_t>(keys + tile_base) % 16) == 0;
+  VT v[ITEMS / PER];
+  if (vec) {
+    // the tile's loads go out before the table staging and the barrier
+    // (LutDigit: the multi-GPU partition's counts 485 -> 369 us at 2^29 keys)
     const VT* vp = reinterpret_cast<const VT*>(keys + tile_base);
-    VT v[ITEMS / PER];
 #pragma unroll
     for (int j = 0; j < ITEMS / PER; ++j) v[j] = load_count_vec(&vp[j * BLOCK + tid]);
+  }
+  const Op op = bind_op(op_in, s_lut, tid, BLOCK);
+  for (uint32_t i = tid; i < COPIES * RADIX; i += BLOCK) (&s_h[0][0])[i] = 0u;
+  for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + tid; i < zero_words; i += (uint64_t)gridDim.x * BLOCK)
+    zero_buf[i] = 0u;
+  __syncthreads();
+  const uint32_t cp = tid % COPIES;
+  if (vec) {
 #pragma unroll
     for (int j = 0; j < ITEMS / PER; ++j)
 #pragma unroll
@@ -2950,11 +2955,25 @@ constexpr size_t kHybMinKeys = 1ull << 27;
 // keys (tools/hyb_sizes.py: (u64, u32) pairs 2^24 0.91x, 2^25 1.41x, 2^26 2.14x)
 constexpr size_t kHybMinKeys64 = 1ull << 25;
 constexpr size_t kHybMaxKeys = (1ull << 28) + (1ull << 24);
+// Range sorts (W bits of key - lo, W < 32: 7 LSD passes at the 8-GPU rounds'
+// W = 27, buckets of W - 16 = 11 bits) gain from fewer keys: the round sorts of
+// configs[3]'s schedule (tools/round_sorts.py, 2^29 keys per rank in 4 rounds)
+// 100M keys 1.44 -> 1.23 ms, 120M 1.49 -> 1.34 ms.
+constexpr size_t kHybMinKeysRange = (1ull << 26) + (1ull << 24);
+// u32 sorts' lower bound (A/B knob LIBSORT_HYB_MIN_LOG2, read once, for both)
+inline size_t hyb_min_keys_u32(bool range) {
+  static const int lg = [] {
+    const char* s = getenv("LIBSORT_HYB_MIN_LOG2");
+    const int v = s && *s ? atoi(s) : 0;
+    return v >= 10 && v <= 28 ? v : 0;
+  }();
+  return lg ? (size_t)1 << lg : range ? kHybMinKeysRange : kHybMinKeys;
+}
 
 
 template <int BITS, typename Op, typename K = uint32_t, typename V = NoValue>
 hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin, V* vout, V* vtmp, size_t n, int W,
-                       uint32_t bias, hipStream_t st, bool* handled) {
+                       uint32_t bias, hipStream_t st, bool* handled, uint64_t span = 0) {
   constexpr int RADIX = 1 << BITS;
   constexpr int B = tp_block<K>(BITS);
   constexpr int ITEMS = tp_items<K, V>(BITS);
@@ -2968,7 +2987,13 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   // buckets), those few are listed for the second, 6 x 256 keys larger.
   // Classes: first size 9 / 13 / 17 / 19 keys per thread.
   constexpr uint32_t kListCap = 1024;
-  const double mean = (double)n / NB;
+  // a range sort's keys lie in [bias, bias + span), span in (2^(W-1), 2^W]:
+  // only the first span / 2^(W-16) of the 16-bit prefixes (and span / 2^(W-BITS)
+  // of the top digits) are populated, each by n * 2^(W-16) / span keys on
+  // average (range rounds of the multi-GPU sort: a W = 27 round spans ~0.8 of
+  // 2^27, which the full-width shares would take for skew)
+  const double fill = span ? (double)span / std::ldexp(1.0, W) : 1.0;
+  const double mean = (double)n / (NB * fill);
   const double need = mean + 3.5 * std::sqrt(mean);
   const int cls = need <= 256.0 * 9 ? 0 : need <= 256.0 * 13 ? 1 : need <= 256.0 * 17 ? 2 : 3;
   static constexpr int kItems1[4] = {9, 13, 17, 19};
@@ -3096,7 +3121,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       }
       // a top digit well above its share (beyond sampling noise), or one
       // whose buckets would average > 0.9 of a block: the LSD sort instead
-      const double share = (double)n / RADIX;
+      const double share = (double)n / (RADIX * fill);
       if ((double)mx > 1.25 * share + 4.0 * std::sqrt(share) + 32.0 ||
           (double)mx / (double)(NB / RADIX) > 0.9 * cap)
         return hipSuccess;
@@ -3143,25 +3168,26 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
 }  // namespace
 
 hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n, int lo,
-                    int hi, int digit_bits, uint32_t* d_bounds, hipStream_t st, uint32_t bias, bool range) {
+                    int hi, int digit_bits, uint32_t* d_bounds, hipStream_t st, uint32_t bias, bool range,
+                    uint64_t span) {
   if (bias && d_bounds) return hipErrorInvalidValue;
   const int hyb = get_hybrid_mode();
   // the hybrid needs the sorted bits to determine the key: a full 32-bit
   // sort, or a range sort (keys in [bias, bias + 2^hi)) of >= 20 bits
   const bool whole = !d_bounds && lo == 0 && ((hi == 32 && !bias) || (range && hi >= 20));
   if (whole && (digit_bits == 4 || digit_bits == 8) &&
-      ((hyb == 1 && n >= kHybMinKeys && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
+      ((hyb == 1 && n >= hyb_min_keys_u32(range && hi < 32) && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
       (get_algorithm() == 0 || get_algorithm() == 3) && in != tmp) {
     bool handled = false;
     NoValue* nv = nullptr;
     if (bias && digit_bits == 4)
-      LS_TRY((sort_hybrid<4, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, bias, st, &handled)));
+      LS_TRY((sort_hybrid<4, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, bias, st, &handled, span)));
     else if (bias)
-      LS_TRY((sort_hybrid<8, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, bias, st, &handled)));
+      LS_TRY((sort_hybrid<8, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, bias, st, &handled, span)));
     else if (digit_bits == 4)
-      LS_TRY((sort_hybrid<4, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, 0u, st, &handled)));
+      LS_TRY((sort_hybrid<4, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, 0u, st, &handled, span)));
     else
-      LS_TRY((sort_hybrid<8, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, 0u, st, &handled)));
+      LS_TRY((sort_hybrid<8, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, hi, 0u, st, &handled, span)));
     if (handled) {
       ws.last_algo = 4;
       return hipSuccess;

@@ -209,6 +209,32 @@ def test_hybrid_auto_range_large(dev, oracle_mod, bits):
     np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(host))
 
 
+@pytest.mark.parametrize("frac", [0.55, 0.9])
+def test_hybrid_auto_range_partial_span(dev, oracle_mod, bits, frac):
+    """A round of the 8-GPU sort: 2^27 + 2^23 keys spanning frac * 2^27 values
+    (the round's share of the key space is no power of two, so W = 27 bits
+    of key - lo are sorted but only frac of their top digits and 16-bit
+    prefixes occur).  The hybrid must size its skew check and buckets by the
+    span and run without a fallback (it used to take the populated top
+    digits for skew, run the LSD sort after its first pass and waste it)."""
+    n, lo = (1 << 27) + (1 << 23), 0x20000000
+    span = int(frac * (1 << 27))
+    x = dev.populate_u32(n, first=9)
+    y = (((x.to(torch.int64) & 0xFFFFFFFF) * span >> 32) + lo).to(torch.int32)
+    dev.timing_enable(True)
+    dev.timing_reset()
+    try:
+        out = dev.sort_keys_range_u32(y, lo, lo + span)
+        torch.cuda.synchronize()
+        nbs, npass = dev.timing_query("bucketsort")[0], dev.timing_query("tilepass")[0]
+    finally:
+        dev.timing_enable(False)
+    assert nbs == 1
+    assert npass == 16 // bits, "a partial span must not look skewed"
+    host = y.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(host))
+
+
 def _pairs_counting(dev, kt, vt):
     dev.timing_enable(True)
     dev.timing_reset()

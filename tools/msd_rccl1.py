@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Times the msd round schedule over a one-rank RCCL communicator at 2^28
-keys (every step of the multi-GPU path except the network: sampled
+keys (MSD_LG=29: 2^29; every step of the multi-GPU path except the network: sampled
 histogram, partition, RCCL self all_to_all per round, per-round range sorts)
 against the plain single-GPU sort.  python tools/msd_rccl1.py [rounds...]"""
 import os
@@ -24,7 +24,7 @@ def main():
     from pylibsort import distrib
     pylibsort.setDigitBits(4)
     ops = distrib.HipOps()
-    n = 1 << 28
+    n = 1 << int(os.environ.get("MSD_LG", "28"))  # keys per rank (29: configs[3]'s share)
     keys = D.populate_u32(n)
     out = torch.empty_like(keys)
     tmp = torch.empty_like(keys)
