@@ -1115,8 +1115,15 @@ struct HybridGeo {
 #else
 #define LS_TP_ATTR
 #endif
+// ANY_ORDER (the keys-only MSD hybrid's digit passes): the bucket sort orders
+// every bucket completely afterwards, so a pass need not keep the input order
+// within a digit run; the rank is then one LDS atomic per key instead of the
+// ballot rank.  LIBSORT_HYB_ATOMIC_RANK=0 at build time keeps the ballot rank.
+#ifndef LIBSORT_HYB_ATOMIC_RANK
+#define LIBSORT_HYB_ATOMIC_RANK 1
+#endif
 template <int BITS, int BLOCK, int ITEMS, typename K, typename V, bool FUSE, typename Op = RadixDigit,
-          typename OpN = RadixDigit, int GEO = 0>
+          typename OpN = RadixDigit, int GEO = 0, bool ANY_ORDER = false>
 __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restrict__ kin, K* __restrict__ kout,
                                                      const V* __restrict__ vin, V* __restrict__ vout,
                                                      uint32_t n, Op op_in, OpN op_next,
@@ -1153,6 +1160,8 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   __shared__ uint32_t s_next[FUSE ? NEXT : 1];
   __shared__ uint32_t s_wsum[WAVES];
   __shared__ __attribute__((aligned(16))) uint8_t s_lut[OpLds<Op>::bytes];
+  constexpr bool ATOMIC_RANK = ANY_ORDER && LIBSORT_HYB_ATOMIC_RANK && !HAS_V;
+  __shared__ uint32_t s_acnt[ATOMIC_RANK ? WAVES : 1][ATOMIC_RANK ? RADIX : 1];
 
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
@@ -1222,7 +1231,16 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
     }
   }
   if constexpr (!HAS_V) __builtin_amdgcn_s_setprio(0);
-  rank_items<BITS, ITEMS>(k, rk, s_whist[w], full, valid, wbase, lane, op);
+  if constexpr (ATOMIC_RANK) {
+    // (one wave's LDS operations complete in order: zeroing, atomics, copy)
+    for (int d = lane; d < RADIX; d += kWave) s_acnt[w][d] = 0u;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (full || wbase + j * kWave + lane < valid) rk[j] = atomicAdd(&s_acnt[w][op(k[j])], 1u);
+    for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = (WaveCount)s_acnt[w][d];
+  } else {
+    rank_items<BITS, ITEMS>(k, rk, s_whist[w], full, valid, wbase, lane, op);
+  }
   __syncthreads();
 
   uint32_t cnt_d = 0;
@@ -1387,6 +1405,15 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 // the whole key in LDS by the thread holding the run's first key -- stable,
 // since only larger keys move.  A bucket with a run longer than 64 reloads
 // its keys and runs every step instead.
+// Keys only (FIX == 0): the first step ranks by LDS atomics instead of the
+// ballot rank.  A bucket's input order is arbitrary and equal keys are
+// indistinguishable, so the first LSD step need not be stable; only the pads
+// must stay behind the real keys of their digit (each wave's pads take their
+// ranks after its keys; later waves hold pads only).  LIBSORT_BUCKET_ATOMIC0=0
+// at build time keeps the ballot rank (A/B).
+#ifndef LIBSORT_BUCKET_ATOMIC0
+#define LIBSORT_BUCKET_ATOMIC0 1
+#endif
 template <int BITS, int BLOCK, int ITEMS, typename Op = RadixDigit, typename K = uint32_t, typename V = NoValue,
           int FIX = 0>
 __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, const V* vin, V* vout,
@@ -1412,6 +1439,8 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
   __shared__ WaveCount s_off[RADIX <= kWave ? WAVES : 1][RADIX];
   __shared__ uint32_t s_wsum[WAVES];
   __shared__ uint16_t s_runs[FIX > 0 ? WAVES : 1][kRunList];
+  constexpr bool ATOMIC0 = LIBSORT_BUCKET_ATOMIC0 && !HAS_V && FIX == 0;
+  __shared__ uint32_t s_acnt[ATOMIC0 ? WAVES : 1][ATOMIC0 ? RADIX : 1];
   if (blockIdx.x >= min(*nb, nb_cap)) return;
   const uint32_t b = ilist ? ilist[blockIdx.x] : blockIdx.x;
   const uint32_t start = bstart[b], len = blen[b];
@@ -1446,8 +1475,23 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
     for (uint32_t shift = lo_bit; shift < hi_bit; shift += BITS) {
       const uint32_t nbits = min((uint32_t)BITS, hi_bit - shift);
       const Op op = make_digit<Op>(shift, (1u << nbits) - 1u, bias);
-      for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0;
-      rank_items_t<BITS, true, ITEMS>(k, rk, s_whist[w], 0u, wbase, lane, op);
+      if (ATOMIC0 && shift == 0) {
+        // (one wave's LDS operations complete in order: the zeroing, the
+        // keys' atomics, the pads' atomics, the copy to the 16-bit row)
+        for (int d = lane; d < RADIX; d += kWave) s_acnt[w][d] = 0u;
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j)
+          if (wbase + j * kWave + lane < len) rk[j] = atomicAdd(&s_acnt[w][op(k[j])], 1u);
+        if (wbase + WSPAN > len) {
+#pragma unroll
+          for (int j = 0; j < ITEMS; ++j)
+            if (wbase + j * kWave + lane >= len) rk[j] = atomicAdd(&s_acnt[w][op(k[j])], 1u);
+        }
+        for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = (WaveCount)s_acnt[w][d];
+      } else {
+        for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0;
+        rank_items_t<BITS, true, ITEMS>(k, rk, s_whist[w], 0u, wbase, lane, op);
+      }
       __syncthreads();
       if constexpr (RADIX <= kWave) {
         // every wave derives its own run offsets (lane d: the digit-d keys of
@@ -3028,6 +3072,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   if (dstream) LS_TRY(ws.ensure_dstream(n));
   ws.part_pending.valid = false;
 
+  // keys only: the passes may reorder within a run (k_tile_pass ANY_ORDER)
+  constexpr bool kAnyOrder = std::is_same<V, NoValue>::value;
   auto buf = [&](int k) -> K* { return k == 0 ? const_cast<K*>(in) : (k & 1) ? tmp : out; };
   auto vbuf = [&](int k) -> V* { return k == 0 ? const_cast<V*>(vin) : (k & 1) ? vtmp : vout; };
   for (int k = 0; k < DEPTHS; ++k) {
@@ -3092,19 +3138,19 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       ScopedTimer tm("tilepass", st, n);
       if (BITS == 4 && !last) {
         if (k == 0)
-          hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 2>),
+          hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 2, kAnyOrder>),
                              dim3(rows), dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C,
                              ws.tb, segbase, Cn, geo);
         else
-          hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 3>),
+          hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 3, kAnyOrder>),
                              dim3(rows), dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C,
                              ws.tb, segbase, Cn, geo);
       } else if (k == 0) {
-        hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, false, Op, Op, 0>), dim3(rows),
+        hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, false, Op, Op, 0, kAnyOrder>), dim3(rows),
                            dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase,
                            Cn, geo);
       } else {
-        hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, false, Op, Op, 1>), dim3(rows),
+        hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, false, Op, Op, 1, kAnyOrder>), dim3(rows),
                            dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase,
                            Cn, geo);
       }
