@@ -2,12 +2,16 @@
 // entry points (reference invokers.cu / utils.cu), additive device-resident
 // entry points, PCG32 host generator and the per-kernel timing registry.
 //
-// NOTE on return types: the reference ABI declares `bool` returns.  ctypes
-// callers (faasTest/pylibsort/sort.py:101,118) never set `restype`, so they
-// read the whole of eax; a `bool` return only defines al.  The entry points
-// are therefore DEFINED here (this TU does not include libsort.h) with an
-// `int` return of 0/1: bool callers (cgo, the C++ harness) read al, int
-// callers read eax, and both see the right value.
+// NOTE on return types: this TU includes libsort.h, so the compiler checks
+// every entry point against its declaration (`bool` as in the reference,
+// libsort/libsort.h:14-32).  ctypes callers (faasTest/pylibsort/sort.py:
+// 101,118) never set `restype` and read the whole of eax, but a `bool`
+// return only defines al (clang: `movb $1, %al`).  So each bool entry point
+// is exported as an alias of an int-returning definition (LS_BOOL_ENTRY
+// below): the machine code leaves 0 or 1 in the whole of eax
+// (tests/test_abi_cpu.py::test_bool_exports_define_eax).
+#include "libsort.h"
+
 #include <hip/hip_runtime.h>
 #include <rocprofiler-sdk-roctx/roctx.h>
 #include <stdint.h>
@@ -26,6 +30,15 @@
 #include "radix.h"
 
 #define LIBSORT_EXPORT extern "C" __attribute__((visibility("default")))
+// An entry point that libsort.h declares `bool`: the exported symbol is an
+// alias of an int-returning definition (result 0 or 1 in the whole of eax),
+// declared here with the header's exact signature, so the compiler checks it
+// against libsort.h and callers reading al (bool: cgo, C++) or eax (ctypes'
+// default restype) both see 0/1.  Host-only TU (hipcc --offload-host-only).
+#define LS_BOOL_ENTRY(name, ...)                                                                \
+  extern "C" int name##_impl(__VA_ARGS__);                                                     \
+  LIBSORT_EXPORT bool name(__VA_ARGS__) __attribute__((alias(#name "_impl")));                 \
+  extern "C" int name##_impl(__VA_ARGS__)
 
 namespace lsort {
 
@@ -638,7 +651,7 @@ using namespace lsort;
 // ===========================================================================
 // Part 1: reference ABI
 // ===========================================================================
-LIBSORT_EXPORT int initLibSort(void) {
+LS_BOOL_ENTRY(initLibSort, void) {
   std::lock_guard<std::mutex> lk(g_init_mu);
   if (g_dev_locks != nullptr) {
     set_error("attempted to initialize multiple times!");
@@ -663,16 +676,16 @@ LIBSORT_EXPORT int initLibSort(void) {
   return 1;
 }
 
-LIBSORT_EXPORT int gpuPartial(uint32_t* h_in, uint32_t* boundaries, size_t h_in_len, uint32_t offset,
+LS_BOOL_ENTRY(gpuPartial, uint32_t* h_in, uint32_t* boundaries, size_t h_in_len, uint32_t offset,
                               uint32_t width) {
   return host_sort(h_in, boundaries, h_in_len, offset, width, true) ? 1 : 0;
 }
 
-LIBSORT_EXPORT int providedGpu(unsigned int* h_in, size_t len) {
+LS_BOOL_ENTRY(providedGpu, unsigned int* h_in, size_t len) {
   return host_sort(h_in, nullptr, len, 0, 32, false) ? 1 : 0;
 }
 
-LIBSORT_EXPORT int providedCpu(unsigned int* in, size_t len) {
+LS_BOOL_ENTRY(providedCpu, unsigned int* in, size_t len) {
   std::sort(in, in + len);
   return 1;
 }
@@ -690,7 +703,7 @@ LIBSORT_EXPORT void populateInput(uint32_t* arr, size_t nelem) {
   g_pcg_state = state;
 }
 
-LIBSORT_EXPORT int gpuPartialProfile(uint32_t* h_in, uint32_t* boundaries, size_t h_in_len,
+LS_BOOL_ENTRY(gpuPartialProfile, uint32_t* h_in, uint32_t* boundaries, size_t h_in_len,
                                      uint32_t offset, uint32_t width) {
   roctxRangePush("gpuPartialProfile");
   int r = gpuPartial(h_in, boundaries, h_in_len, offset, width);
@@ -698,7 +711,7 @@ LIBSORT_EXPORT int gpuPartialProfile(uint32_t* h_in, uint32_t* boundaries, size_
   return r;
 }
 
-LIBSORT_EXPORT int providedGpuProfile(unsigned int* h_in, size_t h_in_len) {
+LS_BOOL_ENTRY(providedGpuProfile, unsigned int* h_in, size_t h_in_len) {
   roctxRangePush("providedGpuProfile");
   int r = providedGpu(h_in, h_in_len);
   roctxRangePop();
@@ -708,9 +721,9 @@ LIBSORT_EXPORT int providedGpuProfile(unsigned int* h_in, size_t h_in_len) {
 // ===========================================================================
 // Part 2: additive API
 // ===========================================================================
-LIBSORT_EXPORT int gpuFullSort(unsigned int* h_in, size_t len) { return providedGpu(h_in, len); }
+LS_BOOL_ENTRY(gpuFullSort, unsigned int* h_in, size_t len) { return providedGpu(h_in, len); }
 
-LIBSORT_EXPORT int gpuPartialSort(uint32_t* h_in, uint32_t* boundaries, size_t h_in_len, uint32_t offset,
+LS_BOOL_ENTRY(gpuPartialSort, uint32_t* h_in, uint32_t* boundaries, size_t h_in_len, uint32_t offset,
                                   uint32_t width) {
   return gpuPartial(h_in, boundaries, h_in_len, offset, width);
 }
@@ -727,7 +740,7 @@ static bool check_range(size_t n, uint32_t offset, uint32_t width, uint32_t keyb
   return true;
 }
 
-LIBSORT_EXPORT int libsortSortKeysU32(const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp, size_t n,
+LS_BOOL_ENTRY(libsortSortKeysU32, const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp, size_t n,
                                       uint32_t offset, uint32_t width, uint32_t* d_boundaries,
                                       void* stream) {
   if (!check_range(n, offset, width, 32)) return 0;
@@ -749,7 +762,7 @@ LIBSORT_EXPORT int libsortSortKeysU32(const uint32_t* d_in, uint32_t* d_out, uin
              : 0;
 }
 
-LIBSORT_EXPORT int libsortSortKeysRangeU32(const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp, size_t n,
+LS_BOOL_ENTRY(libsortSortKeysRangeU32, const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp, size_t n,
                                            uint32_t lo, uint64_t hi, void* stream) {
   if (hi <= (uint64_t)lo || hi > (1ull << 32)) {
     set_error("libsortSortKeysRangeU32: need lo < hi <= 2^32");
@@ -773,7 +786,7 @@ LIBSORT_EXPORT int libsortSortKeysRangeU32(const uint32_t* d_in, uint32_t* d_out
              : 0;
 }
 
-LIBSORT_EXPORT int libsortSortPairsU64U32(const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
+LS_BOOL_ENTRY(libsortSortPairsU64U32, const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
                                           uint32_t* d_vout, uint64_t* d_ktmp, uint32_t* d_vtmp, size_t n,
                                           uint32_t offset, uint32_t width, void* stream) {
   if (!check_range(n, offset, width, 64)) return 0;
@@ -792,7 +805,7 @@ LIBSORT_EXPORT int libsortSortPairsU64U32(const uint64_t* d_kin, const uint32_t*
              : 0;
 }
 
-LIBSORT_EXPORT int libsortSortKeysU64(const uint64_t* d_in, uint64_t* d_out, uint64_t* d_tmp, size_t n,
+LS_BOOL_ENTRY(libsortSortKeysU64, const uint64_t* d_in, uint64_t* d_out, uint64_t* d_tmp, size_t n,
                                       uint32_t offset, uint32_t width, void* stream) {
   if (!check_range(n, offset, width, 64)) return 0;
   if (n > 0 && (!d_in || !d_out || !d_tmp || d_tmp == d_out || (const uint64_t*)d_tmp == d_in)) {
@@ -809,7 +822,7 @@ LIBSORT_EXPORT int libsortSortKeysU64(const uint64_t* d_in, uint64_t* d_out, uin
              : 0;
 }
 
-LIBSORT_EXPORT int libsortSortPairsU64U64(const uint64_t* d_kin, const uint64_t* d_vin, uint64_t* d_kout,
+LS_BOOL_ENTRY(libsortSortPairsU64U64, const uint64_t* d_kin, const uint64_t* d_vin, uint64_t* d_kout,
                                           uint64_t* d_vout, uint64_t* d_ktmp, uint64_t* d_vtmp, size_t n,
                                           uint32_t offset, uint32_t width, void* stream) {
   if (!check_range(n, offset, width, 64)) return 0;
@@ -828,7 +841,7 @@ LIBSORT_EXPORT int libsortSortPairsU64U64(const uint64_t* d_kin, const uint64_t*
              : 0;
 }
 
-LIBSORT_EXPORT int libsortSortPairsU32U32(const uint32_t* d_kin, const uint32_t* d_vin, uint32_t* d_kout,
+LS_BOOL_ENTRY(libsortSortPairsU32U32, const uint32_t* d_kin, const uint32_t* d_vin, uint32_t* d_kout,
                                           uint32_t* d_vout, uint32_t* d_ktmp, uint32_t* d_vtmp, size_t n,
                                           uint32_t offset, uint32_t width, void* stream) {
   if (!check_range(n, offset, width, 32)) return 0;
@@ -847,7 +860,7 @@ LIBSORT_EXPORT int libsortSortPairsU32U32(const uint32_t* d_kin, const uint32_t*
              : 0;
 }
 
-LIBSORT_EXPORT int libsortHistogramU32(const uint32_t* d_keys, size_t n, uint32_t shift, uint32_t bits,
+LS_BOOL_ENTRY(libsortHistogramU32, const uint32_t* d_keys, size_t n, uint32_t shift, uint32_t bits,
                                        uint32_t* d_hist, void* stream) {
   hipStream_t st = as_stream(stream);
   return with_current_ws(st, [&](Workspace& ws) {
@@ -858,7 +871,7 @@ LIBSORT_EXPORT int libsortHistogramU32(const uint32_t* d_keys, size_t n, uint32_
              : 0;
 }
 
-LIBSORT_EXPORT int libsortPartitionU32(const uint32_t* d_in, uint32_t* d_out, size_t n,
+LS_BOOL_ENTRY(libsortPartitionU32, const uint32_t* d_in, uint32_t* d_out, size_t n,
                                        const uint32_t* splitters, uint32_t nsplit, uint32_t* d_counts,
                                        void* stream) {
   if (nsplit > 0 && !splitters) {
@@ -878,7 +891,7 @@ LIBSORT_EXPORT int libsortPartitionU32(const uint32_t* d_in, uint32_t* d_out, si
              : 0;
 }
 
-LIBSORT_EXPORT int libsortPartitionLutU32(const uint32_t* d_in, uint32_t* d_out, size_t n, const uint8_t* d_lut,
+LS_BOOL_ENTRY(libsortPartitionLutU32, const uint32_t* d_in, uint32_t* d_out, size_t n, const uint8_t* d_lut,
                                           uint32_t lut_shift, uint32_t nbuckets, uint32_t* d_bounds,
                                           void* stream) {
   if (n > 0 && (const uint32_t*)d_out == d_in) {
@@ -894,7 +907,7 @@ LIBSORT_EXPORT int libsortPartitionLutU32(const uint32_t* d_in, uint32_t* d_out,
              : 0;
 }
 
-LIBSORT_EXPORT int libsortPartitionLutU64U32(const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
+LS_BOOL_ENTRY(libsortPartitionLutU64U32, const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
                                              uint32_t* d_vout, size_t n, const uint8_t* d_lut, uint32_t lut_shift,
                                              uint32_t nbuckets, uint32_t* d_bounds, void* stream) {
   hipStream_t st = as_stream(stream);
@@ -907,7 +920,7 @@ LIBSORT_EXPORT int libsortPartitionLutU64U32(const uint64_t* d_kin, const uint32
              : 0;
 }
 
-LIBSORT_EXPORT int libsortPartitionLutCountU32(const uint32_t* d_in, size_t n, const uint8_t* d_lut,
+LS_BOOL_ENTRY(libsortPartitionLutCountU32, const uint32_t* d_in, size_t n, const uint8_t* d_lut,
                                                uint32_t lut_shift, uint32_t nbuckets, uint32_t* d_bounds,
                                                void* stream) {
   hipStream_t st = as_stream(stream);
@@ -920,7 +933,7 @@ LIBSORT_EXPORT int libsortPartitionLutCountU32(const uint32_t* d_in, size_t n, c
              : 0;
 }
 
-LIBSORT_EXPORT int libsortPartitionLutScatterU32(const uint32_t* d_in, uint32_t* d_out, size_t n, const uint8_t* d_lut,
+LS_BOOL_ENTRY(libsortPartitionLutScatterU32, const uint32_t* d_in, uint32_t* d_out, size_t n, const uint8_t* d_lut,
                                                  uint32_t lut_shift, uint32_t nbuckets, void* stream) {
   if (n > 0 && (const uint32_t*)d_out == d_in) {
     set_error("libsortPartitionLutScatterU32: out of place only");
@@ -936,7 +949,7 @@ LIBSORT_EXPORT int libsortPartitionLutScatterU32(const uint32_t* d_in, uint32_t*
              : 0;
 }
 
-LIBSORT_EXPORT int libsortPartitionLutCountU64U32(const uint64_t* d_kin, const uint32_t* d_vin, size_t n,
+LS_BOOL_ENTRY(libsortPartitionLutCountU64U32, const uint64_t* d_kin, const uint32_t* d_vin, size_t n,
                                                   const uint8_t* d_lut, uint32_t lut_shift, uint32_t nbuckets,
                                                   uint32_t* d_bounds, void* stream) {
   hipStream_t st = as_stream(stream);
@@ -949,7 +962,7 @@ LIBSORT_EXPORT int libsortPartitionLutCountU64U32(const uint64_t* d_kin, const u
              : 0;
 }
 
-LIBSORT_EXPORT int libsortPartitionLutScatterU64U32(const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
+LS_BOOL_ENTRY(libsortPartitionLutScatterU64U32, const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
                                                     uint32_t* d_vout, size_t n, const uint8_t* d_lut,
                                                     uint32_t lut_shift, uint32_t nbuckets, void* stream) {
   hipStream_t st = as_stream(stream);
@@ -962,7 +975,7 @@ LIBSORT_EXPORT int libsortPartitionLutScatterU64U32(const uint64_t* d_kin, const
              : 0;
 }
 
-LIBSORT_EXPORT int libsortSegmentCopyU32(const uint32_t* d_src, uint32_t* d_dst, size_t nseg,
+LS_BOOL_ENTRY(libsortSegmentCopyU32, const uint32_t* d_src, uint32_t* d_dst, size_t nseg,
                                          const uint64_t* src_off, const uint64_t* dst_off,
                                          const uint64_t* len, void* stream) {
   hipStream_t st = as_stream(stream);
@@ -974,7 +987,7 @@ LIBSORT_EXPORT int libsortSegmentCopyU32(const uint32_t* d_src, uint32_t* d_dst,
              : 0;
 }
 
-LIBSORT_EXPORT int libsortPlanHistogramU32(const uint32_t* d_keys, size_t n, uint32_t block, uint32_t stride,
+LS_BOOL_ENTRY(libsortPlanHistogramU32, const uint32_t* d_keys, size_t n, uint32_t block, uint32_t stride,
                                            int64_t* d_out, void* stream) {
   if (!d_out || block == 0 || (n > 0 && !d_keys)) {
     set_error("libsortPlanHistogramU32: bad arguments");
@@ -988,7 +1001,7 @@ LIBSORT_EXPORT int libsortPlanHistogramU32(const uint32_t* d_keys, size_t n, uin
              : 0;
 }
 
-LIBSORT_EXPORT int libsortPlanRounds(const int64_t* d_rows, uint32_t nranks, uint32_t ld, uint32_t rounds,
+LS_BOOL_ENTRY(libsortPlanRounds, const int64_t* d_rows, uint32_t nranks, uint32_t ld, uint32_t rounds,
                                      double growth, uint8_t* d_lut, int64_t* d_est, void* stream) {
   if (!d_rows || !d_lut || !d_est || nranks < 1 || rounds < 1 || nranks * rounds > 256 || ld < 4096) {
     set_error("libsortPlanRounds: need 1 <= nranks * rounds <= 256 and ld >= 4096");
@@ -999,7 +1012,7 @@ LIBSORT_EXPORT int libsortPlanRounds(const int64_t* d_rows, uint32_t nranks, uin
              : 0;
 }
 
-LIBSORT_EXPORT int libsortDeltaMaxGapU32(const uint32_t* d_keys, size_t n, uint32_t* d_maxgap, void* stream) {
+LS_BOOL_ENTRY(libsortDeltaMaxGapU32, const uint32_t* d_keys, size_t n, uint32_t* d_maxgap, void* stream) {
   if (!d_maxgap || (n > 0 && !d_keys)) {
     set_error("libsortDeltaMaxGapU32: bad arguments");
     return 0;
@@ -1007,7 +1020,7 @@ LIBSORT_EXPORT int libsortDeltaMaxGapU32(const uint32_t* d_keys, size_t n, uint3
   return hip_ok(delta_maxgap_u32(d_keys, n, d_maxgap, as_stream(stream)), "libsortDeltaMaxGapU32") ? 1 : 0;
 }
 
-LIBSORT_EXPORT int libsortDeltaPackU32(const uint32_t* d_keys, size_t n, const uint32_t* d_maxgap, uint32_t* d_out,
+LS_BOOL_ENTRY(libsortDeltaPackU32, const uint32_t* d_keys, size_t n, const uint32_t* d_maxgap, uint32_t* d_out,
                                        void* stream) {
   if (!d_maxgap || (n > 0 && (!d_keys || !d_out))) {
     set_error("libsortDeltaPackU32: bad arguments");
@@ -1016,7 +1029,7 @@ LIBSORT_EXPORT int libsortDeltaPackU32(const uint32_t* d_keys, size_t n, const u
   return hip_ok(delta_pack_u32(d_keys, n, d_maxgap, d_out, as_stream(stream)), "libsortDeltaPackU32") ? 1 : 0;
 }
 
-LIBSORT_EXPORT int libsortDeltaUnpackU32(const uint32_t* d_in, size_t n, uint32_t bits, uint32_t* d_keys,
+LS_BOOL_ENTRY(libsortDeltaUnpackU32, const uint32_t* d_in, size_t n, uint32_t bits, uint32_t* d_keys,
                                          void* stream) {
   if (bits > 32 || (n > 0 && (!d_in || !d_keys))) {
     set_error("libsortDeltaUnpackU32: bad arguments");
@@ -1025,7 +1038,7 @@ LIBSORT_EXPORT int libsortDeltaUnpackU32(const uint32_t* d_in, size_t n, uint32_
   return hip_ok(delta_unpack_u32(d_in, n, bits, d_keys, as_stream(stream)), "libsortDeltaUnpackU32") ? 1 : 0;
 }
 
-LIBSORT_EXPORT int libsortMergeU32(const uint32_t* d_a, size_t na, const uint32_t* d_b, size_t nb, uint32_t* d_out,
+LS_BOOL_ENTRY(libsortMergeU32, const uint32_t* d_a, size_t na, const uint32_t* d_b, size_t nb, uint32_t* d_out,
                                    void* stream) {
   if ((na > 0 && !d_a) || (nb > 0 && !d_b) || (na + nb > 0 && !d_out) || (d_out && (d_out == d_a || d_out == d_b))) {
     set_error("libsortMergeU32: bad arguments (out must be distinct from both inputs)");
@@ -1034,7 +1047,7 @@ LIBSORT_EXPORT int libsortMergeU32(const uint32_t* d_a, size_t na, const uint32_
   return hip_ok(merge_u32(d_a, na, d_b, nb, d_out, as_stream(stream)), "libsortMergeU32") ? 1 : 0;
 }
 
-LIBSORT_EXPORT int libsortPopulateDevice(uint32_t* d_out, size_t n, uint64_t first, void* stream) {
+LS_BOOL_ENTRY(libsortPopulateDevice, uint32_t* d_out, size_t n, uint64_t first, void* stream) {
   return hip_ok(populate_device(d_out, n, first, as_stream(stream)), "libsortPopulateDevice") ? 1 : 0;
 }
 
@@ -1056,12 +1069,12 @@ LIBSORT_EXPORT int libsortSetBoundaryMode(int mode) {
 LIBSORT_EXPORT void libsortTimingEnable(bool on) { timing_enable(on); }
 LIBSORT_EXPORT void libsortTimingReset(void) { timing_reset(); }
 LIBSORT_EXPORT void libsortTimingFilter(const char* kernels) { timing_filter(kernels); }
-LIBSORT_EXPORT int libsortTimingQuery(const char* kernel, uint64_t* launches, double* total_ms,
+LS_BOOL_ENTRY(libsortTimingQuery, const char* kernel, uint64_t* launches, double* total_ms,
                                       uint64_t* total_keys) {
   return timing_query(kernel, launches, total_ms, total_keys) ? 1 : 0;
 }
 
-LIBSORT_EXPORT int gpuDistribSort(uint32_t* h_in, size_t len, int ngpu) {
+LS_BOOL_ENTRY(gpuDistribSort, uint32_t* h_in, size_t len, int ngpu) {
   MultiReservation res;
   if (!res.reserve(ngpu <= 0 ? g_ndev : ngpu)) return 0;
   if (len == 0) return 1;
@@ -1073,7 +1086,7 @@ LIBSORT_EXPORT int gpuDistribSort(uint32_t* h_in, size_t len, int ngpu) {
   return distrib_sort_host_u32(h_in, len, d.data(), (int)d.size(), 0u, g_digit_bits.load()) ? 1 : 0;
 }
 
-LIBSORT_EXPORT int libsortDistribSortU32(int nranks, const int* devices, const uint32_t* const* d_in,
+LS_BOOL_ENTRY(libsortDistribSortU32, int nranks, const int* devices, const uint32_t* const* d_in,
                                          const size_t* n_in, uint32_t* const* d_out, size_t* n_out, uint32_t flags) {
   if (nranks < 1 || !devices || !d_in || !n_in || !d_out || !n_out) {
     set_error("libsortDistribSortU32: need nranks >= 1 and non-NULL tables");
@@ -1097,7 +1110,7 @@ LIBSORT_EXPORT int libsortDistribSortU32(int nranks, const int* devices, const u
   return ok ? 1 : 0;
 }
 
-LIBSORT_EXPORT int libsortReleaseWorkspace(void) {
+LS_BOOL_ENTRY(libsortReleaseWorkspace, void) {
   distrib_release();
   release_all_workspaces();
   return 1;

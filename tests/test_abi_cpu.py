@@ -108,6 +108,46 @@ def test_ctypes_default_int_restype_sees_false():
     assert r in (0, 1)
 
 
+def bool_declared_symbols():
+    return sorted(set(re.findall(r"LIBSORT_API\s+bool\s+(\w+)\s*\(", HEADER.read_text())))
+
+
+def test_bool_exports_define_eax():
+    """libsort.h declares the reference entry points `bool`
+    (libsort/libsort.h:14-32), but ctypes callers with the default restype
+    (faasTest/pylibsort/sort.py:101,118) read the whole of eax, and a C++
+    `bool` return defines only al.  Every bool export must therefore be an
+    alias of the int-returning <name>_impl (libsort_abi.cpp LS_BOOL_ENTRY):
+    same address in the symbol table, and the code writes 32-bit eax (no
+    `mov ..., %al` / `set.. %al` as the last write before a ret)."""
+    out = subprocess.run(["nm", "--defined-only", str(LIB)], capture_output=True, text=True, check=True).stdout
+    addr = {}
+    for ln in out.splitlines():
+        parts = ln.split()
+        if len(parts) == 3:
+            addr.setdefault(parts[2], parts[0])
+    names = bool_declared_symbols()
+    assert len(names) >= 30
+    for n in names:
+        assert n in addr and n + "_impl" in addr, n
+        assert addr[n] == addr[n + "_impl"], "%s is not an alias of %s_impl" % (n, n)
+    # the exported dynamic symbols do not include the _impl names
+    dyn = subprocess.run(["nm", "-D", "--defined-only", str(LIB)], capture_output=True, text=True,
+                         check=True).stdout
+    assert "_impl" not in dyn
+    # machine code of a leaf entry point: returns with a 32-bit write of eax
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if os.path.exists(objdump):
+        dis = subprocess.run([objdump, "-d", "--no-show-raw-insn", "--disassemble-symbols=providedCpu_impl",
+                              str(LIB)], capture_output=True, text=True, check=True).stdout
+        lines = [ln for ln in dis.splitlines() if "\t" in ln]
+        rets = [i for i, ln in enumerate(lines) if ln.strip().endswith("retq")]
+        assert rets
+        for i in rets:
+            last_write = next((ln for ln in reversed(lines[:i]) if re.search(r"%(e?ax|al)\b", ln)), "")
+            assert "%eax" in last_write or "%rax" in last_write, last_write
+
+
 def test_tunables_validate():
     import pylibsort
     prev = pylibsort.setDigitBits(4)
