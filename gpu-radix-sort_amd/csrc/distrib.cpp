@@ -368,12 +368,20 @@ bool run_lsd(Ctx& c, const std::vector<const uint32_t*>& in, const std::vector<u
       dst[r] = c.ranks[r].recv.u32();
     }
     if (!move_pieces(c, o.pieces, src, dst, use_rccl, self_rccl)) return false;
-    // gather into bucket-major / rank-minor order on the compute stream
+    // gather into bucket-major / rank-minor order on the compute stream.
+    // Every compute stream waits for EVERY device's communication stream: a
+    // peer copy (copy mode across devices) is pulled on the receiver's stream
+    // from the sender's `part`, which the sender's next partial sort rewrites
+    // (write-after-read across devices).
     const bool last = step + 1 == 32 / W;
     for (auto& u : c.uniq)
-      if (!ok_hip(hipSetDevice(u->dev), "hipSetDevice") || !ok_hip(hipEventRecord(u->ev_comm, u->cs), "record") ||
-          !ok_hip(hipStreamWaitEvent(u->st, u->ev_comm, 0), "wait"))
+      if (!ok_hip(hipSetDevice(u->dev), "hipSetDevice") || !ok_hip(hipEventRecord(u->ev_comm, u->cs), "record"))
         return false;
+    for (auto& u : c.uniq) {
+      if (!ok_hip(hipSetDevice(u->dev), "hipSetDevice")) return false;
+      for (auto& v : c.uniq)
+        if (!ok_hip(hipStreamWaitEvent(u->st, v->ev_comm, 0), "wait")) return false;
+    }
     for (int r = 0; r < R; ++r) {
       RankState& s = c.ranks[r];
       uint32_t* nxt = last ? out[r] : (step & 1 ? s.outb.u32() : s.alt.u32());

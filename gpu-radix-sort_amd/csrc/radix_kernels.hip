@@ -3015,6 +3015,15 @@ inline size_t hyb_min_keys_u32(bool range) {
 }
 
 
+// The hybrid waits on the host twice per call (its skew and bucket-size
+// read-backs), which a stream under graph capture cannot do: captured sorts
+// take the LSD passes (hipStreamIsCapturing).
+inline int hybrid_mode_for(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return 0;
+  return get_hybrid_mode();
+}
+
 template <int BITS, typename Op, typename K = uint32_t, typename V = NoValue>
 hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin, V* vout, V* vtmp, size_t n, int W,
                        uint32_t bias, hipStream_t st, bool* handled, uint64_t span = 0) {
@@ -3217,7 +3226,7 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
                     int hi, int digit_bits, uint32_t* d_bounds, hipStream_t st, uint32_t bias, bool range,
                     uint64_t span) {
   if (bias && d_bounds) return hipErrorInvalidValue;
-  const int hyb = get_hybrid_mode();
+  const int hyb = hybrid_mode_for(st);
   // the hybrid needs the sorted bits to determine the key: a full 32-bit
   // sort, or a range sort (keys in [bias, bias + 2^hi)) of >= 20 bits
   const bool whole = !d_bounds && lo == 0 && ((hi == 32 && !bias) || (range && hi >= 20));
@@ -3276,7 +3285,7 @@ hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t
                               uint32_t* vout, uint32_t* ktmp, uint32_t* vtmp, size_t n, int lo, int hi,
                               int digit_bits, hipStream_t st) {
   // full-width sorts: the MSD hybrid (stable; the payloads travel with the keys)
-  const int hyb = get_hybrid_mode();
+  const int hyb = hybrid_mode_for(st);
   if (lo == 0 && hi == 32 && (digit_bits == 8 || digit_bits == 4) &&
       ((hyb == 1 && n >= kHybMinKeys && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
       (get_algorithm() == 0 || get_algorithm() == 3) && kin != ktmp) {
@@ -3302,7 +3311,7 @@ hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t
 template <typename V>
 hipError_t sort_64_hybrid_or_lsd(Workspace& ws, const uint64_t* kin, uint64_t* kout, uint64_t* ktmp, const V* vin,
                                  V* vout, V* vtmp, size_t n, int lo, int hi, int digit_bits, hipStream_t st) {
-  const int hyb = get_hybrid_mode();
+  const int hyb = hybrid_mode_for(st);
   if (lo == 0 && hi == 64 && (digit_bits == 8 || digit_bits == 4) &&
       ((hyb == 1 && n >= kHybMinKeys64 && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
       (get_algorithm() == 0 || get_algorithm() == 3) && (const void*)kin != (const void*)ktmp) {

@@ -81,7 +81,11 @@ LIBSORT_API bool gpuPartialSort(uint32_t* h_in, uint32_t* boundaries, size_t h_i
  * d_in is read-only; the result is written to d_out; d_tmp is scratch of n
  * keys.  d_in may equal d_out (in place); d_tmp must alias neither.
  * d_boundaries (nullable, device, 2^width uint32) receives the same
- * boundaries as gpuPartial.  The call is asynchronous w.r.t. the host. */
+ * boundaries as gpuPartial.  The work is enqueued on `stream`; the call
+ * returns before it completes, except that a full-width sort served by the
+ * MSD hybrid (libsortSetHybrid) waits on the host for two small read-backs
+ * while its first and last digit passes run.  Under stream capture (HIP
+ * graphs) the hybrid is never taken, so a captured call never waits. */
 LIBSORT_API bool libsortSortKeysU32(const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp,
                                     size_t n, uint32_t offset, uint32_t width,
                                     uint32_t* d_boundaries, void* stream);

@@ -193,6 +193,32 @@ def test_bench_self_launch_rehearsal():
     assert line["config"]["global_keys"] == 2 << 20 and line["variants"]["digit8"]["value"] > 0
 
 
+def test_bench_self_launch_rehearsal_world8():
+    """configs[3]'s world size on the HIP kernels: `bench.py --gpus 8` with
+    eight gloo ranks sharing the one GPU (BENCH_REHEARSAL), 2^20 keys per
+    rank: the 8-rank plan, partition, exchange, round sorts, re-cut and the
+    collective verification all run on the GPU, and rank 0's line is relayed."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import json
+    import os
+    import pathlib
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["BENCH_REHEARSAL"] = "1"
+    cmd = [sys.executable, str(root / "bench.py"), "--gpus", "8", "--steps", "2", "--warmup", "1", "--keys-log2", "20",
+           "--no-variants"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(root))
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 8 and line["verified"] is True and line["rehearsal"]
+    assert line["config"]["global_keys"] == 8 << 20
+
+
 def test_bench_single_gpu_line_contract():
     """bench.py at N=1 (small steps): one JSON line with the driver's keys,
     the roofline object (live per-launch pass time), a verified sort, the

@@ -4,7 +4,8 @@ libsortDistribSortU32, csrc/distrib.cpp) on the one-GPU test box:
 - one rank over a real single-process RCCL communicator (ncclCommInitAll of
   one device) with every piece sent through RCCL (LIBSORT_DISTRIB_SELF_RCCL),
   both schedules;
-- 2-5 ranks sharing the GPU (device-copy exchanges: RCCL refuses two ranks
+- 2, 3, 5 and 8 ranks sharing the GPU (8 = configs[3]'s world size: 32 (round,
+  rank) buckets, 8-way re-cut and LSD segment gathers on the HIP kernels) (device-copy exchanges: RCCL refuses two ranks
   on one GPU), both schedules, ragged and empty shards, duplicate-heavy and
   skewed inputs (the range schedule falls back to the LSD rounds);
 - the host-pointer entry point gpuDistribSort against the reference's golden
@@ -89,7 +90,7 @@ def _cases(oracle):
     }
 
 
-@pytest.mark.parametrize("R", [2, 3, 5])
+@pytest.mark.parametrize("R", [2, 3, 5, 8])
 @pytest.mark.parametrize("lsd", [False, True], ids=["range", "lsd"])
 @pytest.mark.parametrize("case", ["pcg", "dups", "skewtop", "allequal", "small", "tiny"])
 def test_ranks_sharing_the_gpu(D, oracle_mod, R, lsd, case):

@@ -469,3 +469,32 @@ def test_hybrid_auto_pairs_u32_u32_large(dev, oracle_mod, bits):
     rk, rv = oracle_mod.stable_sort_kv32(_u32(kt), np.arange(n, dtype=np.uint32))
     np.testing.assert_array_equal(_u32(ok_), rk)
     np.testing.assert_array_equal(_u32(ov), rv)
+
+
+def test_graph_capture_skips_the_host_waits(dev, oracle_mod):
+    """Under HIP stream capture a full sort never takes the hybrid (whose two
+    host read-backs cannot happen inside a graph): a forced-hybrid
+    size captured into a graph by torch.cuda.graph replays to the oracle's
+    result."""
+    import pylibsort
+    x = oracle_mod.pcg((1 << 20) + 77, first=3)
+    keys = _tensor(x)
+    out = torch.empty_like(keys)
+    tmp = torch.empty_like(keys)
+    s = torch.cuda.Stream()
+    prev = pylibsort.setHybrid("off")
+    try:
+        with torch.cuda.stream(s):  # warm-up on the capture stream: workspace allocated, same stream
+            dev.sort_keys_u32(keys, out=out, tmp=tmp)
+        s.synchronize()
+        pylibsort.setHybrid("force")
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            dev.sort_keys_u32(keys, out=out, tmp=tmp)
+        out.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+    finally:
+        pylibsort.setHybrid(prev)
