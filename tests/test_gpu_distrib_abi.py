@@ -49,7 +49,7 @@ def _cut(x, R, ragged=False):
     if not ragged:
         S = -(-x.size // R)
         return [x[r * S:(r + 1) * S] for r in range(R)]
-    w = np.array([3, 0, 1, 5, 2][:R], dtype=np.float64) + 1e-9
+    w = np.array([3, 0, 1, 5, 2, 4, 0, 2][:R], dtype=np.float64) + 1e-9
     cuts = np.concatenate([[0], np.round(np.cumsum(w) / w.sum() * x.size).astype(np.int64)])
     cuts[-1] = x.size
     return [x[cuts[r]:cuts[r + 1]] for r in range(R)]
