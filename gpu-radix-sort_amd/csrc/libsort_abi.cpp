@@ -786,6 +786,24 @@ LS_BOOL_ENTRY(libsortSortKeysRangeU32, const uint32_t* d_in, uint32_t* d_out, ui
              : 0;
 }
 
+LS_BOOL_ENTRY(libsortSortPiecesU32, const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp, size_t n,
+              const uint64_t* off, const uint64_t* len, const uint32_t* seg, size_t npieces, uint32_t nseg,
+              uint32_t bits, void* stream) {
+  if (n > 0 && (!d_in || !d_out || !d_tmp || d_out == d_in || d_tmp == d_out || (const uint32_t*)d_tmp == d_in ||
+                !off || !len || !seg)) {
+    set_error("libsortSortPiecesU32: need d_in, d_out, d_tmp distinct and the three piece tables");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(sort_pieces_u32(ws, d_in, d_out, d_tmp, n, off, len, seg, npieces, nseg, (int)bits,
+                                         g_digit_bits.load(), st),
+                         "libsortSortPiecesU32 (pieces in segment order, seg < nseg, lengths summing to n)");
+         })
+             ? 1
+             : 0;
+}
+
 LS_BOOL_ENTRY(libsortSortPairsU64U32, const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
                                           uint32_t* d_vout, uint64_t* d_ktmp, uint32_t* d_vtmp, size_t n,
                                           uint32_t offset, uint32_t width, void* stream) {

@@ -154,6 +154,17 @@ inline int num_passes(int width, int bits) { return width <= 0 ? 0 : (width + bi
 hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n,
                     int lo, int hi, int digit_bits, uint32_t* d_bounds, hipStream_t stream,
                     uint32_t bias = 0, bool range = false, uint64_t span = 0);
+// Sort of pre-partitioned keys (a multi-GPU round's receive buffer, whose
+// pieces arrive partitioned by the senders): piece p = in[off[p], off[p] +
+// len[p]) of segment seg[p] (host arrays; np pieces in non-decreasing segment
+// order, seg < nseg); the keys of segment s share their bits [bits, 32) and
+// those increase with s.  out (distinct from in and tmp) receives the n =
+// sum(len) keys sorted; tmp: scratch of n keys.  The MSD hybrid starts from
+// the pieces' own tiles (no gather, no pass over the top bits); small or
+// skewed inputs are gathered and LSD-sorted.
+hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n,
+                           const uint64_t* off, const uint64_t* len, const uint32_t* seg, size_t np, uint32_t nseg,
+                           int bits, int digit_bits, hipStream_t stream);
 hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t* vin,
                               uint32_t* kout, uint32_t* vout, uint32_t* ktmp, uint32_t* vtmp,
                               size_t n, int lo, int hi, int digit_bits, hipStream_t stream);

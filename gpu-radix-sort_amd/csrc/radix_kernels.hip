@@ -3024,16 +3024,62 @@ inline int hybrid_mode_for(hipStream_t st) {
   return get_hybrid_mode();
 }
 
+// Pre-partitioned input of the hybrid (sort_pieces_u32): depth 0's tiles are
+// cut per PIECE instead of over the whole input.  Piece p = keys in[off_p,
+// off_p + len_p) of segment seg_p; the keys of segment s share every bit above
+// the W sorted bits, segments increase with s, and the output holds them in
+// segment order (segment s from cstart[s]).  The table on the device (built by
+// the host, uploaded once): pieces[np] as uint4 (off, len, seg, first tile),
+// then ctile0[nseg + 1] (each segment's first tile; ctile0[nseg] = T0) and
+// cstart[nseg] (each segment's output start).
+struct HybPieces {
+  const uint32_t* dev;  // the table above
+  uint32_t np, nseg;
+  uint32_t tiles;       // T0 = sum over pieces of ceil(len / TILE)
+  int depths;           // digit passes (the bucket sort covers W - BITS * depths bits)
+};
+
+// Depth 0 of a pre-partitioned input: tile t of piece p (first tile w <= t <
+// next piece's first tile) = (off + k * TILE, min(TILE, len - k * TILE), seg),
+// k = t - w (binary search over the pieces); the segments' first tiles and
+// output starts are copied to the depth-0 parent arrays, ctr[0] = T0.
+template <int TILE>
+__global__ __launch_bounds__(256) void k_hyb_pieces(const uint4* __restrict__ pieces, uint32_t np,
+                                                    const uint32_t* __restrict__ segtab, uint32_t nseg, uint32_t T0,
+                                                    uint4* __restrict__ tiles, uint32_t* __restrict__ ctile0,
+                                                    uint32_t* __restrict__ cstart, uint32_t* __restrict__ ctr) {
+  const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+  if (t <= nseg) ctile0[t] = segtab[t];
+  if (t < nseg) cstart[t] = segtab[nseg + 1 + t];
+  if (t == 0) ctr[0] = T0;
+  if (t >= T0) return;
+  uint32_t lo = 0, hi = np;  // largest p with first tile <= t
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pieces[mid].w <= t) lo = mid; else hi = mid;
+  }
+  const uint4 pc = pieces[lo];
+  const uint32_t k = t - pc.w;
+  tiles[t] = make_uint4(pc.x + k * TILE, min((uint32_t)TILE, pc.y - k * TILE), pc.z, 0u);
+}
+
 template <int BITS, typename Op, typename K = uint32_t, typename V = NoValue>
 hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin, V* vout, V* vtmp, size_t n, int W,
-                       uint32_t bias, hipStream_t st, bool* handled, uint64_t span = 0) {
+                       uint32_t bias, hipStream_t st, bool* handled, uint64_t span = 0,
+                       const HybPieces* pc = nullptr) {
   constexpr int RADIX = 1 << BITS;
   constexpr int B = tp_block<K>(BITS);
   constexpr int ITEMS = tp_items<K, V>(BITS);
   constexpr int TILE = B * ITEMS;
-  constexpr int DEPTHS = 16 / BITS;
-  static_assert(DEPTHS % 2 == 0, "the last depth writes out");
-  constexpr uint32_t NB = 1u << 16;  // buckets
+  // digit passes: 16 / BITS over the top 16 of the W bits, or (pieces) the
+  // caller's count; the last one writes out: depth k writes out when
+  // depths - 1 - k is even, tmp otherwise (depth 0 reads in)
+  const int DEPTHS = pc ? pc->depths : 16 / BITS;
+  const uint32_t nseg0 = pc ? pc->nseg : 1u;  // segments entering depth 0
+  const uint64_t NB64 = (uint64_t)nseg0 << (BITS * DEPTHS);  // buckets
+  if (DEPTHS < 1 || NB64 > (1ull << 22) || (pc && (const void*)in == (const void*)out)) return hipErrorInvalidValue;
+  const uint32_t NB = (uint32_t)NB64;
+  const uint32_t lbits = (uint32_t)(W - BITS * DEPTHS);  // bits the bucket sort orders
   *handled = false;
   // bucket-sort blocks (256 x items keys), in two sizes: the first holds the
   // mean bucket of uniform keys + 3.5 sigma (all but a few of the 65536
@@ -3055,9 +3101,12 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   constexpr int BB = sizeof(K) == 8 ? LIBSORT_BUCKET64_BLOCK : 256;
   const uint32_t cap1 = (uint32_t)BB * (((uint32_t)kItems1[cls] * 256u + BB - 1) / BB);
   const uint32_t cap = (uint32_t)BB * (((uint32_t)(kItems1[cls] + 6) * 256u + BB - 1) / BB);
-  const uint32_t T0 = (uint32_t)((n + TILE - 1) / TILE);
-  auto tbound = [&](int k) { return k == 0 ? T0 : T0 + (1u << (BITS * k)); };
-  const uint32_t TB = tbound(DEPTHS - 1);
+  const uint32_t T0 = pc ? pc->tiles : (uint32_t)((n + TILE - 1) / TILE);
+  // segments of depth k (each child has at most one partial tile)
+  auto nseg_at = [&](int k) { return nseg0 << (BITS * k); };
+  auto tbound = [&](int k) { return k == 0 ? T0 : T0 + nseg_at(k); };
+  uint32_t TB = 0;
+  for (int k = 0; k < DEPTHS; ++k) TB = std::max(TB, tbound(k));
   LS_TRY(ws.ensure_tiles((size_t)TB * RADIX, ((size_t)tp_chunks(TB, BITS) + 1) * RADIX));
   // hybrid block: tiles[2] | segbase | cstart[2] | nsize | ctile0[2] | ntl | counters
   const size_t w_tiles = (size_t)TB * 4;
@@ -3072,23 +3121,33 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   uint32_t* ctile0[2] = {h, h + NB + 1}; h += 2 * ((size_t)NB + 1);
   uint32_t* ntl = h; h += NB;
   uint32_t* ctr = h;  // [k] tiles of depth k, [8] buckets over the first block, [9] bucket count, [10] over the
-                      // second, [11] largest bucket, [12] buckets over the first block (planning)
+                      // second, [11] largest bucket, [12] buckets over the first block (planning),
+                      // [13] largest child of depth 0 (pieces), [14] scratch
   h += 16;
   uint32_t* olist = h;  // the buckets over the first block (kListCap)
   hipLaunchKernelGGL(k_hyb_init, dim3(1), dim3(64), 0, st, ctr, NB);  // one launch, not two memsets (4 fills)
   LS_TRY(hipGetLastError());
+  if (pc) {
+    // depth 0's tile table and parent arrays from the piece table
+    const uint32_t g = std::max(T0, pc->nseg + 1);
+    hipLaunchKernelGGL((k_hyb_pieces<TILE>), dim3((g + 255) / 256), dim3(256), 0, st,
+                       reinterpret_cast<const uint4*>(pc->dev), pc->np, pc->dev + 4 * (size_t)pc->np, pc->nseg, T0,
+                       tiles[0], ctile0[0], cstart[0], ctr);
+    LS_TRY(hipGetLastError());
+  }
   const bool dstream = BITS == 8 && sizeof(K) == 8 && dstream_on();
   if (dstream) LS_TRY(ws.ensure_dstream(n));
   ws.part_pending.valid = false;
 
   // keys only: the passes may reorder within a run (k_tile_pass ANY_ORDER)
   constexpr bool kAnyOrder = std::is_same<V, NoValue>::value;
-  auto buf = [&](int k) -> K* { return k == 0 ? const_cast<K*>(in) : (k & 1) ? tmp : out; };
-  auto vbuf = [&](int k) -> V* { return k == 0 ? const_cast<V*>(vin) : (k & 1) ? vtmp : vout; };
+  auto buf = [&](int k) -> K* { return k == 0 ? const_cast<K*>(in) : ((DEPTHS - k) & 1) ? tmp : out; };
+  auto vbuf = [&](int k) -> V* { return k == 0 ? const_cast<V*>(vin) : ((DEPTHS - k) & 1) ? vtmp : vout; };
   for (int k = 0; k < DEPTHS; ++k) {
     const bool last = k == DEPTHS - 1;
+    const bool tab = k > 0 || pc;  // this depth's tiles come from a table
     const uint32_t rows = tbound(k);
-    const uint32_t nseg = 1u << (BITS * k);
+    const uint32_t nseg = nseg_at(k);
     const uint32_t m = nseg * RADIX;  // children
     const Op op = make_digit<Op>((uint32_t)(W - BITS * (k + 1)), (uint32_t)RADIX - 1u, bias);
     const Op op_next = make_digit<Op>((uint32_t)(last ? 0 : W - BITS * (k + 2)), (uint32_t)RADIX - 1u, bias);
@@ -3098,16 +3157,16 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     K* dst = buf(k + 1);
     const V* vsrc = vbuf(k);
     V* vdst = vbuf(k + 1);
-    // counts of this depth: depth 0 reads the keys; 4-bit deeper depths were
-    // counted by the previous pass (fused); 8-bit deeper depths read the keys
-    // tile by tile from the table
-    if (k == 0) {
+    // counts of this depth: depth 0 reads the keys (pieces: tile by tile from
+    // the table); 4-bit deeper depths were counted by the previous pass
+    // (fused); 8-bit deeper depths read the keys tile by tile from the table
+    if (k == 0 && !pc) {
       LS_TRY((tiles_counts<BITS, K, Op, V>(ws, src, n, op, T0, C, BITS == 4 ? Cn : nullptr,
                                            BITS == 4 ? T0 * (uint32_t)RADIX : 0u, st)));
-    } else if (BITS == 8 && dstream) {
+    } else if (BITS == 8 && dstream && k > 0) {
       // the digits depth k - 1 wrote (1 B per key)
       LS_TRY((tiles_counts_u8<K, V, true>(ws, n, rows, C, tiles[k & 1], ctr + k, st)));
-    } else if (BITS == 8) {
+    } else if (BITS == 8 || k == 0) {
       ScopedTimer tm("tilecounts", st, n);
       hipLaunchKernelGGL((k_tile_counts<BITS, B, ITEMS, K, Op, true>), dim3(rows), dim3(B), 0, st, src,
                          (uint32_t)n, op, C, nullptr, 0u, tiles[k & 1], ctr + k);
@@ -3115,20 +3174,26 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     }
     LS_TRY(tiles_colscan<BITS>(ws, C, rows, st));
     const uint32_t* D = tiles_digit_starts(ws, rows, BITS);
-    if (k == 0) {
+    if (k == 0 && !pc) {
       // the top digit's sizes, for the skew check below
       LS_TRY(hipMemcpyAsync(ws.hyb_host, D, RADIX * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       LS_TRY(hipEventRecord(ws.hyb_evt, st));
     }
     {
       ScopedTimer tm("hybplan", st, m);
+      // stats: the last depth's bucket sizes (ctr[11], [12]); pieces, depth 0
+      // of several: its largest child (ctr[13]) for the skew check
+      uint32_t* stats = last ? ctr + 11 : (pc && k == 0) ? ctr + 13 : nullptr;
       hipLaunchKernelGGL((k_hyb_children<RADIX, TILE>), dim3((m + 255) / 256), dim3(256), 0, st, C, ws.tb, D, rows,
-                         (uint32_t)n, nseg, k == 0 ? nullptr : ctile0[k & 1], cstart[k & 1], T0, segbase,
-                         cstart[(k + 1) & 1], nsize, last ? nullptr : ntl, last ? ctr + 11 : nullptr, cap1);
+                         (uint32_t)n, nseg, tab ? ctile0[k & 1] : nullptr, cstart[k & 1], T0, segbase,
+                         cstart[(k + 1) & 1], nsize, last ? nullptr : ntl, stats, cap1);
       LS_TRY(hipGetLastError());
       if (last) {
         // the bucket sizes, read back while the last pass runs
         LS_TRY(hipMemcpyAsync(ws.hyb_host + 20, ctr + 11, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        LS_TRY(hipEventRecord(ws.hyb_evt, st));
+      } else if (pc && k == 0) {
+        LS_TRY(hipMemcpyAsync(ws.hyb_host + 24, ctr + 13, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         LS_TRY(hipEventRecord(ws.hyb_evt, st));
       }
       if (!last) {
@@ -3146,7 +3211,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     {
       ScopedTimer tm("tilepass", st, n);
       if (BITS == 4 && !last) {
-        if (k == 0)
+        if (!tab)
           hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 2, kAnyOrder>),
                              dim3(rows), dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C,
                              ws.tb, segbase, Cn, geo);
@@ -3154,7 +3219,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
           hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 3, kAnyOrder>),
                              dim3(rows), dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C,
                              ws.tb, segbase, Cn, geo);
-      } else if (k == 0) {
+      } else if (!tab) {
         hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, false, Op, Op, 0, kAnyOrder>), dim3(rows),
                            dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase,
                            Cn, geo);
@@ -3165,7 +3230,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       }
       LS_TRY(hipGetLastError());
     }
-    if (k == 0) {
+    if (k == 0 && !pc) {
       // skew check (the pass above keeps the GPU busy meanwhile; it wrote
       // only tmp, so abandoning here leaves in intact)
       LS_TRY(hipEventSynchronize(ws.hyb_evt));
@@ -3180,6 +3245,11 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       if ((double)mx > 1.25 * share + 4.0 * std::sqrt(share) + 32.0 ||
           (double)mx / (double)(NB / RADIX) > 0.9 * cap)
         return hipSuccess;
+    } else if (k == 0 && !last) {
+      // pieces: a depth-0 child whose buckets would average > 0.9 of a block
+      // (a skewed input): the caller's LSD sort instead (in is untouched)
+      LS_TRY(hipEventSynchronize(ws.hyb_evt));
+      if ((double)ws.hyb_host[24] / (double)(1ull << (BITS * (DEPTHS - 1))) > 0.9 * cap) return hipSuccess;
     }
   }
   // the bucket sizes (read back while the last pass runs): a bucket larger
@@ -3187,14 +3257,16 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   // holds -> the LSD sort of out (any order sorts) instead of the bucket sort
   LS_TRY(hipEventSynchronize(ws.hyb_evt));
   *handled = true;
-  if (ws.hyb_host[21] > kListCap || ws.hyb_host[20] > cap)
+  if (ws.hyb_host[21] > kListCap || ws.hyb_host[20] > cap) {
+    // pieces: every bit (the segments' own bits vary across out)
+    if (pc) return sort_impl<K, V>(ws, out, out, tmp, vout, vout, vtmp, n, 0, 8 * (int)sizeof(K), BITS, st);
     return sort_impl<K, V>(ws, out, out, tmp, vout, vout, vtmp, n, 0, W, BITS, st, bias);
-  // bucket sort of the 2^16 buckets in place in out (cstart/nsize of the
-  // last depth's children)
+  }
+  // bucket sort of the NB buckets in place in out (cstart/nsize of the last
+  // depth's children)
   {
     ScopedTimer tm("bucketsort", st, n);
     const uint32_t* bstart = cstart[DEPTHS & 1];
-    const uint32_t lbits = (uint32_t)(W - 16);
     // 64-bit keys: 512-thread blocks (BB; the same slots in half the keys per
     // thread: 152 -> ~90 VGPRs for (u64, u32) pairs at 17 slots per 256)
     // 64-bit keys: on-chip steps over the top 16 of the 48 bucket bits, then
@@ -3279,6 +3351,104 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
     }
   }
   return hipSuccess;
+}
+
+// Keys per piece-sort below which auto mode gathers and runs the LSD sort
+// (the hybrid's ~10 launches per depth outweigh its saved passes).
+constexpr size_t kPiecesMinKeys = 1ull << 20;
+
+hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n,
+                           const uint64_t* off, const uint64_t* len, const uint32_t* seg, size_t np, uint32_t nseg,
+                           int bits, int digit_bits, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (n > 0xffffffffull || in == out || tmp == out || tmp == in || nseg == 0 || nseg > (1u << 20) || bits < 1 ||
+      bits > 32 || (digit_bits != 4 && digit_bits != 8))
+    return hipErrorInvalidValue;
+  // the non-empty pieces, checked: segments non-decreasing and < nseg, offsets
+  // below 2^32, lengths summing to n
+  std::vector<size_t> keep;
+  keep.reserve(np);
+  uint64_t total = 0, maxlen = 0;
+  uint32_t prev = 0;
+  for (size_t p = 0; p < np; ++p) {
+    if (seg[p] < prev || seg[p] >= nseg) return hipErrorInvalidValue;
+    prev = seg[p];
+    if (!len[p]) continue;
+    if (off[p] + len[p] > 0xffffffffull) return hipErrorInvalidValue;
+    total += len[p];
+    maxlen = std::max(maxlen, len[p]);
+    keep.push_back(p);
+  }
+  if (total != n || keep.size() > 65535) return hipErrorInvalidValue;
+  const uint32_t K = (uint32_t)keep.size();
+  // digit passes: the fewest that bring the mean bucket (n / (nseg * RADIX^d)
+  // keys, values uniform in each segment) to <= 4096 keys, within `bits`
+  const int hyb = hybrid_mode_for(st);
+  int depths = 0;
+  if (hyb == 2 ? n >= 1024 : (hyb == 1 && n >= kPiecesMinKeys)) {
+    for (int d = 1; d * digit_bits <= bits; ++d) {
+      depths = d;
+      if ((double)n / std::ldexp((double)nseg, d * digit_bits) <= 4096.0) break;
+    }
+    if (((uint64_t)nseg << (digit_bits * depths)) > (1ull << 22)) depths = 0;
+  }
+  // host table (pinned staging, one upload): pieces uint4 (off, len, seg,
+  // first tile) | ctile0[nseg + 1] | cstart[nseg] | (8-byte aligned) the
+  // gather table of the fallback: src_off[K] | dst_off[K] | len[K] (uint64)
+  const uint32_t TILE = (uint32_t)(tp_block<uint32_t>(digit_bits) * tp_items<uint32_t>(digit_bits));
+  const size_t w32 = 4 * (size_t)K + 2 * (size_t)nseg + 1;
+  const size_t g64 = (w32 + 1) / 2;  // first uint64 word of the gather table
+  LS_TRY(ws.ensure_seg(g64 + 3 * (size_t)K));
+  LS_TRY(hipEventSynchronize(ws.seg_evt));  // the staging may still feed the previous upload
+  uint32_t* h32 = reinterpret_cast<uint32_t*>(ws.seg_host);
+  uint64_t* hg = ws.seg_host + g64;
+  uint32_t* ct0 = h32 + 4 * (size_t)K;
+  uint32_t* cst = ct0 + nseg + 1;
+  std::vector<uint64_t> segsize(nseg, 0);
+  for (uint32_t i = 0; i < K; ++i) segsize[seg[keep[i]]] += len[keep[i]];
+  {
+    uint64_t run = 0;
+    for (uint32_t s = 0; s < nseg; ++s) {
+      cst[s] = (uint32_t)run;
+      run += segsize[s];
+    }
+  }
+  uint32_t tile = 0, i = 0;
+  std::vector<uint64_t> dpos(cst, cst + nseg);
+  for (uint32_t s = 0; s <= nseg; ++s) {
+    ct0[s] = tile;  // segment s's pieces start at this tile
+    for (; i < K && (s == nseg || seg[keep[i]] == s); ++i) {
+      const size_t p = keep[i];
+      h32[4 * (size_t)i + 0] = (uint32_t)off[p];
+      h32[4 * (size_t)i + 1] = (uint32_t)len[p];
+      h32[4 * (size_t)i + 2] = seg[p];
+      h32[4 * (size_t)i + 3] = tile;
+      tile += (uint32_t)((len[p] + TILE - 1) / TILE);
+      hg[i] = off[p];
+      hg[K + i] = dpos[seg[p]];
+      hg[2 * (size_t)K + i] = len[p];
+      dpos[seg[p]] += len[p];
+    }
+  }
+  LS_TRY(hipMemcpyAsync(ws.seg_dev, ws.seg_host, (g64 + 3 * (size_t)K) * sizeof(uint64_t), hipMemcpyHostToDevice,
+                        st));
+  LS_TRY(hipEventRecord(ws.seg_evt, st));
+  if (depths > 0) {
+    HybPieces pc{reinterpret_cast<const uint32_t*>(ws.seg_dev), K, nseg, tile, depths};
+    bool handled = false;
+    NoValue* nv = nullptr;
+    if (digit_bits == 4)
+      LS_TRY((sort_hybrid<4, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, 0u, st, &handled, 0, &pc)));
+    else
+      LS_TRY((sort_hybrid<8, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, 0u, st, &handled, 0, &pc)));
+    if (handled) {
+      ws.last_algo = 4;
+      return hipSuccess;
+    }
+  }
+  // small or skewed: gather the pieces into segment order, LSD sort in place
+  LS_TRY(segment_copy_dev_u32(in, out, ws.seg_dev + g64, K, maxlen, n, st));
+  return sort_impl<uint32_t, NoValue>(ws, out, out, tmp, nullptr, nullptr, nullptr, n, 0, 32, digit_bits, st);
 }
 
 hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t* vin, uint32_t* kout,

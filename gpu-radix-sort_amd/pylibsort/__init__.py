@@ -46,6 +46,9 @@ _SIGS = [
      [_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
     ("libsortSortKeysRangeU32", ctypes.c_int,
      [_vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, _vp]),
+    ("libsortSortPiecesU32", ctypes.c_int,
+     [_vp, _vp, _vp, ctypes.c_size_t, _u64p, _u64p, _u32p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+      _vp]),
     ("libsortSortPairsU64U32", ctypes.c_int,
      [_vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     ("libsortSortKeysU64", ctypes.c_int,

@@ -78,6 +78,34 @@ def sort_keys_range_u32(keys, lo, hi, out=None, tmp=None):
     return out
 
 
+def sort_pieces_u32(keys, off, lens, segs, nseg, bits, out=None, tmp=None):
+    """Sort of pre-partitioned uint32 keys (libsortSortPiecesU32): piece p =
+    keys[off[p] : off[p] + lens[p]] of segment segs[p] (host arrays, pieces in
+    non-decreasing segment order); every key of segment s shares its bits
+    [bits, 32), increasing with s.  Returns `out` holding the sum(lens) keys
+    sorted (out and tmp distinct from keys)."""
+    _need(keys, _U32, "keys")
+    o = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(lens, dtype=np.uint64)
+    sg = np.ascontiguousarray(segs, dtype=np.uint32)
+    if not (o.size == ln.size == sg.size):
+        raise ValueError("piece tables differ in length")
+    if o.size and int((o + ln).max()) > keys.numel():
+        raise ValueError("piece out of range")
+    n = int(ln.sum())
+    out = torch.empty(n, dtype=keys.dtype, device=keys.device) if out is None else out
+    tmp = torch.empty(n, dtype=keys.dtype, device=keys.device) if tmp is None else tmp
+    _need(out, _U32, "out")
+    _need(tmp, _U32, "tmp")
+    if out.numel() < n or tmp.numel() < n:
+        raise ValueError("out / tmp smaller than the pieces")
+    p64 = ctypes.POINTER(ctypes.c_uint64)
+    _check(_lib().libsortSortPiecesU32(_ptr(keys), _ptr(out), _ptr(tmp), n, o.ctypes.data_as(p64),
+                                       ln.ctypes.data_as(p64), sg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                       o.size, int(nseg), int(bits), _stream()), "libsortSortPiecesU32")
+    return out
+
+
 def sort_pairs_u64_u32(keys, vals, out_keys=None, out_vals=None, tmp_keys=None, tmp_vals=None,
                        offset=0, width=None):
     """Stable sort of (uint64 key, uint32 payload) pairs by key bits."""

@@ -98,6 +98,22 @@ LIBSORT_API bool libsortSortKeysU32(const uint32_t* d_in, uint32_t* d_out, uint3
 LIBSORT_API bool libsortSortKeysRangeU32(const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp,
                                          size_t n, uint32_t lo, uint64_t hi, void* stream);
 
+/* Sort of pre-partitioned keys: the receive buffer of a multi-GPU round,
+ * whose pieces arrive already partitioned by the senders' top-digit pass
+ * (the gather fused into the next pass's tile loader
+ * as a segment table).  Piece p = d_in[off[p], off[p] + len[p]) belongs to
+ * segment seg[p]; off/len/seg are host arrays of npieces entries listed in
+ * non-decreasing segment order, seg[p] < nseg.  Every key of segment s has
+ * the same bits [bits, 32), and those increase with s.  d_out receives the
+ * n = sum(len) keys in ascending order; d_tmp is scratch of n keys; d_in,
+ * d_out and d_tmp are distinct.  The digit passes start from the pieces'
+ * own tiles (no gather copy and no pass over the bits the segments already
+ * fix); small or skewed inputs are gathered and LSD-sorted instead.  Waits on
+ * the host like the hybrid sorts (libsortSetHybrid). */
+LIBSORT_API bool libsortSortPiecesU32(const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp, size_t n,
+                                      const uint64_t* off, const uint64_t* len, const uint32_t* seg,
+                                      size_t npieces, uint32_t nseg, uint32_t bits, void* stream);
+
 /* Stable key-value sort: 64-bit keys, 32-bit payloads (BASELINE config C5). */
 LIBSORT_API bool libsortSortPairsU64U32(const uint64_t* d_kin, const uint32_t* d_vin,
                                         uint64_t* d_kout, uint32_t* d_vout,
