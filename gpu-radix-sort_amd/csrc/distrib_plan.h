@@ -55,7 +55,8 @@ inline void add_interval_counts(uint64_t a, uint64_t len, uint64_t S, int R, uin
 // normalised prefix of growth^i); rank * K + round is made monotone over the
 // buckets (cumulative max).  The same arithmetic as the device planner
 // (k_plan_rounds) and pylibsort.distrib._plan_rounds_t.
-inline void plan_rounds(const int64_t* H, int R, size_t ld, int K, double growth, uint8_t* lut, int64_t* est) {
+inline void plan_rounds(const int64_t* H, int R, size_t ld, int K, double growth, uint8_t* lut, int64_t* est,
+                        int bins = kHistBins) {
   std::vector<double> cw(K);
   double acc = 0.0, p = 1.0;
   for (int i = 0; i < K; ++i) {
@@ -64,9 +65,9 @@ inline void plan_rounds(const int64_t* H, int R, size_t ld, int K, double growth
     p *= growth;
   }
   for (int i = 0; i < K; ++i) cw[i] /= acc;
-  std::vector<uint64_t> G(kHistBins, 0);
+  std::vector<uint64_t> G(bins, 0);
   uint64_t total = 0;
-  for (int b = 0; b < kHistBins; ++b) {
+  for (int b = 0; b < bins; ++b) {
     for (int r = 0; r < R; ++r) G[b] += (uint64_t)H[(size_t)r * ld + b];
     total += G[b];
   }
@@ -74,7 +75,7 @@ inline void plan_rounds(const int64_t* H, int R, size_t ld, int K, double growth
   for (int r = 0; r < R; ++r) est[r] = 0;
   uint64_t cum = 0;
   uint32_t run = 0;
-  for (int b = 0; b < kHistBins; ++b) {
+  for (int b = 0; b < bins; ++b) {
     cum += G[b];
     const double x = ((double)cum - (double)G[b] / 2.0) / Td * (double)R;
     int64_t rank = (int64_t)std::floor(x);
@@ -198,6 +199,104 @@ inline std::vector<Piece> recut_pieces(const std::vector<uint64_t>& n_have) {
     g += n_have[s];
   }
   return out;
+}
+
+// ---------------------------------------------------------------------------
+// top-digit rounds ("msd"): the exchange is planned on the EXACT counts of the
+// top 8 key bits, which every rank has from its partition pass (a stable
+// partition by the top digit, the reference's gpuPartial(offset 24, width 8)
+// building block), so the receiver's pieces arrive partitioned by the digit
+// and its round sort starts below it (sort_pieces_u32).
+// ---------------------------------------------------------------------------
+constexpr int kTopBits = 8;
+constexpr int kTopDigits = 1 << kTopBits;  // 256
+constexpr int kTopShift = 32 - kTopBits;   // digit = key >> 24
+
+// C: R rows of 256 exact digit counts.  lut[g] = round * R + rank of digit g
+// (plan_rounds over 256 bins: contiguous digit ranges, ~1/R of the keys per
+// rank, rounds growing by `growth`); est[r] = keys rank r receives (exact).
+inline void plan_digit_rounds(const std::vector<std::vector<uint64_t>>& C, int K, double growth, uint8_t* lut,
+                              int64_t* est) {
+  const int R = (int)C.size();
+  std::vector<int64_t> H((size_t)R * kTopDigits);
+  for (int r = 0; r < R; ++r)
+    for (int g = 0; g < kTopDigits; ++g) H[(size_t)r * kTopDigits + g] = (int64_t)C[r][g];
+  plan_rounds(H.data(), R, kTopDigits, K, growth, lut, est, kTopDigits);
+}
+
+// Digit range [a, b) of group `code` (a == b: empty).  The table is monotone
+// in rank * K + round over the digits, so each group's digits are contiguous.
+inline void digit_range(const uint8_t* lut, int code, int* a, int* b) {
+  int first = -1, last = -1;
+  for (int g = 0; g < kTopDigits; ++g)
+    if (lut[g] == code) {
+      if (first < 0) first = g;
+      last = g;
+    }
+  *a = first < 0 ? 0 : first;
+  *b = first < 0 ? 0 : last + 1;
+}
+
+// The exchange and the receivers' piece tables.  Rank s's partition holds its
+// keys in digit order (part_start[s][g] = start of digit g).  Round i sends
+// rank s's digits [a, b) of group (d, i) to rank d, into d's receive buffer
+// at roff[d][i] + (keys of the earlier sources): pieces in source order.  The
+// round sort of rank d, round i sees piece (s, g) at offset src_base + (keys
+// of s's digits a..g-1) -- listed digit-major, source-minor, segment g - a.
+struct DigitPlan {
+  int R = 0, K = 0;
+  std::vector<int> lo, hi;                     // [R*K] digit range of group code i*R + d
+  std::vector<uint64_t> roff;                  // [R][K+1]
+  std::vector<uint64_t> n_recv;                // [R]
+  std::vector<std::vector<Piece>> rounds;      // [K] exchange pieces
+  // [R][K] the round sort's pieces (offsets within the round's receive region)
+  std::vector<std::vector<uint64_t>> p_off, p_len;
+  std::vector<std::vector<uint32_t>> p_seg;
+};
+
+inline DigitPlan digit_plan(const std::vector<std::vector<uint64_t>>& C, const uint8_t* lut, int K) {
+  DigitPlan p;
+  const int R = (int)C.size();
+  p.R = R;
+  p.K = K;
+  p.lo.assign((size_t)R * K, 0);
+  p.hi.assign((size_t)R * K, 0);
+  for (int c = 0; c < R * K; ++c) digit_range(lut, c, &p.lo[c], &p.hi[c]);
+  std::vector<std::vector<uint64_t>> start(R, std::vector<uint64_t>(kTopDigits + 1, 0));
+  for (int s = 0; s < R; ++s)
+    for (int g = 0; g < kTopDigits; ++g) start[s][g + 1] = start[s][g] + C[s][g];
+  p.roff.assign((size_t)R * (K + 1), 0);
+  p.n_recv.assign(R, 0);
+  p.rounds.assign(K, {});
+  p.p_off.assign((size_t)R * K, {});
+  p.p_len.assign((size_t)R * K, {});
+  p.p_seg.assign((size_t)R * K, {});
+  for (int d = 0; d < R; ++d) {
+    uint64_t run = 0;
+    for (int i = 0; i < K; ++i) {
+      p.roff[(size_t)d * (K + 1) + i] = run;
+      const int a = p.lo[(size_t)i * R + d], b = p.hi[(size_t)i * R + d];
+      std::vector<uint64_t> base(R, 0);
+      uint64_t at = 0;
+      for (int s = 0; s < R; ++s) {
+        base[s] = at;
+        const uint64_t m = start[s][b] - start[s][a];
+        if (m) p.rounds[i].push_back(Piece{s, d, start[s][a], run + at, m});
+        at += m;
+      }
+      const size_t q = (size_t)d * K + i;
+      for (int g = a; g < b; ++g)
+        for (int s = 0; s < R; ++s) {
+          p.p_off[q].push_back(base[s] + (start[s][g] - start[s][a]));
+          p.p_len[q].push_back(C[s][g]);
+          p.p_seg[q].push_back((uint32_t)(g - a));
+        }
+      run += at;
+    }
+    p.roff[(size_t)d * (K + 1) + K] = run;
+    p.n_recv[d] = run;
+  }
+  return p;
 }
 
 // ---------------------------------------------------------------------------

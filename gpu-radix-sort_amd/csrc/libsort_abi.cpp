@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "boundaries.h"
+#include "distrib_plan.h"
 #include "radix.h"
 
 #define LIBSORT_EXPORT extern "C" __attribute__((visibility("default")))
@@ -1090,6 +1091,26 @@ LIBSORT_EXPORT void libsortTimingFilter(const char* kernels) { timing_filter(ker
 LS_BOOL_ENTRY(libsortTimingQuery, const char* kernel, uint64_t* launches, double* total_ms,
                                       uint64_t* total_keys) {
   return timing_query(kernel, launches, total_ms, total_keys) ? 1 : 0;
+}
+
+LS_BOOL_ENTRY(libsortDistribPlanDigits, const int64_t* counts, uint32_t nranks, uint32_t rounds, double growth,
+              uint8_t* lut, int64_t* est) {
+  if (!counts || !lut || !est || nranks < 1 || rounds < 1 || (uint64_t)nranks * rounds > 256 || !(growth > 0.0)) {
+    set_error("libsortDistribPlanDigits: need the tables, 1 <= nranks * rounds <= 256 and growth > 0");
+    return 0;
+  }
+  std::vector<std::vector<uint64_t>> C(nranks, std::vector<uint64_t>(dplan::kTopDigits));
+  for (uint32_t r = 0; r < nranks; ++r)
+    for (int g = 0; g < dplan::kTopDigits; ++g) {
+      const int64_t v = counts[(size_t)r * dplan::kTopDigits + g];
+      if (v < 0) {
+        set_error("libsortDistribPlanDigits: negative count");
+        return 0;
+      }
+      C[r][g] = (uint64_t)v;
+    }
+  dplan::plan_digit_rounds(C, (int)rounds, growth, lut, est);
+  return 1;
 }
 
 LS_BOOL_ENTRY(gpuDistribSort, uint32_t* h_in, size_t len, int ngpu) {

@@ -38,6 +38,9 @@ import torch
 import torch.distributed as dist
 
 HIST_BITS = 12
+# the top-digit rounds partition by key >> TOP_SHIFT (8 bits, 256 digits)
+TOP_BITS = 8
+TOP_SHIFT = 32 - TOP_BITS
 # msd exchange rounds and their size growth.  A round's exchange overlaps the
 # previous round's sort; the first round's exchange and the last round's sort
 # are exposed, and every round costs ~0.1 ms of kernel boundaries (measured).
@@ -106,6 +109,36 @@ class HipOps:
         ov = self.empty(n) if out_vals is None else out_vals
         return self.D.sort_pairs_u64_u32(keys, vals, out_keys=ok_, out_vals=ov, tmp_keys=self._scratch64(n),
                                          tmp_vals=self._scratch(n))
+
+    def _top_lut(self):
+        """The identity table of the 256 top digits: the table partition with
+        it is the stable partition by key >> 24 (gpuPartial offset 24, width 8)."""
+        if getattr(self, "_lut8", None) is None:
+            self._lut8 = torch.arange(256, dtype=torch.uint8, device=self.device)
+        return self._lut8
+
+    def top_count_t(self, keys):
+        """Count half of the top-digit partition: the 256 bucket starts
+        (uint32 in an int32 device tensor) while nothing has moved yet."""
+        return self.D.partition_lut_count_u32(keys, self._top_lut(), TOP_SHIFT, 256)
+
+    def top_scatter_t(self, keys):
+        return self.D.partition_lut_scatter_u32(keys, self._top_lut(), TOP_SHIFT, 256, out=self.empty(keys.numel()))
+
+    def top_pairs_count_t(self, keys, vals):
+        """The same for (u64 key, u32 payload) pairs: digit = key >> 56."""
+        return self.D.partition_lut_pairs_count_u64_u32(keys, vals, self._top_lut(), TOP_SHIFT, 256)
+
+    def top_pairs_scatter_t(self, keys, vals):
+        n = keys.numel()
+        return self.D.partition_lut_pairs_scatter_u64_u32(keys, vals, self._top_lut(), TOP_SHIFT, 256,
+                                                          out_keys=self.empty64(n), out_vals=self.empty(n))
+
+    def sort_pieces(self, keys, off, lens, segs, nseg, out):
+        """Round sort straight from the received pieces (libsortSortPiecesU32):
+        segment = top digit - the round's first digit, 24 bits left to sort."""
+        n = int(np.sum(lens)) if len(lens) else 0
+        return self.D.sort_pieces_u32(keys, off, lens, segs, nseg, TOP_SHIFT, out=out, tmp=self._scratch(n))
 
     def partition(self, keys, splitters, out=None):
         out = self.empty(keys.numel()) if out is None else out
@@ -535,86 +568,132 @@ def _mark(trace, label):
         trace.append((label, time.perf_counter()))
 
 
-def _msd_partition(keys, ops, group, R, K, sample_stride, trace=None, growth=None):
-    """The prefix of the range-round schedules: sampled histogram, all-gather,
-    round plan, table partition into R*K (round, destination) buckets, and the
-    exact bucket sizes of every rank on the host.  Returns (part, C[R, R*K],
-    n_all[R], est[R], lut[4096])."""
+def plan_digits(C, R, K, growth=None):
+    """(lut uint8[256], est int64[R]) of the top-digit rounds from the
+    gathered exact digit counts C[R, 256]: libsort's host plan
+    (libsortDistribPlanDigits = csrc/distrib_plan.h plan_digit_rounds, the
+    arithmetic the single-process engine runs too).  lut[g] = round * R +
+    rank of digit g: contiguous digit ranges in key order, ~1/R of the keys
+    per rank, K rounds growing by `growth`; est[r] = keys rank r receives."""
+    from . import lib
+    Cc = np.ascontiguousarray(C, dtype=np.int64)
+    lut = np.zeros(256, dtype=np.uint8)
+    est = np.zeros(R, dtype=np.int64)
+    if lib().libsortDistribPlanDigits(Cc.ctypes.data, R, K, float(GROWTH if growth is None else growth),
+                                      lut.ctypes.data, est.ctypes.data) != 1:
+        raise RuntimeError("libsortDistribPlanDigits failed")
+    return lut, est
+
+
+class _DigitRounds:
+    """Exchange geometry of the top-digit rounds for rank r: group code j =
+    round * R + dest covers digits [lo[j], hi[j]); rank s's partition holds
+    digit g at [start[s][g], start[s][g+1]); CB[s][j] = keys of rank s in
+    group j (what s sends for it)."""
+
+    def __init__(self, C, lut, R, K):
+        self.R, self.K = R, K
+        self.lo = np.zeros(R * K, dtype=np.int64)
+        self.hi = np.zeros(R * K, dtype=np.int64)
+        for j in range(R * K):
+            idx = np.nonzero(lut == j)[0]
+            if idx.size:
+                self.lo[j], self.hi[j] = idx[0], idx[-1] + 1
+        self.C = np.asarray(C, dtype=np.int64)
+        self.start = np.zeros((R, 257), dtype=np.int64)
+        self.start[:, 1:] = np.cumsum(self.C, axis=1)
+        self.CB = self.start[:, self.hi] - self.start[:, self.lo]
+
+    def send_slice(self, s, j):
+        """[a, b) of rank s's partition that group j takes."""
+        a = int(self.start[s][self.lo[j]])
+        return a, a + int(self.CB[s][j])
+
+    def pieces(self, j):
+        """The receiver's round-sort pieces of group j, whose sources arrive
+        one after another: (off, len, seg) digit-major, source-minor; nseg."""
+        a, b = int(self.lo[j]), int(self.hi[j])
+        base = np.concatenate([[0], np.cumsum(self.CB[:, j])[:-1]])
+        off = (base[None, :] + (self.start[:, a:b] - self.start[:, a:a + 1]).T).reshape(-1)
+        ln = self.C[:, a:b].T.reshape(-1)
+        seg = np.repeat(np.arange(b - a, dtype=np.int64), self.R)
+        return off, ln, seg, b - a
+
+
+def _digit_partition(keys, ops, group, vals=None):
+    """The prefix of the top-digit round schedules: per-tile counts of the
+    top 8 key bits + column scan (the bucket starts), the stable top-digit
+    scatter queued right behind them, and beside it (side stream) the bucket
+    sizes, their all-gather and ONE small device-to-host copy -- the host
+    plans and issues the exchange while the scatter moves the data.
+    Returns (part, C[R, 256] host int64) or, with vals (pairs: digit =
+    key >> 56), ((part_keys, part_vals), C)."""
     n = keys.numel()
-    NB = R * K
-    HN = _allgather_t(_plan_row(ops, keys, sample_stride), group)     # [R, 4097]: histogram | n
-    lut_t, est_t = _plan(ops, HN, R, K, growth)
-    _mark(trace, "histogram+allgather+plan")
-    split = hasattr(ops, "partition_lut_count_t")
-    if split:
-        # counts + scan, then the scatter right away; the sizes, their gather
-        # and the small D2H run on a side stream beside it, so the host plans
-        # and issues the exchange while the data moves (the one host
-        # synchronisation waits for the sizes only)
-        b_t = ops.partition_lut_count_t(keys, lut_t, 32 - HIST_BITS, NB)
-        side = _SideWork(b_t, HN, est_t, lut_t)
-        part = ops.partition_lut_scatter_t(keys, lut_t, 32 - HIST_BITS, NB)
+    if vals is None:
+        b_t = ops.top_count_t(keys)
+        side = _SideWork(b_t)
+        part = ops.top_scatter_t(keys)
     else:
-        part, b_t = ops.partition_lut_t(keys, lut_t, 32 - HIST_BITS, NB)
-        side = _SideWork(b_t, HN, est_t, lut_t)
-    with side:                                                 # beside the scatter, not before it
+        b_t = ops.top_pairs_count_t(keys, vals)
+        side = _SideWork(b_t)
+        part = ops.top_pairs_scatter_t(keys, vals)
+    with side:
         sizes_t = _sizes_from_starts(b_t, n)
-        C_t = _allgather_t(sizes_t, group)                     # [R, NB], bucket j = round * R + dest
-        pending = _to_host_async(torch.cat([C_t.flatten(), HN[:, -1], est_t.to(torch.int64),
-                                            lut_t.to(torch.int64)]))
-    host = pending.wait()
-    _mark(trace, "partition+allgather sizes")
-    C = host[:R * NB].reshape(R, NB)
-    n_all = host[R * NB:R * NB + R]
-    est = host[R * NB + R:R * NB + 2 * R]
-    lut = host[R * NB + 2 * R:].astype(np.uint8)
-    return part, C, n_all, est, lut
+        pending = _to_host_async(_allgather_t(sizes_t, group))
+    return part, pending.wait()
 
 
-def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None, sample_stride=16, self_local=True,
-             trace=None):
-    """Range-split rounds schedule; see module docstring.  `trace` (a list)
+def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None, self_local=True, trace=None,
+             growth=None):
+    """Top-digit rounds schedule; see module docstring.  `trace` (a list)
     records synchronised timestamps of the steps (diagnostics only)."""
     R = dist.get_world_size(group)
     r = dist.get_rank(group)
     _mark(trace, "start")
     K = max(1, min(int(ROUNDS if rounds is None else rounds), 256 // R))
-    n = keys.numel()
-    NB = R * K
-    # histogram -> allgather -> plan -> partition -> allgather of the exact
-    # sizes, all on the device; ONE host transfer afterwards
-    part, C, n_all, est, lut = _msd_partition(keys, ops, group, R, K, sample_stride, trace)
-    N = int(n_all.sum())
+    # partition by the top digit, exact digit counts of every rank (one host
+    # synchronisation), the host plan
+    part, C = _digit_partition(keys, ops, group)
+    N = int(C.sum())
     S, _ = shard_cut(N, R)
-    hs = float(est.sum())
-    if N and hs and est.max() * N / hs > max_imbalance * S + 4096:
+    lut, est = plan_digits(C, R, K, growth)
+    _mark(trace, "partition+allgather sizes+plan")
+    if N and est.max() > max_imbalance * S + 4096:
         return sort_lsd(keys, ops, group)                      # identical decision on every rank
-    sizes = C[r]
-    b = np.concatenate([[0], np.cumsum(sizes)[:-1]])
-    recv_tot = np.array([int(C[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
+    g = _DigitRounds(C, lut, R, K)
+    recv_tot = np.array([int(g.CB[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
     roff = np.concatenate([[0], np.cumsum(recv_tot)])
     recv = ops.empty(int(roff[-1]))
     out = ops.empty(int(roff[-1]))
+    # every round's exchange issued now (RCCL's stream runs them back to
+    # back); the rank's own piece is a local copy
     works = []
     for i in range(K):
-        if not C[:, i * R:(i + 1) * R].any():                  # identical on every rank
-            works.append(None)
-            continue
-        s0 = int(b[i * R])
-        ss = sizes[i * R:(i + 1) * R]
-        works.append(_alltoallv_into(recv[int(roff[i]):int(roff[i + 1])], part[s0:s0 + int(ss.sum())], ss,
-                                     C[:, i * R + r], group, async_op=True, self_local=self_local))
+        sends, recvs = {}, {}
+        for d in range(R):
+            a, b = g.send_slice(r, i * R + d)
+            if b > a:
+                sends[d] = part[a:b]
+        at = int(roff[i])
+        for src in range(R):
+            m = int(g.CB[src][i * R + r])
+            if m:
+                recvs[src] = recv[at:at + m]
+            at += m
+        if self_local and r in sends:
+            recvs.pop(r).copy_(sends.pop(r))
+        works.append(_exchange_pieces(sends, recvs, group))
     for i in range(K):
         if works[i] is not None:
             works[i].wait()                                    # stream-level: the sort waits on RCCL
         if recv_tot[i]:
-            lo, hi = _group_range(lut, i * R + r)              # every key of the round lies in it
-            ops.sort_range(recv[int(roff[i]):int(roff[i + 1])], lo, hi, out=out[int(roff[i]):int(roff[i + 1])])
+            off, ln, seg, nseg = g.pieces(i * R + r)
+            a, z = int(roff[i]), int(roff[i + 1])
+            ops.sort_pieces(recv[a:z], off, ln, seg, nseg, out=out[a:z])
         _mark(trace, "round %d" % i)
     if not balance:
         return out
-    n_recv = np.array([int(C[:, d::R].sum()) for d in range(R)], dtype=np.int64)
-    res = _rebalance(out, n_recv, ops, group)
+    res = _rebalance(out, est, ops, group)
     _mark(trace, "rebalance")
     return res
 
@@ -671,8 +750,7 @@ def _merge_runs(runs, ops, out):
     return ops.merge(runs[0], runs[1], out)
 
 
-def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None, sample_stride=16, trace=None,
-              self_local=True):
+def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None, trace=None, self_local=True):
     """Range rounds with delta-coded exchange, for link-bound world sizes (the
     bench default at 2 GPUs, where one xGMI link carries half of every shard).
     The same plan and table partition as sort_msd; then per round the SENDER
@@ -694,14 +772,17 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
     _mark(trace, "start")
     K = max(1, min(int(ROUNDS if rounds is None else rounds), 256 // R))
     n = keys.numel()
-    part, C, n_all, est, lut = _msd_partition(keys, ops, group, R, K, sample_stride, trace, GROWTH_Z)
-    N = int(n_all.sum())
+    part, Cd = _digit_partition(keys, ops, group)
+    N = int(Cd.sum())
     S, _ = shard_cut(N, R)
-    hs = float(est.sum())
-    if N and hs and est.max() * N / hs > max_imbalance * S + 4096:
+    lut, est = plan_digits(Cd, R, K, GROWTH_Z)
+    _mark(trace, "partition+allgather sizes+plan")
+    if N and est.max() > max_imbalance * S + 4096:
         return sort_lsd(keys, ops, group)                      # identical decision on every rank
+    g = _DigitRounds(Cd, lut, R, K)
+    C = g.CB                                                   # [R, R*K]: keys of rank s for group round*R + dest
     sizes = C[r]
-    b = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    b = g.start[r][g.lo]                                       # where group j's keys start in this rank's partition
     recv_tot = np.array([int(C[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
     roff = np.concatenate([[0], np.cumsum(recv_tot)])
     out = ops.empty(int(roff[-1]))
@@ -715,11 +796,16 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
     coded = ops.empty(int(coff[-1]))
     evs = []
     for i in range(K):
-        s0, s1 = int(b[i * R]), int(b[i * R]) + int(sizes[i * R:(i + 1) * R].sum())
-        if s1 > s0:
-            bk = np.nonzero((lut >= i * R) & (lut < (i + 1) * R))[0]
-            lo, hi = int(bk[0]) << (32 - HIST_BITS), (int(bk[-1]) + 1) << (32 - HIST_BITS)
-            ops.sort_range(part[s0:s1], lo, hi, out=srt[s0:s1])
+        for d in range(R):
+            # each outgoing piece (one contiguous digit range of the
+            # partition) sorted from its digit pieces
+            j = i * R + d
+            if sizes[j]:
+                a0, z0 = int(g.lo[j]), int(g.hi[j])
+                s0 = int(b[j])
+                off = g.start[r][a0:z0] - s0
+                ops.sort_pieces(part[s0:s0 + int(sizes[j])], off, g.C[r][a0:z0], np.arange(z0 - a0), z0 - a0,
+                                out=srt[s0:s0 + int(sizes[j])])
         for d in range(R):
             j = i * R + d
             if remote(d) and sizes[j]:
@@ -800,64 +886,53 @@ def _rebalance_pairs(keys, vals, n_all, ops, group):
     return rk, rv
 
 
-def distrib_sort_pairs(keys, vals, ops=None, group=None, rounds=None, sample_stride=16):
+def distrib_sort_pairs(keys, vals, ops=None, group=None, rounds=None):
     """Stable sort of the distributed (uint64 key, uint32 payload) array whose
-    rank-r shard is (keys, vals) -- SURVEY C5.  The "msd" range-split rounds of
-    sort_msd on the top 12 bits of the key: one stable pair partition
-    (libsortPartitionLutU64U32), per round an alltoallv of the keys and one of
-    the payloads (issued up front, RCCL runs them back to back), a stable local
-    pair sort of each round as it arrives, then the equal re-cut.  Equal keys
-    keep their original global order: the partition and the local sort are
-    stable and a round's data arrive in source-rank order.  There is no
-    skew fallback: a heavy key range concentrates work on one rank, the result
-    stays exact.  Returns this rank's (keys, vals) shard, ceil(N/R) pairs."""
+    rank-r shard is (keys, vals) -- SURVEY C5.  The top-digit rounds of
+    sort_msd on the key's top 8 bits: one stable pair partition by key >> 56,
+    the exact digit counts gathered, the same host plan (plan_digits), per
+    round one point-to-point exchange of the keys and one of the payloads
+    (issued up front, RCCL runs them back to back), a stable pair sort of each
+    round as it arrives, then the equal re-cut.  Equal keys keep their
+    original global order: the partition and the round sort are stable and a
+    round's data arrive in source-rank order.  There is no skew fallback: a
+    heavy key range concentrates work on one rank, the result stays exact.
+    Returns this rank's (keys, vals) shard, ceil(N/R) pairs."""
     ops = HipOps() if ops is None else ops
     if dist.get_world_size(group) == 1:
         return ops.sort_pairs(keys, vals)
-    return _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride)
+    return _sort_pairs_rounds(keys, vals, ops, group, rounds)
 
 
-def _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride, self_local=True):
+def _sort_pairs_rounds(keys, vals, ops, group, rounds, self_local=True):
     """The round schedule of distrib_sort_pairs (any world size)."""
     R = dist.get_world_size(group)
     r = dist.get_rank(group)
     K = max(1, min(int(ROUNDS if rounds is None else rounds), 256 // R))
-    n = keys.numel()
-    NB = R * K
-    hi = ops.sample_hi(keys, sample_stride)
-    h = ops.histogram(hi, 32 - HIST_BITS, HIST_BITS)
-    HN = _allgather_t(torch.cat([h.to(torch.int64), torch.tensor([n], dtype=torch.int64, device=h.device)]), group)
-    lut_t, _ = _plan(ops, HN, R, K)
-    split = hasattr(ops, "partition_lut_pairs_count_t")
-    if split:
-        b_t = ops.partition_lut_pairs_count_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
-        side = _SideWork(b_t)
-        pk, pv = ops.partition_lut_pairs_scatter_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
-    else:
-        pk, pv, b_t = ops.partition_lut_pairs_t(keys, vals, lut_t, 32 - HIST_BITS, NB)
-        side = _SideWork(b_t)
-    with side:
-        sizes_t = _sizes_from_starts(b_t, n)
-        C_t = _allgather_t(sizes_t, group)
-        pending = _to_host_async(C_t)
-    C = pending.wait()                                         # the one host transfer
-    sizes = C[r]
-    b = np.concatenate([[0], np.cumsum(sizes)[:-1]])
-    recv_tot = np.array([int(C[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
+    (pk, pv), Cd = _digit_partition(keys, ops, group, vals=vals)
+    lut, est = plan_digits(Cd, R, K)
+    g = _DigitRounds(Cd, lut, R, K)
+    recv_tot = np.array([int(g.CB[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
     roff = np.concatenate([[0], np.cumsum(recv_tot)])
     T = int(roff[-1])
     rk, rv, ok_, ov = ops.empty64(T), ops.empty(T), ops.empty64(T), ops.empty(T)
     works = []
     for i in range(K):
-        if not C[:, i * R:(i + 1) * R].any():
-            works.append(())
-            continue
-        s0, ss = int(b[i * R]), sizes[i * R:(i + 1) * R]
-        a, z = int(roff[i]), int(roff[i + 1])
-        works.append((_alltoallv_into(rk[a:z], pk[s0:s0 + int(ss.sum())], ss, C[:, i * R + r], group, async_op=True,
-                                      self_local=self_local),
-                      _alltoallv_into(rv[a:z], pv[s0:s0 + int(ss.sum())], ss, C[:, i * R + r], group, async_op=True,
-                                      self_local=self_local)))
+        ks, kr, vs, vr = {}, {}, {}, {}
+        for d in range(R):
+            a, z = g.send_slice(r, i * R + d)
+            if z > a:
+                ks[d], vs[d] = pk[a:z], pv[a:z]
+        at = int(roff[i])
+        for src in range(R):
+            m = int(g.CB[src][i * R + r])
+            if m:
+                kr[src], vr[src] = rk[at:at + m], rv[at:at + m]
+            at += m
+        if self_local and r in ks:
+            kr.pop(r).copy_(ks.pop(r))
+            vr.pop(r).copy_(vs.pop(r))
+        works.append((_exchange_pieces(ks, kr, group), _exchange_pieces(vs, vr, group)))
     for i in range(K):
         for w in works[i]:
             if w is not None:
@@ -865,8 +940,7 @@ def _sort_pairs_rounds(keys, vals, ops, group, rounds, sample_stride, self_local
         a, z = int(roff[i]), int(roff[i + 1])
         if z > a:
             ops.sort_pairs(rk[a:z], rv[a:z], out_keys=ok_[a:z], out_vals=ov[a:z])
-    n_recv = np.array([int(C[:, d::R].sum()) for d in range(R)], dtype=np.int64)
-    return _rebalance_pairs(ok_, ov, n_recv, ops, group)
+    return _rebalance_pairs(ok_, ov, est, ops, group)
 
 
 def distrib_sort(keys, ops=None, group=None, schedule="auto", **kw):

@@ -264,6 +264,16 @@ LIBSORT_API bool libsortDistribSortU32(int nranks, const int* devices, const uin
                                        const size_t* n_in, uint32_t* const* d_out, size_t* n_out,
                                        uint32_t flags);
 
+/* Host plan of the multi-GPU top-digit rounds (pylibsort.distrib and the
+ * single-process engine above both run it; csrc/distrib_plan.h).
+ * counts[r * 256 + g] = keys of rank r whose top 8 bits are g (exact, from
+ * each rank's partition pass).  Writes lut[g] = round * nranks + rank of
+ * digit g -- contiguous digit ranges in key order, about 1/nranks of the keys
+ * per rank, `rounds` rounds per rank growing by `growth` -- and est[r] = keys
+ * rank r receives.  nranks * rounds <= 256.  Host only (no device needed). */
+LIBSORT_API bool libsortDistribPlanDigits(const int64_t* counts, uint32_t nranks, uint32_t rounds, double growth,
+                                          uint8_t* lut, int64_t* est);
+
 /* Writes elements [first, first+n) of the populateInput stream of a fresh
  * process (state 0x4d595df4d0f33173) to device memory, by LCG skip-ahead. */
 LIBSORT_API bool libsortPopulateDevice(uint32_t* d_out, size_t n, uint64_t first, void* stream);

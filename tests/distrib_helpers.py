@@ -95,6 +95,44 @@ class OracleOps:
         k, v, starts = self.partition_lut_pairs(keys, vals, lut.numpy(), shift, nbuckets)
         return k, v, self.torch.from_numpy(starts)
 
+    # top-digit rounds (distrib.sort_msd / sort_msdz / pairs)
+    def top_count_t(self, keys):
+        x = self._np(keys)
+        c = np.bincount(x >> np.uint32(24), minlength=256)
+        return self.torch.from_numpy(np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.int64))
+
+    def top_scatter_t(self, keys):
+        x = self._np(keys)
+        return self._t(x[np.argsort(x >> np.uint32(24), kind="stable")])
+
+    def top_pairs_count_t(self, keys, vals):
+        k = keys.numpy().view(np.uint64)
+        c = np.bincount((k >> np.uint64(56)).astype(np.int64), minlength=256)
+        return self.torch.from_numpy(np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.int64))
+
+    def top_pairs_scatter_t(self, keys, vals):
+        k = keys.numpy().view(np.uint64)
+        o = np.argsort(k >> np.uint64(56), kind="stable")
+        return self.torch.from_numpy(k[o].view(np.int64).copy()), self._t(vals.numpy().view(np.uint32)[o])
+
+    def sort_pieces(self, keys, off, lens, segs, nseg, out):
+        """libsortSortPiecesU32's contract, checked: every key of a segment
+        shares its top 8 bits and those increase with the segment."""
+        x = self._np(keys)
+        parts, tops = [], []
+        for o, ln, sg in zip(off, lens, segs):
+            p = x[int(o):int(o) + int(ln)]
+            if p.size:
+                t = np.unique(p >> np.uint32(24))
+                assert t.size == 1, "piece spans several top digits"
+                tops.append((int(sg), int(t[0])))
+            parts.append(p)
+        assert all(a[1] - a[0] == tops[0][1] - tops[0][0] for a in tops), "segment != top digit - first digit"
+        assert all(0 <= sg < nseg for sg in segs)
+        res = np.sort(np.concatenate(parts)) if parts else np.empty(0, np.uint32)
+        out.copy_(self._t(res))
+        return out
+
     def sample(self, keys, stride, block=4096):
         nb = keys.numel() // block
         if stride <= 1 or nb < 4 * stride:

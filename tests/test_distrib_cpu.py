@@ -52,9 +52,8 @@ def test_msd_rounds_gloo(tmp_path, world, rounds):
     assert [s.size for s in shards] == [s.size for s in shard_inputs(x, world)]
 
 
-def test_msd_sampled_histogram_gloo(tmp_path):
-    """Large enough for the sampled top-bit histogram (every 16th 4096-key
-    block): the plan is estimated, the exchange sizes exact."""
+def test_msd_larger_input_gloo(tmp_path):
+    """600K keys over 2 ranks: every digit populated, 4 rounds of ~16 digits."""
     from oracle import oracle
     x = oracle.pcg(2 * 300007, first=11)
     shards = run_ranks(x, 2, "msd", tmp_path, port=29790, kw={"rounds": 4})
@@ -95,41 +94,71 @@ def test_distrib_pairs_stable_gloo(tmp_path, world, rounds, case):
     assert [x.size for x in ks] == [min(n, (r + 1) * S) - min(n, r * S) for r in range(world)]
 
 
-def test_plan_rounds_contiguous_and_balanced():
-    from pylibsort.distrib import plan_rounds, _group_range
+def _plan_digits_restated(C, R, K, growth):
+    """numpy restatement of csrc/distrib_plan.h plan_rounds over the 256 top
+    digits (the checker of the one host plan both engines run): digit g's
+    middle in rank coordinates x = (cum(g) - G(g)/2) / N * R gives rank
+    floor(x); its round is the first i with x - rank < cw[i]; rank * K +
+    round made monotone by a cumulative max."""
+    G = C.sum(axis=0).astype(np.float64)
+    T = max(G.sum(), 1.0)
+    x = (np.cumsum(G) - G / 2.0) / T * R
+    rank = np.clip(np.floor(x), 0, R - 1).astype(np.int64)
+    w, p = [], 1.0
+    for _ in range(K):
+        w.append(p)
+        p *= growth
+    cw = np.cumsum(w) / np.sum(w)
+    rnd = np.minimum(np.searchsorted(cw, x - rank, side="right"), K - 1)
+    grp = np.maximum.accumulate(rank * K + rnd)
+    lut = ((grp % K) * R + grp // K).astype(np.uint8)
+    est = np.bincount(grp // K, weights=C.sum(axis=0), minlength=R).astype(np.int64)
+    return lut, est
+
+
+@pytest.mark.parametrize("R,K", [(1, 1), (2, 4), (3, 5), (8, 4), (16, 16), (4, 64)])
+@pytest.mark.parametrize("kind", ["uniform", "skew", "zero", "sparse"])
+def test_digit_plan_c_matches_restatement(R, K, kind):
+    """libsortDistribPlanDigits (the host plan sort_msd, sort_msdz, the pair
+    rounds and the single-process engine all run) equals the numpy
+    restatement; groups are contiguous, monotone and cover every digit."""
+    from pylibsort.distrib import plan_digits
+    rng = np.random.default_rng(R * 100 + K)
+    if kind == "uniform":
+        C = rng.integers(0, 100000, (R, 256))
+    elif kind == "skew":
+        C = rng.integers(0, 3, (R, 256))
+        C[:, 77] = 10 ** 9
+    elif kind == "zero":
+        C = np.zeros((R, 256), dtype=np.int64)
+    else:
+        C = np.zeros((R, 256), dtype=np.int64)
+        C[:, rng.integers(0, 256, 5)] = rng.integers(1, 5000, (R, 5))
+    for growth in (1.2, 0.6):
+        lut, est = plan_digits(C, R, K, growth)
+        lut_ref, est_ref = _plan_digits_restated(C, R, K, growth)
+        np.testing.assert_array_equal(lut, lut_ref)
+        np.testing.assert_array_equal(est, est_ref)
+        grp = (lut.astype(np.int64) % R) * K + lut // R
+        assert np.all(np.diff(grp) >= 0) and est.sum() == C.sum()
+
+
+def test_digit_plan_balanced_rounds_grow():
+    from pylibsort.distrib import plan_digits, shard_cut
     rng = np.random.default_rng(4)
     R, K = 8, 4
-    H = np.stack([np.bincount(rng.integers(0, 4096, 200000), minlength=4096) for _ in range(R)])
-    lut, est = plan_rounds(H, R, K, growth=1.6)
-    grp = (lut % R) * K + lut // R                 # back to key-order group index
-    assert lut.dtype == np.uint8 and lut.size == 4096
-    assert np.all(np.diff(grp.astype(np.int64)) >= 0) and grp[0] == 0 and grp[-1] == R * K - 1
-    tot, bmax = H.sum(), H.sum(axis=0).max()
-    assert abs(est.sum() - tot) < 1e-6 and np.all(np.abs(est - tot / R) <= bmax + 1)   # ranks balanced
-    g = np.bincount(grp, weights=H.sum(axis=0), minlength=R * K).reshape(R, K)
-    w = 1.6 ** np.arange(K)
-    np.testing.assert_allclose(g / g.sum(axis=1, keepdims=True), np.tile(w / w.sum(), (R, 1)), atol=0.02)
-    lo, hi = _group_range(lut, 0 * R + 0)          # first round of rank 0 starts at key 0
-    assert lo == 0 and hi > 0
-    assert _group_range(lut, (K - 1) * R + R - 1)[1] == 1 << 32
-    lut0, est0 = plan_rounds(np.zeros((R, 4096)), R, K)
-    assert not lut0.any() and not est0.any()
-
-
-def test_plan_msd_balances_uniform_and_flags_skew():
-    from pylibsort.distrib import plan_msd, shard_cut
-    rng = np.random.default_rng(3)
-    R = 8
-    H = np.stack([np.bincount(rng.integers(0, 4096, 100000), minlength=4096) for _ in range(R)])
-    splitters, dest, n_recv = plan_msd(H, R)
-    S, _ = shard_cut(int(H.sum()), R)
-    assert len(splitters) == R - 1 and splitters == sorted(splitters)
-    assert np.all(np.diff(dest) >= 0) and n_recv.sum() == H.sum()
-    assert n_recv.max() <= S + H.sum(axis=0).max()
-    skew = np.zeros((R, 4096), dtype=np.int64)
+    C = np.stack([np.bincount(rng.integers(0, 256, 2000000), minlength=256) for _ in range(R)])
+    lut, est = plan_digits(C, R, K, 1.2)
+    S, _ = shard_cut(int(C.sum()), R)
+    assert np.abs(est - S).max() <= C.sum(axis=0).max()        # within one digit of the equal share
+    grp = (lut.astype(np.int64) % R) * K + lut // R
+    g = np.bincount(grp, weights=C.sum(axis=0), minlength=R * K).reshape(R, K)
+    w = 1.2 ** np.arange(K)
+    np.testing.assert_allclose(g / g.sum(axis=1, keepdims=True), np.tile(w / w.sum(), (R, 1)), atol=0.04)
+    skew = np.zeros((R, 256), dtype=np.int64)
     skew[:, 17] = 1000
-    _, _, n2 = plan_msd(skew, R)
-    assert n2.max() == skew.sum()  # one bucket holds everything -> sort_msd falls back to lsd
+    _, est2 = plan_digits(skew, R, K)
+    assert est2.max() == skew.sum()  # one digit holds everything -> sort_msd falls back to lsd
 
 
 def test_shard_cut_matches_reference():
