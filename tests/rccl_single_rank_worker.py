@@ -45,7 +45,7 @@ def main():
     v = np.arange(m, dtype=np.uint32)
     kt = torch.from_numpy(k.view(np.int64)).cuda()
     vt = torch.from_numpy(v.view(np.int32)).cuda()
-    rk, rv = distrib._sort_pairs_rounds(kt, vt, ops, None, 4, 16, self_local=False)
+    rk, rv = distrib._sort_pairs_rounds(kt, vt, ops, None, 4, self_local=False)
     torch.cuda.synchronize()
     o = np.argsort(k, kind="stable")
     assert np.array_equal(rk.cpu().numpy().view(np.uint64), k[o]), "pairs keys"

@@ -38,10 +38,30 @@ def main():
         torch.cuda.synchronize()
         return (time.perf_counter() - t0) / reps * 1e3
 
+    if os.environ.get("MSD_PROFILE"):
+        # for rocprofv3 --kernel-trace --stats: only the K = 4 schedule,
+        # 2 warm-up + MSD_PROFILE timed steps (kernel totals / steps = the
+        # GPU work of one step, by kernel)
+        reps = int(os.environ["MSD_PROFILE"])
+        for _ in range(2 + reps):
+            distrib.sort_msd(keys, ops, rounds=4)
+        torch.cuda.synchronize()
+        print({"msd_profile_steps": reps, "warmup": 2})
+        dist.destroy_process_group()
+        return
     res = {"plain_sort_ms": timed(lambda: D.sort_keys_u32(keys, out=out, tmp=tmp))}
+    # at one rank the "self piece" of every round is the whole round (a
+    # device copy of all n keys); at R ranks it is 1/R of the keys -- the
+    # copy's own time is reported so it can be taken out of the schedule
+    res["selfcopy_all_keys_ms"] = timed(lambda: out.copy_(keys))
     for K in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
         res["msd_rounds%d_selfcopy_ms" % K] = timed(lambda: distrib.sort_msd(keys, ops, rounds=K))
+        res["msd_rounds%d_minus_selfcopy_ms" % K] = res["msd_rounds%d_selfcopy_ms" % K] - res["selfcopy_all_keys_ms"]
         res["msd_rounds%d_via_rccl_ms" % K] = timed(lambda: distrib.sort_msd(keys, ops, rounds=K, self_local=False))
+    if os.environ.get("MSD_DIGIT8", "1") == "1":
+        pylibsort.setDigitBits(8)
+        res["digit8_msd_rounds4_selfcopy_ms"] = timed(lambda: distrib.sort_msd(keys, ops, rounds=4))
+        pylibsort.setDigitBits(4)
     print({k: round(v, 3) for k, v in res.items()})
     for K in (1, 4):
         tr = []
