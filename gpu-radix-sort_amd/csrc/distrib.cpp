@@ -11,15 +11,23 @@
 // state -- rank r holds keys [r*S, (r+1)*S) of the sorted whole, S =
 // ceil(N/R), the reference's equal re-cut (distrib.go:113):
 //
-//   range rounds (default): a sampled top-12-bit histogram per rank, ONE
-//     host plan of (rank, round) key ranges (distrib_plan.h plan_rounds), one
-//     stable table partition per rank (round-major, destination-minor), K
-//     exchange rounds issued up front on each rank's communication stream,
-//     and each round sorted into its slice of the rank's output on the
-//     compute stream as soon as it has arrived (range-restricted LSD: digits
-//     of key - lo), overlapping the later rounds' exchange; then the equal
-//     re-cut moves the few surplus keys.  Falls back to the LSD rounds when
-//     one key range would overload a rank (identical decision for all).
+//   top-digit rounds (default): per rank a stable partition by the top 8
+//     key bits (the reference's gpuPartial(offset 24, width 8) building
+//     block, split in a count and a scatter call) whose 256 exact bucket
+//     counts go to the host while the scatter runs; ONE host plan of (rank,
+//     round) digit ranges (distrib_plan.h plan_digit_rounds, the same plan
+//     pylibsort.distrib runs); K exchange rounds issued up front on each
+//     rank's communication stream; each round sorted into its slice of the
+//     rank's output as soon as it has arrived, straight from the received
+//     (source, digit) pieces (sort_pieces_u32: no gather, no pass over the
+//     top digit), overlapping the later rounds' exchange -- the round sorts
+//     of different devices are issued by one host thread per device, so one
+//     device's host read-backs never hold another's; then the equal re-cut
+//     moves the few surplus keys.  Falls back to the LSD rounds when one
+//     digit range would overload a rank (identical decision for all).
+//     (u64 key, u32 payload) pairs (configs[4], distrib_sort_pairs_u64_u32)
+//     take the same rounds on the key's top 8 bits with a stable pair sort
+//     per round.
 //   LSD rounds (LIBSORT_DISTRIB_LSD): the reference's BSP semantics -- per
 //     8-bit digit a stable local partial sort (gpuPartial on the device), the
 //     bucket counts to the host, one exchange of contiguous slices and a
@@ -44,6 +52,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "distrib_plan.h"
@@ -150,13 +159,14 @@ struct DevState {
   hipStream_t st = nullptr;  // compute
   hipStream_t cs = nullptr;  // exchanges
   hipEvent_t ev_comm = nullptr, ev_comp = nullptr;
-  DBuf lut, tmp;
+  DBuf lut;        // the identity table of the 256 top digits (partition by key >> 24)
+  DBuf tmp, tmpv;  // round-sort scratch (keys; pair payloads)
 };
 
 struct RankState {
   int dev = -1;
   DevState* d = nullptr;
-  DBuf row, bounds, part, recv, outb, alt;
+  DBuf bounds, part, pv, recv, rv, outb, ov, alt;  // pv / rv / ov: pair payloads
   DBuf hin, hout;  // staging of the host-pointer entry point
   hipEvent_t ev_part = nullptr, ev_bounds = nullptr, ev_done = nullptr;
   hipEvent_t ev_x[kMaxRounds] = {};
@@ -167,7 +177,6 @@ struct Ctx {
   std::vector<std::unique_ptr<DevState>> uniq;  // one per distinct device
   std::vector<RankState> ranks;
   std::vector<ncclComm_t> comms;               // RCCL communicator of each rank (distinct devices only)
-  int64_t* h_rows = nullptr;                   // pinned: R x 4097 plan rows
   uint32_t* h_bounds = nullptr;                // pinned: R x 256 bucket starts
   bool distinct = false;
 
@@ -175,14 +184,8 @@ struct Ctx {
     for (ncclComm_t c : comms)
       if (c && g_rccl.loaded) (void)g_rccl.commDestroy(c);
     for (auto& r : ranks) {
-      r.row.release();
-      r.bounds.release();
-      r.part.release();
-      r.recv.release();
-      r.outb.release();
-      r.alt.release();
-      r.hin.release();
-      r.hout.release();
+      for (DBuf* b : {&r.bounds, &r.part, &r.pv, &r.recv, &r.rv, &r.outb, &r.ov, &r.alt, &r.hin, &r.hout})
+        b->release();
       (void)hipSetDevice(r.dev);
       for (hipEvent_t e : {r.ev_part, r.ev_bounds, r.ev_done})
         if (e) (void)hipEventDestroy(e);
@@ -192,13 +195,13 @@ struct Ctx {
     for (auto& u : uniq) {
       u->lut.release();
       u->tmp.release();
+      u->tmpv.release();
       (void)hipSetDevice(u->dev);
       if (u->st) (void)hipStreamDestroy(u->st);
       if (u->cs) (void)hipStreamDestroy(u->cs);
       if (u->ev_comm) (void)hipEventDestroy(u->ev_comm);
       if (u->ev_comp) (void)hipEventDestroy(u->ev_comp);
     }
-    if (h_rows) (void)hipHostFree(h_rows);
     if (h_bounds) (void)hipHostFree(h_bounds);
   }
 
@@ -206,6 +209,15 @@ struct Ctx {
     devs = d;
     const int R = (int)d.size();
     std::map<int, DevState*> by_dev;
+    static const uint8_t kIdentity[dplan::kTopDigits] = {
+#define LS_I4(x) x, x + 1, x + 2, x + 3
+#define LS_I16(x) LS_I4(x), LS_I4(x + 4), LS_I4(x + 8), LS_I4(x + 12)
+#define LS_I64(x) LS_I16(x), LS_I16(x + 16), LS_I16(x + 32), LS_I16(x + 48)
+        LS_I64(0), LS_I64(64), LS_I64(128), LS_I64(192)
+#undef LS_I64
+#undef LS_I16
+#undef LS_I4
+    };
     for (int dev : d) {
       if (by_dev.count(dev)) continue;
       auto u = std::make_unique<DevState>();
@@ -215,7 +227,9 @@ struct Ctx {
           !ok_hip(hipStreamCreateWithFlags(&u->st, hipStreamNonBlocking), "hipStreamCreate") ||
           !ok_hip(hipStreamCreateWithFlags(&u->cs, hipStreamNonBlocking), "hipStreamCreate") ||
           !ok_hip(hipEventCreateWithFlags(&u->ev_comm, hipEventDisableTiming), "hipEventCreate") ||
-          !ok_hip(hipEventCreateWithFlags(&u->ev_comp, hipEventDisableTiming), "hipEventCreate"))
+          !ok_hip(hipEventCreateWithFlags(&u->ev_comp, hipEventDisableTiming), "hipEventCreate") ||
+          !u->lut.ensure(dev, dplan::kTopDigits) ||
+          !ok_hip(hipMemcpy(u->lut.p, kIdentity, dplan::kTopDigits, hipMemcpyHostToDevice), "H2D digit table"))
         return false;
       by_dev[dev] = u.get();
       uniq.push_back(std::move(u));
@@ -231,13 +245,9 @@ struct Ctx {
         if (!ok_hip(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate")) return false;
       for (hipEvent_t& e : s.ev_x)
         if (!ok_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate")) return false;
-      if (!s.row.ensure(s.dev, (dplan::kHistBins + 1) * sizeof(int64_t)) || !s.bounds.ensure(s.dev, 256 * 4))
-        return false;
+      if (!s.bounds.ensure(s.dev, dplan::kTopDigits * 4)) return false;
     }
-    for (auto& u : uniq)
-      if (!u->lut.ensure(u->dev, dplan::kHistBins)) return false;
-    return ok_hip(hipHostMalloc(&h_rows, (size_t)R * (dplan::kHistBins + 1) * sizeof(int64_t), 0), "hipHostMalloc") &&
-           ok_hip(hipHostMalloc(&h_bounds, (size_t)R * 256 * sizeof(uint32_t), 0), "hipHostMalloc");
+    return ok_hip(hipHostMalloc(&h_bounds, (size_t)R * dplan::kTopDigits * sizeof(uint32_t), 0), "hipHostMalloc");
   }
 
   bool ensure_comms() {
@@ -252,29 +262,33 @@ std::mutex g_dist_mu;  // one distributed sort at a time (it holds several devic
 std::unique_ptr<Ctx> g_ctx;
 
 // Moves the pieces: rank p.src's src[p.src] + src_off -> rank p.dst's
-// dst[p.dst] + dst_off, on the communication streams.  A piece within one
-// device is a device copy (unless self_rccl); across devices RCCL
-// point-to-point (one group for the whole set) or, with `copy`, a peer copy
-// pulled by the receiver.
-bool move_pieces(Ctx& c, const std::vector<dplan::Piece>& ps, const std::vector<const uint32_t*>& src,
-                 const std::vector<uint32_t*>& dst, bool use_rccl, bool self_rccl) {
+// dst[p.dst] + dst_off (offsets and counts in elements of `esize` bytes: 4 or
+// 8), on the communication streams.  A piece within one device is a device
+// copy (unless self_rccl); across devices RCCL point-to-point (one group for
+// the whole set) or, with `copy`, a peer copy pulled by the receiver.
+bool move_pieces(Ctx& c, const std::vector<dplan::Piece>& ps, const std::vector<const void*>& src,
+                 const std::vector<void*>& dst, size_t esize, bool use_rccl, bool self_rccl) {
+  const ncclDataType_t dt = esize == 8 ? ncclUint64 : ncclUint32;
+  auto at = [esize](const void* base, uint64_t off) { return static_cast<const char*>(base) + off * esize; };
+  auto atw = [esize](void* base, uint64_t off) { return static_cast<char*>(base) + off * esize; };
   std::vector<const dplan::Piece*> net;
   for (const dplan::Piece& p : ps) {
     if (!p.count) continue;
     RankState& a = c.ranks[p.src];
     RankState& b = c.ranks[p.dst];
-    const size_t bytes = p.count * sizeof(uint32_t);
+    const size_t bytes = p.count * esize;
     if (use_rccl && (p.src != p.dst || self_rccl)) {
       net.push_back(&p);
     } else if (a.dev == b.dev) {
       if (!ok_hip(hipSetDevice(b.dev), "hipSetDevice") ||
-          !ok_hip(hipMemcpyAsync(dst[p.dst] + p.dst_off, src[p.src] + p.src_off, bytes, hipMemcpyDeviceToDevice,
-                                 b.d->cs),
+          !ok_hip(hipMemcpyAsync(atw(dst[p.dst], p.dst_off), at(src[p.src], p.src_off), bytes,
+                                 hipMemcpyDeviceToDevice, b.d->cs),
                   "device copy"))
         return false;
     } else {
       if (!ok_hip(hipSetDevice(b.dev), "hipSetDevice") ||
-          !ok_hip(hipMemcpyPeerAsync(dst[p.dst] + p.dst_off, b.dev, src[p.src] + p.src_off, a.dev, bytes, b.d->cs),
+          !ok_hip(hipMemcpyPeerAsync(atw(dst[p.dst], p.dst_off), b.dev, at(src[p.src], p.src_off), a.dev, bytes,
+                                     b.d->cs),
                   "peer copy"))
         return false;
     }
@@ -285,12 +299,27 @@ bool move_pieces(Ctx& c, const std::vector<dplan::Piece>& ps, const std::vector<
   for (const dplan::Piece* p : net) {
     RankState& a = c.ranks[p->src];
     RankState& b = c.ranks[p->dst];
-    ok = ok && g_rccl.ok(g_rccl.send(src[p->src] + p->src_off, p->count, ncclUint32, p->dst, c.comms[p->src], a.d->cs),
+    ok = ok && g_rccl.ok(g_rccl.send(at(src[p->src], p->src_off), p->count, dt, p->dst, c.comms[p->src], a.d->cs),
                          "ncclSend") &&
-         g_rccl.ok(g_rccl.recv(dst[p->dst] + p->dst_off, p->count, ncclUint32, p->src, c.comms[p->dst], b.d->cs),
+         g_rccl.ok(g_rccl.recv(atw(dst[p->dst], p->dst_off), p->count, dt, p->src, c.comms[p->dst], b.d->cs),
                    "ncclRecv");
   }
   return g_rccl.ok(g_rccl.groupEnd(), "ncclGroupEnd") && ok;
+}
+
+// Copy mode across devices: a peer copy is pulled on the RECEIVER's stream
+// from the sender's buffer, so every compute stream waits for every device's
+// communication stream before the buffers those copies read are rewritten.
+bool compute_waits_all_comm(Ctx& c) {
+  for (auto& u : c.uniq)
+    if (!ok_hip(hipSetDevice(u->dev), "hipSetDevice") || !ok_hip(hipEventRecord(u->ev_comm, u->cs), "record"))
+      return false;
+  for (auto& u : c.uniq) {
+    if (!ok_hip(hipSetDevice(u->dev), "hipSetDevice")) return false;
+    for (auto& v : c.uniq)
+      if (!ok_hip(hipStreamWaitEvent(u->st, v->ev_comm, 0), "wait")) return false;
+  }
+  return true;
 }
 
 // every communication stream waits for every rank's `ev` (cheap: R events)
@@ -310,13 +339,6 @@ bool sync_all(Ctx& c) {
          ok_hip(hipStreamSynchronize(u->st), "sync compute") && ok;
   }
   return ok;
-}
-
-int span_bits(uint64_t lo, uint64_t hi) {
-  const uint64_t span = hi - lo - 1;
-  int w = 0;
-  while (w < 32 && (span >> w) != 0) ++w;
-  return std::max(w, 1);
 }
 
 // The reference's BSP rounds (see the file comment).  cur: per-rank input.
@@ -361,27 +383,20 @@ bool run_lsd(Ctx& c, const std::vector<const uint32_t*>& in, const std::vector<u
     }
     dplan::LsdRound o = dplan::lsd_round(C, S);
     if (!comm_waits(c, &RankState::ev_part)) return false;
-    std::vector<const uint32_t*> src(R);
-    std::vector<uint32_t*> dst(R);
+    std::vector<const void*> src(R);
+    std::vector<void*> dst(R);
     for (int r = 0; r < R; ++r) {
-      src[r] = c.ranks[r].part.u32();
-      dst[r] = c.ranks[r].recv.u32();
+      src[r] = c.ranks[r].part.p;
+      dst[r] = c.ranks[r].recv.p;
     }
-    if (!move_pieces(c, o.pieces, src, dst, use_rccl, self_rccl)) return false;
+    if (!move_pieces(c, o.pieces, src, dst, 4, use_rccl, self_rccl)) return false;
     // gather into bucket-major / rank-minor order on the compute stream.
     // Every compute stream waits for EVERY device's communication stream: a
     // peer copy (copy mode across devices) is pulled on the receiver's stream
     // from the sender's `part`, which the sender's next partial sort rewrites
     // (write-after-read across devices).
     const bool last = step + 1 == 32 / W;
-    for (auto& u : c.uniq)
-      if (!ok_hip(hipSetDevice(u->dev), "hipSetDevice") || !ok_hip(hipEventRecord(u->ev_comm, u->cs), "record"))
-        return false;
-    for (auto& u : c.uniq) {
-      if (!ok_hip(hipSetDevice(u->dev), "hipSetDevice")) return false;
-      for (auto& v : c.uniq)
-        if (!ok_hip(hipStreamWaitEvent(u->st, v->ev_comm, 0), "wait")) return false;
-    }
+    if (!compute_waits_all_comm(c)) return false;
     for (int r = 0; r < R; ++r) {
       RankState& s = c.ranks[r];
       uint32_t* nxt = last ? out[r] : (step & 1 ? s.outb.u32() : s.alt.u32());
@@ -418,14 +433,197 @@ Ctx* ctx_for(const int* devices, int R) {
   return g_ctx.get();
 }
 
-bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32_t* const* d_out, size_t* n_out,
-                 unsigned flags, int bits) {
+// Every involved workspace held (ascending device order) and its stream
+// ordered after other callers' work, for the whole sort; release() syncs.
+struct Hold {
+  Ctx& c;
+  std::vector<std::unique_lock<std::mutex>> locks;
+  bool ok = true;
+  explicit Hold(Ctx& cx) : c(cx) {
+    std::vector<DevState*> order;
+    for (auto& u : c.uniq) order.push_back(u.get());
+    std::sort(order.begin(), order.end(), [](DevState* a, DevState* b) { return a->dev < b->dev; });
+    for (DevState* u : order) locks.emplace_back(u->ws->mu);
+    for (DevState* u : order)
+      if (!ws_acquire_stream(u->dev, u->st)) ok = false;
+  }
+  bool finish(bool result) {
+    const bool synced = sync_all(c);
+    for (auto& u : c.uniq) ws_release_stream(u->dev, u->st);
+    return result && synced;
+  }
+};
+
+// fn(device) for every distinct device, each on a host thread of its own
+// (the round sorts wait on the host for small read-backs; one device's waits
+// must not hold another device's issue -- ADVICE r02); inline for one device.
+// A failing thread's message is re-raised on the caller's thread.
+template <typename F>
+bool per_device(Ctx& c, F&& fn) {
+  if (c.uniq.size() == 1) return ok_hip(hipSetDevice(c.uniq[0]->dev), "hipSetDevice") && fn(*c.uniq[0]);
+  std::vector<std::string> err(c.uniq.size());
+  std::vector<char> good(c.uniq.size(), 1);
+  std::vector<std::thread> th;
+  for (size_t u = 0; u < c.uniq.size(); ++u)
+    th.emplace_back([&, u] {
+      DevState& d = *c.uniq[u];
+      if (!ok_hip(hipSetDevice(d.dev), "hipSetDevice") || !fn(d)) {
+        good[u] = 0;
+        err[u] = last_error();
+      }
+    });
+  for (auto& t : th) t.join();
+  for (size_t u = 0; u < good.size(); ++u)
+    if (!good[u]) {
+      set_error(err[u]);
+      return false;
+    }
+  return true;
+}
+
+// Stable partition of every rank's keys (and payloads) by their top 8 bits
+// into part (pv): the count call (per-tile counts + column scan) and the
+// 256 bucket starts' copy to the host are queued first, then the scatter, so
+// the host reads the counts while the data moves.  C[r][g] = rank r's keys
+// in digit g.
+template <typename K>
+bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<const uint32_t*>* vin,
+                   const std::vector<uint64_t>& n, std::vector<std::vector<uint64_t>>& C) {
   const int R = (int)c.ranks.size();
-  const bool copy = (flags & kDistribCopy) != 0 || !c.distinct;
-  const bool self_rccl = (flags & kDistribSelfRccl) != 0 && !copy;
-  if (!copy && !c.ensure_comms()) return false;
-  uint64_t N = 0;
-  std::vector<uint64_t> n(R);
+  constexpr int NB = dplan::kTopDigits;
+  for (int r = 0; r < R; ++r) {
+    RankState& s = c.ranks[r];
+    if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !s.part.ensure(s.dev, std::max<uint64_t>(n[r], 1) * sizeof(K)) ||
+        (vin && !s.pv.ensure(s.dev, std::max<uint64_t>(n[r], 1) * 4)))
+      return false;
+    const uint8_t* lut = static_cast<const uint8_t*>(s.d->lut.p);
+    Workspace& ws = *s.d->ws;
+    if (n[r]) {
+      hipError_t e1, e2;
+      if constexpr (sizeof(K) == 4) {
+        e1 = partition_lut_u32(ws, in[r], nullptr, n[r], lut, dplan::kTopShift, NB, s.bounds.u32(), s.d->st,
+                               kPartCount);
+      } else {
+        e1 = partition_lut_pairs_u64_u32(ws, in[r], (*vin)[r], nullptr, nullptr, n[r], lut, dplan::kTopShift, NB,
+                                         s.bounds.u32(), s.d->st, kPartCount);
+      }
+      if (!ok_hip(e1, "partition counts") ||
+          !ok_hip(hipMemcpyAsync(c.h_bounds + (size_t)r * NB, s.bounds.p, NB * 4, hipMemcpyDeviceToHost, s.d->st),
+                  "D2H bucket starts") ||
+          !ok_hip(hipEventRecord(s.ev_bounds, s.d->st), "hipEventRecord"))
+        return false;
+      if constexpr (sizeof(K) == 4) {
+        e2 = partition_lut_u32(ws, in[r], s.part.u32(), n[r], lut, dplan::kTopShift, NB, nullptr, s.d->st,
+                               kPartScatter);
+      } else {
+        e2 = partition_lut_pairs_u64_u32(ws, in[r], (*vin)[r], static_cast<uint64_t*>(s.part.p), s.pv.u32(), n[r],
+                                         lut, dplan::kTopShift, NB, nullptr, s.d->st, kPartScatter);
+      }
+      if (!ok_hip(e2, "partition scatter")) return false;
+    }
+    if (!ok_hip(hipEventRecord(s.ev_part, s.d->st), "hipEventRecord")) return false;
+  }
+  C.assign(R, std::vector<uint64_t>(NB, 0));
+  for (int r = 0; r < R; ++r) {
+    if (!n[r]) continue;
+    if (!ok_hip(hipEventSynchronize(c.ranks[r].ev_bounds), "hipEventSynchronize")) return false;
+    const uint32_t* b = c.h_bounds + (size_t)r * NB;
+    for (int g = 0; g < NB; ++g) C[r][g] = (g + 1 < NB ? (uint64_t)b[g + 1] : n[r]) - b[g];
+  }
+  return true;
+}
+
+// The rounds after the partition: every round's exchange issued up front on
+// the communication streams, each round sorted into its slice of the rank's
+// output as soon as it has arrived (keys: straight from the (source, digit)
+// pieces; pairs: a stable pair sort, the pieces arriving in source order),
+// then the equal re-cut into out (vout).
+template <typename K>
+bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& out,
+                      const std::vector<uint32_t*>* vout, bool use_rccl, bool self_rccl, int bits) {
+  const int R = (int)c.ranks.size(), K_ = p.K;
+  const bool pairs = vout != nullptr;
+  std::map<DevState*, uint64_t> round_max;
+  for (int r = 0; r < R; ++r) {
+    RankState& s = c.ranks[r];
+    const uint64_t m = std::max<uint64_t>(p.n_recv[r], 1);
+    if (!s.recv.ensure(s.dev, m * sizeof(K)) || !s.outb.ensure(s.dev, m * sizeof(K)) ||
+        (pairs && (!s.rv.ensure(s.dev, m * 4) || !s.ov.ensure(s.dev, m * 4))))
+      return false;
+    for (int i = 0; i < K_; ++i)
+      round_max[s.d] = std::max(round_max[s.d], p.roff[(size_t)r * (K_ + 1) + i + 1] - p.roff[(size_t)r * (K_ + 1) + i]);
+  }
+  for (auto& kv : round_max)
+    if (!kv.first->tmp.ensure(kv.first->dev, std::max<uint64_t>(kv.second, 1) * sizeof(K)) ||
+        (pairs && !kv.first->tmpv.ensure(kv.first->dev, std::max<uint64_t>(kv.second, 1) * 4)))
+      return false;
+  if (!comm_waits(c, &RankState::ev_part)) return false;
+  std::vector<const void*> src(R), vsrc(R);
+  std::vector<void*> dst(R), vdst(R);
+  for (int r = 0; r < R; ++r) {
+    src[r] = c.ranks[r].part.p;
+    dst[r] = c.ranks[r].recv.p;
+    vsrc[r] = c.ranks[r].pv.p;
+    vdst[r] = c.ranks[r].rv.p;
+  }
+  for (int i = 0; i < K_; ++i) {
+    if (!move_pieces(c, p.rounds[i], src, dst, sizeof(K), use_rccl, self_rccl) ||
+        (pairs && !move_pieces(c, p.rounds[i], vsrc, vdst, 4, use_rccl, self_rccl)))
+      return false;
+    for (int r = 0; r < R; ++r) {
+      RankState& s = c.ranks[r];
+      if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !ok_hip(hipEventRecord(s.ev_x[i], s.d->cs), "record"))
+        return false;
+    }
+  }
+  // each round sorted on arrival, one host thread per device
+  const bool sorted = per_device(c, [&](DevState& d) {
+    for (int i = 0; i < K_; ++i)
+      for (int r = 0; r < R; ++r) {
+        RankState& s = c.ranks[r];
+        if (s.d != &d) continue;
+        const uint64_t a = p.roff[(size_t)r * (K_ + 1) + i], z = p.roff[(size_t)r * (K_ + 1) + i + 1];
+        if (!ok_hip(hipStreamWaitEvent(d.st, s.ev_x[i], 0), "wait")) return false;
+        if (z == a) continue;
+        hipError_t e;
+        if constexpr (sizeof(K) == 4) {
+          const size_t q = (size_t)r * K_ + i;
+          e = sort_pieces_u32(*d.ws, s.recv.u32() + a, s.outb.u32() + a, d.tmp.u32(), z - a, p.p_off[q].data(),
+                              p.p_len[q].data(), p.p_seg[q].data(), p.p_off[q].size(),
+                              (uint32_t)(p.hi[(size_t)i * R + r] - p.lo[(size_t)i * R + r]), dplan::kTopShift, bits,
+                              d.st);
+        } else {
+          e = sort_pairs_u64_u32(*d.ws, static_cast<uint64_t*>(s.recv.p) + a, s.rv.u32() + a,
+                                 static_cast<uint64_t*>(s.outb.p) + a, s.ov.u32() + a, static_cast<uint64_t*>(d.tmp.p),
+                                 d.tmpv.u32(), z - a, 0, 64, bits, d.st);
+        }
+        if (!ok_hip(e, "round sort")) return false;
+      }
+    return true;
+  });
+  if (!sorted) return false;
+  // the equal re-cut into the caller's shards
+  for (int r = 0; r < R; ++r) {
+    RankState& s = c.ranks[r];
+    if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !ok_hip(hipEventRecord(s.ev_done, s.d->st), "record"))
+      return false;
+  }
+  if (!comm_waits(c, &RankState::ev_done)) return false;
+  const std::vector<dplan::Piece> cut = dplan::recut_pieces(p.n_recv);
+  for (int r = 0; r < R; ++r) {
+    src[r] = c.ranks[r].outb.p;
+    dst[r] = out[r];
+    vsrc[r] = c.ranks[r].ov.p;
+    vdst[r] = pairs ? (*vout)[r] : nullptr;
+  }
+  return move_pieces(c, cut, src, dst, sizeof(K), use_rccl, self_rccl) &&
+         (!pairs || move_pieces(c, cut, vsrc, vdst, 4, use_rccl, self_rccl));
+}
+
+// Shared prologue of both entry points: sizes, the output shard counts.
+bool check_sizes(int R, const size_t* n_in, std::vector<uint64_t>& n, uint64_t& N, size_t* n_out) {
+  n.assign(R, 0);
+  N = 0;
   for (int r = 0; r < R; ++r) {
     n[r] = n_in[r];
     N += n[r];
@@ -439,143 +637,69 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
     set_error("distributed sort: at most 2^32-1 keys per output shard");
     return false;
   }
-  for (int r = 0; r < R; ++r) n_out[r] = (size_t)(std::min<uint64_t>(N, (uint64_t)(r + 1) * S) -
-                                                  std::min<uint64_t>(N, (uint64_t)r * S));
-  // hold every involved workspace (ascending device order) for the whole sort
-  std::vector<std::unique_lock<std::mutex>> locks;
-  {
-    std::vector<DevState*> order;
-    for (auto& u : c.uniq) order.push_back(u.get());
-    std::sort(order.begin(), order.end(), [](DevState* a, DevState* b) { return a->dev < b->dev; });
-    for (DevState* u : order) locks.emplace_back(u->ws->mu);
-    for (DevState* u : order)
-      if (!ws_acquire_stream(u->dev, u->st)) return false;
-  }
-  auto finish = [&](bool ok) {
-    const bool synced = sync_all(c);
-    for (auto& u : c.uniq) ws_release_stream(u->dev, u->st);
-    return ok && synced;
-  };
+  for (int r = 0; r < R; ++r)
+    n_out[r] = (size_t)(std::min<uint64_t>(N, (uint64_t)(r + 1) * S) - std::min<uint64_t>(N, (uint64_t)r * S));
+  return true;
+}
+
+bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32_t* const* d_out, size_t* n_out,
+                 unsigned flags, int bits) {
+  const int R = (int)c.ranks.size();
+  const bool copy = (flags & kDistribCopy) != 0 || !c.distinct;
+  const bool self_rccl = (flags & kDistribSelfRccl) != 0 && !copy;
+  if (!copy && !c.ensure_comms()) return false;
+  std::vector<uint64_t> n;
+  uint64_t N = 0;
+  if (!check_sizes(R, n_in, n, N, n_out)) return false;
+  Hold hold(c);
+  if (!hold.ok) return hold.finish(false);
   std::vector<const uint32_t*> in(d_in, d_in + R);
   std::vector<uint32_t*> out(d_out, d_out + R);
-  if (N == 0) return finish(true);
-
-  bool lsd = (flags & kDistribLsd) != 0;
+  if (N == 0) return hold.finish(true);
+  const uint64_t S = dplan::shard_size(N, R);
+  if (flags & kDistribLsd) return hold.finish(run_lsd(c, in, n, out, S, bits, !copy, self_rccl));
   const int K = std::max(1, std::min(kMaxRounds, 256 / R));
-  std::vector<uint8_t> lut(dplan::kHistBins);
-  if (!lsd) {
-    // 1. sampled top-12-bit histogram of every rank (every 16th 4096-key block)
-    for (int r = 0; r < R; ++r) {
-      RankState& s = c.ranks[r];
-      int64_t* h = c.h_rows + (size_t)r * (dplan::kHistBins + 1);
-      if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice")) return finish(false);
-      if (!n[r]) {
-        memset(h, 0, (dplan::kHistBins + 1) * sizeof(int64_t));
-        continue;
-      }
-      if (!ok_hip(plan_hist_u32(*s.d->ws, in[r], n[r], 12, 4096, 16, static_cast<int64_t*>(s.row.p), s.d->st),
-                  "plan histogram") ||
-          !ok_hip(hipMemcpyAsync(h, s.row.p, (dplan::kHistBins + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s.d->st),
-                  "D2H plan row") ||
-          !ok_hip(hipEventRecord(s.ev_bounds, s.d->st), "hipEventRecord"))
-        return finish(false);
-    }
-    for (int r = 0; r < R; ++r)
-      if (n[r] && !ok_hip(hipEventSynchronize(c.ranks[r].ev_bounds), "hipEventSynchronize")) return finish(false);
-    // 2. the plan, once, on the host
-    std::vector<int64_t> est(R);
-    dplan::plan_rounds(c.h_rows, R, dplan::kHistBins + 1, K, 1.2, lut.data(), est.data());
-    lsd = dplan::msd_too_skewed(est.data(), R, N);
+  std::vector<std::vector<uint64_t>> C;
+  if (!partition_top<uint32_t>(c, in, nullptr, n, C)) return hold.finish(false);
+  std::vector<uint8_t> lut(dplan::kTopDigits);
+  std::vector<int64_t> est(R);
+  dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
+  // one digit range would overload a rank: the LSD rounds from the untouched input
+  if (dplan::msd_too_skewed(est.data(), R, N)) return hold.finish(run_lsd(c, in, n, out, S, bits, !copy, self_rccl));
+  return hold.finish(run_digit_rounds<uint32_t>(c, dplan::digit_plan(C, lut.data(), K), out, nullptr, !copy, self_rccl,
+                                                bits));
+}
+
+bool sort_device_pairs(Ctx& c, const uint64_t* const* d_kin, const uint32_t* const* d_vin, const size_t* n_in,
+                       uint64_t* const* d_kout, uint32_t* const* d_vout, size_t* n_out, unsigned flags, int bits) {
+  const int R = (int)c.ranks.size();
+  const bool copy = (flags & kDistribCopy) != 0 || !c.distinct;
+  const bool self_rccl = (flags & kDistribSelfRccl) != 0 && !copy;
+  if (flags & kDistribLsd) {
+    set_error("distributed pair sort: the LSD rounds are for keys only");
+    return false;
   }
-  if (lsd) return finish(run_lsd(c, in, n, out, S, 8, !copy, self_rccl));
-  const int NB = R * K;
-  // 3. table partition of every rank: counts + scan, bucket starts to the
-  //    host, then the scatter (queued before the host waits for the starts)
-  for (auto& u : c.uniq)
-    if (!ok_hip(hipSetDevice(u->dev), "hipSetDevice") ||
-        !ok_hip(hipMemcpyAsync(u->lut.p, lut.data(), dplan::kHistBins, hipMemcpyHostToDevice, u->st), "H2D plan"))
-      return finish(false);
-  for (int r = 0; r < R; ++r) {
-    RankState& s = c.ranks[r];
-    if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !s.part.ensure(s.dev, std::max<uint64_t>(n[r], 1) * 4))
-      return finish(false);
-    const uint8_t* dl = static_cast<const uint8_t*>(s.d->lut.p);
-    if (n[r]) {
-      if (!ok_hip(partition_lut_u32(*s.d->ws, in[r], nullptr, n[r], dl, dplan::kLutShift, NB, s.bounds.u32(), s.d->st,
-                                    kPartCount),
-                  "partition counts") ||
-          !ok_hip(hipMemcpyAsync(c.h_bounds + (size_t)r * 256, s.bounds.p, NB * 4, hipMemcpyDeviceToHost, s.d->st),
-                  "D2H bucket starts") ||
-          !ok_hip(hipEventRecord(s.ev_bounds, s.d->st), "hipEventRecord") ||
-          !ok_hip(partition_lut_u32(*s.d->ws, in[r], s.part.u32(), n[r], dl, dplan::kLutShift, NB, nullptr, s.d->st,
-                                    kPartScatter),
-                  "partition scatter"))
-        return finish(false);
-    }
-    if (!ok_hip(hipEventRecord(s.ev_part, s.d->st), "hipEventRecord")) return finish(false);
-  }
-  std::vector<std::vector<uint64_t>> C(R, std::vector<uint64_t>(NB, 0));
-  for (int r = 0; r < R; ++r) {
-    if (!n[r]) continue;
-    if (!ok_hip(hipEventSynchronize(c.ranks[r].ev_bounds), "hipEventSynchronize")) return finish(false);
-    const uint32_t* b = c.h_bounds + (size_t)r * 256;
-    for (int j = 0; j < NB; ++j) C[r][j] = (j + 1 < NB ? (uint64_t)b[j + 1] : n[r]) - b[j];
-  }
-  dplan::MsdPlan p = dplan::msd_plan(C, K);
-  uint64_t round_max = 1;
-  for (int r = 0; r < R; ++r) {
-    RankState& s = c.ranks[r];
-    if (!s.recv.ensure(s.dev, std::max<uint64_t>(p.n_recv[r], 1) * 4) ||
-        !s.outb.ensure(s.dev, std::max<uint64_t>(p.n_recv[r], 1) * 4))
-      return finish(false);
-    for (int i = 0; i < K; ++i)
-      round_max = std::max(round_max, p.roff[(size_t)r * (K + 1) + i + 1] - p.roff[(size_t)r * (K + 1) + i]);
-  }
-  for (auto& u : c.uniq)
-    if (!u->tmp.ensure(u->dev, round_max * 4)) return finish(false);
-  // 4. every round's exchange, issued now on the communication streams
-  if (!comm_waits(c, &RankState::ev_part)) return finish(false);
-  std::vector<const uint32_t*> src(R);
-  std::vector<uint32_t*> dst(R);
-  for (int r = 0; r < R; ++r) {
-    src[r] = c.ranks[r].part.u32();
-    dst[r] = c.ranks[r].recv.u32();
-  }
-  for (int i = 0; i < K; ++i) {
-    if (!move_pieces(c, p.rounds[i], src, dst, !copy, self_rccl)) return finish(false);
-    for (int r = 0; r < R; ++r) {
-      RankState& s = c.ranks[r];
-      if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !ok_hip(hipEventRecord(s.ev_x[i], s.d->cs), "record"))
-        return finish(false);
-    }
-  }
-  // 5. each round sorted into its slice as soon as it has arrived
-  for (int i = 0; i < K; ++i)
-    for (int r = 0; r < R; ++r) {
-      RankState& s = c.ranks[r];
-      const uint64_t a = p.roff[(size_t)r * (K + 1) + i], z = p.roff[(size_t)r * (K + 1) + i + 1];
-      if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !ok_hip(hipStreamWaitEvent(s.d->st, s.ev_x[i], 0), "wait"))
-        return finish(false);
-      if (z == a) continue;
-      uint64_t lo = 0, hi = 0;
-      if (!dplan::group_range(lut.data(), i * R + r, &lo, &hi)) {
-        set_error("distributed sort: round without a key range");
-        return finish(false);
-      }
-      if (!ok_hip(sort_u32(*s.d->ws, s.recv.u32() + a, s.outb.u32() + a, s.d->tmp.u32(), z - a, 0,
-                           span_bits(lo, hi), bits, nullptr, s.d->st, (uint32_t)lo, true, hi - lo),
-                  "round sort"))
-        return finish(false);
-    }
-  // 6. the equal re-cut into the caller's shards
-  for (int r = 0; r < R; ++r) {
-    RankState& s = c.ranks[r];
-    if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !ok_hip(hipEventRecord(s.ev_done, s.d->st), "record"))
-      return finish(false);
-  }
-  if (!comm_waits(c, &RankState::ev_done)) return finish(false);
-  for (int r = 0; r < R; ++r) src[r] = c.ranks[r].outb.u32();
-  return finish(move_pieces(c, dplan::recut_pieces(p.n_recv), src, out, !copy, self_rccl));
+  if (!copy && !c.ensure_comms()) return false;
+  std::vector<uint64_t> n;
+  uint64_t N = 0;
+  if (!check_sizes(R, n_in, n, N, n_out)) return false;
+  Hold hold(c);
+  if (!hold.ok) return hold.finish(false);
+  if (N == 0) return hold.finish(true);
+  std::vector<const uint64_t*> kin(d_kin, d_kin + R);
+  std::vector<const uint32_t*> vin(d_vin, d_vin + R);
+  std::vector<uint64_t*> kout(d_kout, d_kout + R);
+  std::vector<uint32_t*> vout(d_vout, d_vout + R);
+  const int K = std::max(1, std::min(kMaxRounds, 256 / R));
+  std::vector<std::vector<uint64_t>> C;
+  if (!partition_top<uint64_t>(c, kin, &vin, n, C)) return hold.finish(false);
+  std::vector<uint8_t> lut(dplan::kTopDigits);
+  std::vector<int64_t> est(R);
+  dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
+  // no skew fallback (as pylibsort.distrib): a heavy digit range concentrates
+  // work on one rank, the result stays exact
+  return hold.finish(run_digit_rounds<uint64_t>(c, dplan::digit_plan(C, lut.data(), K), kout, &vout, !copy,
+                                                self_rccl, bits));
 }
 
 }  // namespace
@@ -585,6 +709,14 @@ bool distrib_sort_u32(const int* devices, int R, const uint32_t* const* d_in, co
   std::lock_guard<std::mutex> glk(g_dist_mu);
   Ctx* c = ctx_for(devices, R);
   return c && sort_device(*c, d_in, n_in, d_out, n_out, flags, bits);
+}
+
+bool distrib_sort_pairs_u64_u32(const int* devices, int R, const uint64_t* const* d_kin, const uint32_t* const* d_vin,
+                                const size_t* n_in, uint64_t* const* d_kout, uint32_t* const* d_vout, size_t* n_out,
+                                unsigned flags, int bits) {
+  std::lock_guard<std::mutex> glk(g_dist_mu);
+  Ctx* c = ctx_for(devices, R);
+  return c && sort_device_pairs(*c, d_kin, d_vin, n_in, d_kout, d_vout, n_out, flags, bits);
 }
 
 bool distrib_sort_host_u32(uint32_t* h, size_t len, const int* devices, int R, unsigned flags, int bits) {

@@ -91,21 +91,7 @@ inline void plan_rounds(const int64_t* H, int R, size_t ld, int K, double growth
   }
 }
 
-// [lo, hi) key range of the buckets with lut == code (false if none).
-inline bool group_range(const uint8_t* lut, int code, uint64_t* lo, uint64_t* hi) {
-  int first = -1, last = -1;
-  for (int b = 0; b < kHistBins; ++b)
-    if (lut[b] == code) {
-      if (first < 0) first = b;
-      last = b;
-    }
-  if (first < 0) return false;
-  *lo = (uint64_t)first << kLutShift;
-  *hi = (uint64_t)(last + 1) << kLutShift;
-  return true;
-}
-
-// Skew fallback of the range schedule (identical on every rank): a rank
+// Skew fallback of the digit rounds (identical on every rank): a rank
 // would receive more than max_imbalance * S (+ one tile) keys.
 inline bool msd_too_skewed(const int64_t* est, int R, uint64_t N, double max_imbalance = 1.5) {
   double hs = 0.0, mx = 0.0;
@@ -124,57 +110,6 @@ struct Piece {
   int src, dst;
   uint64_t src_off, dst_off, count;
 };
-
-// The range-round exchange.  C[r][j] = keys of rank r in partition bucket j
-// = round * R + dest (from its table partition's bucket starts).  Round i of
-// rank r receives, in source-rank order, C[s][i*R + r] keys from every s,
-// into recv[roff[r][i] ...); the pieces of round i are rounds[i].
-struct MsdPlan {
-  int R = 0, K = 0;
-  std::vector<uint64_t> send_start;             // [R][R*K]: bucket starts of rank r's partition
-  std::vector<uint64_t> roff;                   // [R][K+1]: round offsets of rank r's receive buffer
-  std::vector<std::vector<Piece>> rounds;       // [K]
-  std::vector<uint64_t> n_recv;                 // [R]
-};
-
-inline MsdPlan msd_plan(const std::vector<std::vector<uint64_t>>& C, int K) {
-  MsdPlan p;
-  const int R = (int)C.size();
-  p.R = R;
-  p.K = K;
-  const int NB = R * K;
-  p.send_start.assign((size_t)R * NB, 0);
-  for (int r = 0; r < R; ++r) {
-    uint64_t run = 0;
-    for (int j = 0; j < NB; ++j) {
-      p.send_start[(size_t)r * NB + j] = run;
-      run += C[r][j];
-    }
-  }
-  p.roff.assign((size_t)R * (K + 1), 0);
-  p.n_recv.assign(R, 0);
-  for (int r = 0; r < R; ++r) {
-    uint64_t run = 0;
-    for (int i = 0; i < K; ++i) {
-      p.roff[(size_t)r * (K + 1) + i] = run;
-      for (int s = 0; s < R; ++s) run += C[s][(size_t)i * R + r];
-    }
-    p.roff[(size_t)r * (K + 1) + K] = run;
-    p.n_recv[r] = run;
-  }
-  p.rounds.assign(K, {});
-  for (int i = 0; i < K; ++i) {
-    for (int d = 0; d < R; ++d) {
-      uint64_t at = p.roff[(size_t)d * (K + 1) + i];
-      for (int s = 0; s < R; ++s) {
-        const uint64_t m = C[s][(size_t)i * R + d];
-        if (m) p.rounds[i].push_back(Piece{s, d, p.send_start[(size_t)s * NB + (size_t)i * R + d], at, m});
-        at += m;
-      }
-    }
-  }
-  return p;
-}
 
 // Placement of the per-rank results (rank r holds n_have[r] keys, the
 // concatenation over ranks in rank order is the sorted array) into the equal

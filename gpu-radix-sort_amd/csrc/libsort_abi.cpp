@@ -1149,6 +1149,32 @@ LS_BOOL_ENTRY(libsortDistribSortU32, int nranks, const int* devices, const uint3
   return ok ? 1 : 0;
 }
 
+LS_BOOL_ENTRY(libsortDistribSortPairsU64U32, int nranks, const int* devices, const uint64_t* const* d_kin,
+              const uint32_t* const* d_vin, const size_t* n_in, uint64_t* const* d_kout, uint32_t* const* d_vout,
+              size_t* n_out, uint32_t flags) {
+  if (nranks < 1 || !devices || !d_kin || !d_vin || !n_in || !d_kout || !d_vout || !n_out) {
+    set_error("libsortDistribSortPairsU64U32: need nranks >= 1 and non-NULL tables");
+    return 0;
+  }
+  if (flags & ~(kDistribCopy | kDistribSelfRccl)) {
+    set_error("libsortDistribSortPairsU64U32: unknown flags (LSD rounds are for keys only)");
+    return 0;
+  }
+  int ndev = 0;
+  if (!hip_ok(hipGetDeviceCount(&ndev), "hipGetDeviceCount")) return 0;
+  for (int r = 0; r < nranks; ++r)
+    if (devices[r] < 0 || devices[r] >= ndev) {
+      set_error("libsortDistribSortPairsU64U32: device out of range");
+      return 0;
+    }
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  const bool ok = distrib_sort_pairs_u64_u32(devices, nranks, d_kin, d_vin, n_in, d_kout, d_vout, n_out, flags,
+                                             g_digit_bits.load());
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return ok ? 1 : 0;
+}
+
 LS_BOOL_ENTRY(libsortReleaseWorkspace, void) {
   distrib_release();
   release_all_workspaces();

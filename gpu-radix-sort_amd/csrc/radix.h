@@ -250,6 +250,11 @@ constexpr unsigned kDistribSelfRccl = 4u;  // a rank's own pieces through RCCL t
 // ceil(N/R); n_out[r] receives the count.  Synchronous.
 bool distrib_sort_u32(const int* devices, int R, const uint32_t* const* d_in, const size_t* n_in, uint32_t* const* d_out,
                       size_t* n_out, unsigned flags, int digit_bits);
+// (u64 key, u32 payload) pairs, stable (configs[4]): the top-digit rounds on
+// the key's top 8 bits; flags: kDistribCopy / kDistribSelfRccl.  Synchronous.
+bool distrib_sort_pairs_u64_u32(const int* devices, int R, const uint64_t* const* d_kin, const uint32_t* const* d_vin,
+                                const size_t* n_in, uint64_t* const* d_kout, uint32_t* const* d_vout, size_t* n_out,
+                                unsigned flags, int digit_bits);
 // Host-pointer form: h[0..len) is cut into R shards of ceil(len/R) keys,
 // sorted across the ranks' devices and copied back in place.
 bool distrib_sort_host_u32(uint32_t* h, size_t len, const int* devices, int R, unsigned flags, int digit_bits);

@@ -84,6 +84,8 @@ _SIGS = [
     ("libsortMergeU32", ctypes.c_int, [_vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp]),
     ("gpuDistribSort", ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_int]),
     ("libsortDistribSortU32", ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32]),
+    ("libsortDistribSortPairsU64U32", ctypes.c_int,
+     [ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32]),
     ("libsortDistribPlanDigits", ctypes.c_int,
      [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, _vp, _vp]),
     ("libsortPopulateDevice", ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_uint64, _vp]),

@@ -417,6 +417,36 @@ def distrib_sort_u32(shards, flags=0):
     return [o[:int(arr_nout[r])] for r, o in enumerate(outs)]
 
 
+def distrib_sort_pairs_u64_u32(key_shards, val_shards, flags=0):
+    """libsortDistribSortPairsU64U32: the single-process multi-GPU stable
+    sort of (uint64 key, uint32 payload) pairs (configs[4]).  Returns rank
+    r's (keys, payloads) shard of the sorted whole on shard r's device."""
+    R = len(key_shards)
+    if len(val_shards) != R:
+        raise ValueError("one payload shard per key shard")
+    devs = []
+    for i, (k, v) in enumerate(zip(key_shards, val_shards)):
+        _need(k, _U64, "key_shards[%d]" % i)
+        _need(v, _U32, "val_shards[%d]" % i)
+        if k.numel() != v.numel() or k.device != v.device:
+            raise ValueError("shard %d: keys and payloads differ in length or device" % i)
+        devs.append(k.device.index)
+    for d in sorted(set(devs)):
+        torch.cuda.synchronize(d)
+    N = sum(t.numel() for t in key_shards)
+    S = -(-N // R) if R else 0
+    ko = [torch.empty(max(S, 1), dtype=torch.int64, device=t.device) for t in key_shards]
+    vo = [torch.empty(max(S, 1), dtype=torch.int32, device=t.device) for t in key_shards]
+    P = ctypes.c_void_p * R
+    arr_nout = (ctypes.c_size_t * R)()
+    _check(_lib().libsortDistribSortPairsU64U32(R, (ctypes.c_int * R)(*devs), P(*[t.data_ptr() for t in key_shards]),
+                                                P(*[t.data_ptr() for t in val_shards]),
+                                                (ctypes.c_size_t * R)(*[t.numel() for t in key_shards]),
+                                                P(*[t.data_ptr() for t in ko]), P(*[t.data_ptr() for t in vo]),
+                                                arr_nout, flags), "libsortDistribSortPairsU64U32")
+    return [k[:int(arr_nout[r])] for r, k in enumerate(ko)], [v[:int(arr_nout[r])] for r, v in enumerate(vo)]
+
+
 def populate_u32(n, first=0, device=None, out=None):
     """Elements [first, first+n) of the reference populateInput stream (fresh
     process), generated on the device."""

@@ -254,7 +254,7 @@ LIBSORT_API bool gpuDistribSort(uint32_t* h_in, size_t len, int ngpu);
  * copies; RCCL refuses two ranks on one GPU).  Synchronous: returns when every
  * device is done.  flags: LIBSORT_DISTRIB_LSD runs the reference's BSP LSD
  * rounds (8-bit digits, bucket-major / rank-minor re-cut after every round)
- * instead of the default range rounds; LIBSORT_DISTRIB_COPY exchanges with
+ * instead of the default top-digit rounds; LIBSORT_DISTRIB_COPY exchanges with
  * peer copies (hipMemcpyPeerAsync) instead of RCCL; LIBSORT_DISTRIB_SELF_RCCL
  * sends a rank's own pieces through RCCL too (tests). */
 #define LIBSORT_DISTRIB_LSD 1u
@@ -263,6 +263,18 @@ LIBSORT_API bool gpuDistribSort(uint32_t* h_in, size_t len, int ngpu);
 LIBSORT_API bool libsortDistribSortU32(int nranks, const int* devices, const uint32_t* const* d_in,
                                        const size_t* n_in, uint32_t* const* d_out, size_t* n_out,
                                        uint32_t flags);
+
+/* The same engine for (uint64 key, uint32 payload) pairs, stable (BASELINE
+ * configs[4]: 2^31 pairs over 8 GPUs): rank r's shard (d_kin[r], d_vin[r],
+ * n_in[r] pairs on devices[r]) -> (d_kout[r], d_vout[r]) = pairs [r*S,
+ * (r+1)*S) of the stably sorted whole (payloads of equal keys keep the input
+ * order: shard 0 first).  The top-digit rounds on the key's top 8 bits with a
+ * stable pair sort per round.  flags: LIBSORT_DISTRIB_COPY /
+ * LIBSORT_DISTRIB_SELF_RCCL (not _LSD).  Synchronous. */
+LIBSORT_API bool libsortDistribSortPairsU64U32(int nranks, const int* devices, const uint64_t* const* d_kin,
+                                               const uint32_t* const* d_vin, const size_t* n_in,
+                                               uint64_t* const* d_kout, uint32_t* const* d_vout, size_t* n_out,
+                                               uint32_t flags);
 
 /* Host plan of the multi-GPU top-digit rounds (pylibsort.distrib and the
  * single-process engine above both run it; csrc/distrib_plan.h).

@@ -1,9 +1,10 @@
 // distrib_sim.cpp -- CPU simulation of the single-process multi-GPU sort
 // (gpu-radix-sort_amd/csrc/distrib.cpp) over R host "ranks": the SAME host
-// arithmetic (csrc/distrib_plan.h: round plan, exchange pieces, LSD gather
-// tables, equal re-cut) drives plain host copies, with the oracle's CPU
-// restatements as the local operations.  Checked against the oracle
-// (oracle/oracle.cpp, compiled in): the range rounds give std::sort cut into
+// arithmetic (csrc/distrib_plan.h: digit plan, exchange pieces, the round
+// sorts' piece tables, LSD gather tables, equal re-cut) drives plain host
+// copies, with the oracle's CPU restatements as the local operations.
+// Checked against the oracle (oracle/oracle.cpp, compiled in): the top-digit
+// rounds give std::sort cut into
 // ceil(N/R) shards; the LSD rounds give, shard for shard, the reference BSP
 // driver's output (oracle_distrib_bsp_u32: distrib.go:90-179).  Built and run
 // with AddressSanitizer + UBSan by tests/test_distrib_plan_cpu.py.
@@ -48,46 +49,62 @@ static void apply(const std::vector<Piece>& ps, const std::vector<Vec>& src, std
   for (const Piece& p : ps) memcpy(dst[p.dst].data() + p.dst_off, src[p.src].data() + p.src_off, p.count * 4);
 }
 
-// range rounds: full (unsampled) histograms, table partition, rounds, re-cut
+// top-digit rounds: exact digit counts, stable partition by key >> 24, the
+// plan, the rounds (the receiver's piece table checked piece by piece: inside
+// the round, the right digit, covering the round exactly), re-cut
 static bool run_msd(const Vec& x, int R, int K, double growth) {
   std::vector<Vec> in = split(x, R);
-  std::vector<int64_t> H((size_t)R * kHistBins, 0);
-  for (int r = 0; r < R; ++r)
-    for (uint32_t k : in[r]) H[(size_t)r * kHistBins + (k >> kLutShift)]++;
-  std::vector<uint8_t> lut(kHistBins);
+  std::vector<std::vector<uint64_t>> C(R, std::vector<uint64_t>(kTopDigits, 0));
+  std::vector<Vec> part(R);
+  for (int r = 0; r < R; ++r) {
+    for (uint32_t k : in[r]) C[r][k >> kTopShift]++;
+    std::vector<uint64_t> at(kTopDigits + 1, 0);
+    for (int g = 0; g < kTopDigits; ++g) at[g + 1] = at[g] + C[r][g];
+    part[r].resize(in[r].size());
+    for (uint32_t k : in[r]) part[r][at[k >> kTopShift]++] = k;  // stable
+  }
+  std::vector<uint8_t> lut(kTopDigits);
   std::vector<int64_t> est(R);
-  plan_rounds(H.data(), R, kHistBins, K, growth, lut.data(), est.data());
+  plan_digit_rounds(C, K, growth, lut.data(), est.data());
   uint64_t tot = 0;
   for (int r = 0; r < R; ++r) tot += (uint64_t)est[r];
   CHECK(tot == x.size(), "est sum %llu != %zu", (unsigned long long)tot, x.size());
-  for (int b = 1; b < kHistBins; ++b) {  // monotone (round, rank) groups
-    const int c0 = lut[b - 1] % R * K + lut[b - 1] / R, c1 = lut[b] % R * K + lut[b] / R;
-    CHECK(c1 >= c0, "plan not monotone at %d", b);
+  for (int g = 1; g < kTopDigits; ++g) {  // monotone (rank, round) groups
+    const int c0 = lut[g - 1] % R * K + lut[g - 1] / R, c1 = lut[g] % R * K + lut[g] / R;
+    CHECK(c1 >= c0, "plan not monotone at %d", g);
   }
-  const int NB = R * K;
-  std::vector<Vec> part(R);
-  std::vector<std::vector<uint64_t>> C(R, std::vector<uint64_t>(NB, 0));
-  for (int r = 0; r < R; ++r) {
-    for (uint32_t k : in[r]) C[r][lut[k >> kLutShift]]++;
-    std::vector<uint64_t> at(NB + 1, 0);
-    for (int j = 0; j < NB; ++j) at[j + 1] = at[j] + C[r][j];
-    part[r].resize(in[r].size());
-    for (uint32_t k : in[r]) part[r][at[lut[k >> kLutShift]]++] = k;  // stable
-  }
-  MsdPlan p = msd_plan(C, K);
+  DigitPlan p = digit_plan(C, lut.data(), K);
   std::vector<Vec> recv(R), out(R);
   for (int r = 0; r < R; ++r) {
     recv[r].assign(p.n_recv[r], 0xdeadbeefu);
     out[r].assign(p.n_recv[r], 0);
+    CHECK((int64_t)p.n_recv[r] == est[r], "rank %d receives %llu, plan says %lld", r,
+          (unsigned long long)p.n_recv[r], (long long)est[r]);
   }
   for (int i = 0; i < K; ++i) {
     apply(p.rounds[i], part, recv);
     for (int r = 0; r < R; ++r) {
       const uint64_t a = p.roff[(size_t)r * (K + 1) + i], z = p.roff[(size_t)r * (K + 1) + i + 1];
-      if (z == a) continue;
-      uint64_t lo, hi;
-      CHECK(group_range(lut.data(), i * R + r, &lo, &hi), "round %d rank %d has keys but no range", i, r);
-      for (uint64_t q = a; q < z; ++q) CHECK(recv[r][q] >= lo && recv[r][q] < hi, "key outside its round range");
+      const size_t q = (size_t)r * K + i;
+      const int lo = p.lo[(size_t)i * R + r], hi = p.hi[(size_t)i * R + r];
+      std::vector<char> seen(z - a, 0);
+      uint64_t covered = 0;
+      uint32_t prev_seg = 0;
+      for (size_t j = 0; j < p.p_off[q].size(); ++j) {
+        const uint64_t o = p.p_off[q][j], m = p.p_len[q][j];
+        const uint32_t sg = p.p_seg[q][j];
+        CHECK(sg >= prev_seg && (int)sg < hi - lo, "piece segment %u out of order / range", sg);
+        prev_seg = sg;
+        CHECK(o + m <= z - a, "piece past its round");
+        for (uint64_t t = 0; t < m; ++t) {
+          CHECK(!seen[o + t], "pieces overlap");
+          seen[o + t] = 1;
+          CHECK((int)(recv[r][a + o + t] >> kTopShift) == lo + (int)sg, "key of digit %u in segment %u",
+                recv[r][a + o + t] >> kTopShift, sg);
+        }
+        covered += m;
+      }
+      CHECK(covered == z - a, "pieces cover %llu of %llu", (unsigned long long)covered, (unsigned long long)(z - a));
       std::copy(recv[r].begin() + a, recv[r].begin() + z, out[r].begin() + a);
       std::sort(out[r].begin() + a, out[r].begin() + z);
     }
@@ -184,8 +201,9 @@ int main() {
           ++cases;
         }
       }
-  // R * K = 256 partition buckets (the table limit)
+  // R * K = 256 groups (the table limit): most digits a group of their own
   run_msd(make("wide", 100003, 5), 2, 128, 1.2);
+  run_msd(make("pcg", 300007, 6), 64, 4, 1.2);
   ++cases;
   run_lsd(make("pcg", 4099, 0), 4, 4);
   ++cases;

@@ -137,3 +137,72 @@ def test_reference_size_over_rccl(D, golden):
     h = hashlib.sha256(out.cpu().numpy().view(np.uint32).tobytes()).hexdigest()[:16]
     assert h == g["sha256_prefix"][str(n)]["sorted"]
     assert pylibsort.lib().libsortDeviceErrors() == 0
+
+
+def _pair_case(oracle, case):
+    rng = np.random.default_rng(len(case))
+    if case == "c5":            # configs[4]'s pairs: key = draw 2i << 32 | draw 2i+1
+        w = oracle.pcg(2 * ((1 << 20) + 333), first=3).astype(np.uint64)
+        return (w[0::2] << np.uint64(32)) | w[1::2]
+    if case == "ties":          # equal keys spread over every rank (stability across ranks)
+        return rng.integers(0, 1 << 12, 300007, dtype=np.uint64) * np.uint64(0x0010000100000001)
+    if case == "onekey":
+        return np.full(100003, 0x123456789ABCDEF0, dtype=np.uint64)
+    return rng.integers(0, 1 << 63, 5, dtype=np.uint64)  # tiny: empty shards at 8 ranks
+
+
+@pytest.mark.parametrize("R", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("case", ["c5", "ties", "onekey", "tiny"])
+def test_pairs_engine(D, oracle_mod, bits, R, case):
+    """configs[4] behind the C ABI (libsortDistribSortPairsU64U32): one RCCL
+    rank with every piece through RCCL, or R ranks sharing the GPU; the
+    concatenated shards equal std::stable_sort by key of (key, input index)
+    -- payloads of equal keys in input order across ranks -- and each shard
+    holds ceil(N/R) pairs."""
+    k = _pair_case(oracle_mod, case)
+    n = k.size
+    v = np.arange(n, dtype=np.uint32)
+    S = -(-n // R)
+    ks = [torch.from_numpy(k[r * S:(r + 1) * S].view(np.int64).copy()).cuda() for r in range(R)]
+    vs = [torch.from_numpy(v[r * S:(r + 1) * S].view(np.int32).copy()).cuda() for r in range(R)]
+    ko, vo = D.distrib_sort_pairs_u64_u32(ks, vs, SELF_RCCL if R == 1 else COPY)
+    rk, rv = oracle_mod.stable_sort_kv64(k, v)
+    assert [t.numel() for t in ko] == [max(0, min(n, (r + 1) * S) - r * S) for r in range(R)]
+    np.testing.assert_array_equal(np.concatenate([t.cpu().numpy().view(np.uint64) for t in ko]), rk)
+    np.testing.assert_array_equal(np.concatenate([t.cpu().numpy().view(np.uint32) for t in vo]), rv)
+
+
+def test_pairs_engine_rejects_lsd(D):
+    import pylibsort
+    k = [torch.zeros(10, dtype=torch.int64, device="cuda")]
+    v = [torch.zeros(10, dtype=torch.int32, device="cuda")]
+    with pytest.raises(RuntimeError):
+        D.distrib_sort_pairs_u64_u32(k, v, LSD)
+    assert "keys only" in pylibsort.last_error()
+
+
+@pytest.mark.slow
+def test_config5_share_over_rccl(D):
+    """configs[4]'s per-GPU share (2^28 pairs) through the C-ABI pair engine
+    over one RCCL rank (every piece through RCCL): the oracle's sha256 of the
+    stably sorted keys and payloads (tests/golden/big_golden.json)."""
+    import hashlib
+    import json
+    import pathlib
+    big = json.loads((pathlib.Path(__file__).with_name("golden") / "big_golden.json").read_text())
+    n = 1 << 28
+    want = big["c5_pairs"][str(n)]
+    w = D.populate_u32(2 * n).view(n, 2).to(torch.int64)
+    keys = (w[:, 0] << 32) | (w[:, 1] & 0xFFFFFFFF)
+    del w
+    vals = torch.arange(n, dtype=torch.int64, device="cuda").to(torch.int32)
+    ko, vo = D.distrib_sort_pairs_u64_u32([keys], [vals], SELF_RCCL)
+    del keys, vals
+
+    def sha(t, dt):
+        h = hashlib.sha256()
+        for i in range(0, t.numel(), 1 << 26):
+            h.update(t[i:i + (1 << 26)].cpu().numpy().view(dt).tobytes())
+        return h.hexdigest()
+    assert sha(ko[0], np.uint64) == want["keys"]
+    assert sha(vo[0], np.uint32) == want["payloads"]
