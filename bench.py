@@ -38,6 +38,9 @@ for p in (str(ROOT), str(ROOT / "gpu-radix-sort_amd")):
         sys.path.insert(0, p)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+# N>1 engine when --engine auto (the faster of the two
+# on the one-GPU schedule measurement at 2^29 keys per rank)
+DEFAULT_ENGINE = "torch"
 PASS_KERNELS = "tilepass,onesweep,downsweep"  # the roofline kernel candidates (timed-region events)
 
 
@@ -52,6 +55,10 @@ def parse():
     ap.add_argument("--schedule", default="auto", choices=["auto", "msd", "msdz", "lsd"],
                     help="auto: msdz (delta-coded exchange) at 2 GPUs, msd otherwise")
     ap.add_argument("--rounds", type=int, default=4, help="msd exchange rounds (pylibsort.distrib.ROUNDS)")
+    ap.add_argument("--engine", default="auto", choices=["auto", "torch", "cabi"],
+                    help="N>1: torch = one process per GPU (pylibsort.distrib over torch.distributed); cabi = rank "
+                         "0 drives every GPU through the C ABI (libsortDistribSortU32 / ...PairsU64U32, the "
+                         "single-process RCCL engine C and Go callers bind); auto = DEFAULT_ENGINE")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=28,
                     help="keys of the providedCpu baseline sample (BASELINE.md section 3: 2^28)")
@@ -175,8 +182,37 @@ def main():
         tmp = torch.empty_like(keys)
     torch.cuda.synchronize()
     ops = distrib.HipOps() if world > 1 else None
+    engine = DEFAULT_ENGINE if args.engine == "auto" else args.engine
+    cabi = world > 1 and engine == "cabi"
+    shards = vshards = None
+    if cabi:
+        # one process drives every GPU through the C ABI (what a C or Go
+        # caller binds); the other ranks keep the barriers and the max-over-
+        # ranks timing.  Shard r = the same keys rank r holds in torch mode.
+        del keys
+        keys = None
+        devs = [0] * world if rehearsal else list(range(world))
+        if rank == 0:
+            shards, vshards = [], []
+            for rr, dv in enumerate(devs):
+                if pairs:
+                    w = D.populate_u32(2 * n, first=rr * 2 * n, device=dv).view(n, 2).to(torch.int64)
+                    shards.append((w[:, 0] << 32) | (w[:, 1] & 0xFFFFFFFF))
+                    del w
+                    vshards.append(torch.arange(rr * n, (rr + 1) * n, dtype=torch.int64,
+                                                device=torch.device("cuda", dv)).to(torch.int32))
+                else:
+                    shards.append(D.populate_u32(n, first=rr * n, device=dv))
+            for dv in sorted(set(devs)):
+                torch.cuda.synchronize(dv)
 
     def step():
+        if cabi:
+            if rank != 0:
+                return None
+            if pairs:
+                return D.distrib_sort_pairs_u64_u32(shards, vshards)
+            return D.distrib_sort_u32(shards)
         if pairs:
             if world == 1:
                 return D.sort_pairs_u64_u32(keys, vals, out_keys=out, out_vals=outv, tmp_keys=tmp, tmp_vals=tmpv)
@@ -245,7 +281,9 @@ def main():
 
     # verification outside the timed region: sorted + same multiset (checksums)
     verified = None
-    if not args.no_verify:
+    if not args.no_verify and cabi:
+        verified = verify_cabi(torch, shards, res, vshards) if rank == 0 else None
+    elif not args.no_verify:
         verified = verify(torch, dist, world, keys, res, vals)
 
     # N>1: the same distributed sort with 8-bit local digits (all ranks take
@@ -295,6 +333,15 @@ def main():
             # kernel trace, so `frac` can be re-derived from profiles/
             if args.workload == "c2" and world == 1 and args.keys_log2 == 28 and ds_name == "tilepass":
                 roofline.update(committed_profile(bytes_per_launch))
+        if roofline is not None and world == 1 and not pairs:
+            roofline["step"] = step_roofline(n, args.digit_bits, ms_per_step, kern)
+        bs = kern.get("bucketsort")
+        if bs:
+            ach = 8.0 * bs["keys_per_launch"] / (bs["avg_us"] * 1e-6) / 1e9 if not pairs else None
+            if ach:
+                bs["achieved_gbps"] = round(ach, 1)
+                bs["frac"] = round(ach / HBM_PEAK_GBPS, 4)
+                bs["bytes_per_key"] = 8.0
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not pairs:
             cpu = cpu_baseline_leg(torch, pylibsort, keys, out, args.cpu_sample_log2)
@@ -320,6 +367,8 @@ def main():
             variants["digit8"] = {"ms_per_step": round(ms8, 4), "value": round(n / (ms8 * 1e-3) / 1e9, 3),
                                   "note": "same sort with 8-bit digits (4 passes, configs[2] digit width); output "
                                           "checked equal to the 4-bit sort"}
+        if world == 1 and not args.no_variants and args.workload == "c2":
+            variants["lsd"] = lsd_variant(torch, pylibsort, D, keys, out, tmp, max(5, args.steps // 2))
         if world == 1 and not args.no_variants and not args.no_legs and args.workload == "c2" and args.keys_log2 == 28:
             # the other single-GPU configurations, each with its own live
             # per-kernel timings (never `value`)
@@ -333,11 +382,14 @@ def main():
             sname = args.schedule
             if sname == "auto":
                 sname = "msdz" if world == 2 else "msd"
-            if pairs:
+            if pairs or cabi:
                 sname = "msd"
-            sched = (", %s schedule%s, %d rounds, over %d GPUs (RCCL point-to-point)"
-                     % (sname, " (delta-coded exchange)" if sname == "msdz" else "", args.rounds, world)
+            sched = (", %s schedule (top-digit rounds)%s, %d rounds, over %d GPUs (RCCL point-to-point)"
+                     % (sname, " with delta-coded exchange" if sname == "msdz" else "", args.rounds, world)
                      if sname != "lsd" else ", lsd schedule over %d GPUs (RCCL alltoallv)" % world)
+            sched += (", C-ABI engine (one process drives every GPU: libsortDistribSort%s)"
+                      % ("PairsU64U32" if pairs else "U32") if cabi else
+                      ", torch engine (one process per GPU, pylibsort.distrib)")
         if pairs:
             metric, unit, dtype = "Gpairs/sec (u64 key, u32 payload) stable sort", "Gpairs/s", "u64+u32"
             workload = "configs[4]: 2^%d (u64 key, u32 payload) pairs per GPU, %d-bit digits, stable sort%s" % (
@@ -407,6 +459,51 @@ def committed_profile(bytes_per_launch):
     except (OSError, ValueError, KeyError):
         pass
     return out
+
+
+def step_roofline(n, digit_bits, ms_per_step, kern):
+    """The whole N=1 step against HBM: the bytes the
+    hybrid sort actually moves per step -- one count read (4 B/key), 16 /
+    digit_bits digit passes and the bucket sort (read + write, 8 B/key each)
+    -- and SURVEY.md section 8(d)'s LSD-equivalent figure (32 / digit_bits
+    passes x 8 B/key: 64 B/key at 4-bit digits), each / ms_per_step."""
+    passes = 16 // digit_bits if "bucketsort" in kern else 32 // digit_bits
+    actual = n * (4.0 + 8.0 * passes + (8.0 if "bucketsort" in kern else 0.0))
+    lsd_eq = n * 8.0 * (32 // digit_bits)
+    t = ms_per_step * 1e-3
+    return {"actual_bytes_per_key": actual / n, "actual_gbps": round(actual / t / 1e9, 1),
+            "actual_frac": round(actual / t / 1e9 / HBM_PEAK_GBPS, 4),
+            "lsd_equivalent_bytes_per_key": lsd_eq / n, "lsd_equivalent_gbps": round(lsd_eq / t / 1e9, 1),
+            "lsd_equivalent_frac": round(lsd_eq / t / 1e9 / HBM_PEAK_GBPS, 4),
+            "note": "whole step (ms_per_step): actual = count read + %d digit passes%s; lsd_equivalent = "
+                    "SURVEY 8(d) %d LSD passes x 8 B/key" % (passes, " + bucket sort" if "bucketsort" in kern else "",
+                                                            32 // digit_bits)}
+
+
+def lsd_variant(torch, pylibsort, D, keys, out, tmp, reps):
+    """The reference-shaped LSB sort (libsortSetHybrid(0): 32 / digit-bits
+    LSD passes, what north_star names), timed beside the hybrid line and
+    checked equal to its output."""
+    ref = out.clone()
+    prev = pylibsort.setHybrid("off")
+    try:
+        for _ in range(2):
+            D.sort_keys_u32(keys, out=out, tmp=tmp)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(out, ref))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            D.sort_keys_u32(keys, out=out, tmp=tmp)
+        torch.cuda.synchronize()
+        ms = 1e3 * (time.perf_counter() - t0) / reps
+    finally:
+        pylibsort.setHybrid(prev)
+    if not same:
+        raise RuntimeError("LSD variant disagrees with the hybrid sort")
+    return {"ms_per_step": round(ms, 4), "value": round(keys.numel() / (ms * 1e-3) / 1e9, 3),
+            "verified_equal_to_value_sort": same,
+            "note": "libsortSetHybrid(0): the LSB radix sort of north_star (%d LSD passes at the line's digit width), "
+                    "output checked equal to the hybrid sort's" % (32 // pylibsort.getDigitBits())}
 
 
 def _cpu_model():
@@ -543,6 +640,51 @@ def host_abi_leg(torch, pylibsort, keys, sorted_keys, calls=3):
             "value": round(keys.numel() / t / 1e9, 3), "unit": "Gkeys/s", "calls": calls,
             "note": "PCIe-inclusive (H2D + sort + D2H, median of %d calls), never `value`; "
                     "output checked equal to the device-resident sort" % calls}
+
+
+def verify_cabi(torch, shards, res, vshards=None):
+    """The C-ABI engine's result on rank 0: every output shard sorted (and,
+    pairs, stable), the shards in order across their edges, the same
+    multiset as the input shards (checksums over all devices)."""
+    def csum(ts, vs=None):
+        acc = [0, 0, 0]
+        for i, t in enumerate(ts):
+            if vs is None:
+                k = t.to(torch.int64) & 0xFFFFFFFF
+                acc[0] += int(k.sum())
+                acc[1] += int((k * k % 1000000007).sum())
+            else:
+                v = vs[i].to(torch.int64) & 0xFFFFFFFF
+                acc[0] += int((((t & 0xFFFFFF) * 1000003 + (t >> 40) * 7 + v) % 1000000007).sum())
+                acc[1] += int(v.sum())
+            acc[2] += t.numel()
+        return acc
+    if vshards is None:
+        outs = res
+        ok = csum(shards) == csum(outs)
+        prev = None
+        for t in outs:
+            if t.numel() == 0:
+                continue
+            k = t.to(torch.int64) & 0xFFFFFFFF
+            ok = ok and bool((k[1:] >= k[:-1]).all()) and (prev is None or prev <= int(k[0]))
+            prev = int(k[-1])
+        return ok
+    ko, vo = res
+    ok = csum(shards, vshards) == csum(ko, vo)
+    prev = None
+    flip = -(1 << 63)
+    for k, v in zip(ko, vo):
+        if k.numel() == 0:
+            continue
+        s_ = torch.bitwise_xor(k, torch.tensor(flip, dtype=torch.int64, device=k.device))
+        vv = v.to(torch.int64) & 0xFFFFFFFF
+        eq = s_[1:] == s_[:-1]
+        ok = ok and bool((s_[1:] >= s_[:-1]).all()) and bool((vv[1:][eq] > vv[:-1][eq]).all())
+        first = (int(s_[0]), int(vv[0]))
+        ok = ok and (prev is None or prev[0] < first[0] or (prev[0] == first[0] and prev[1] < first[1]))
+        prev = (int(s_[-1]), int(vv[-1]))
+    return ok
 
 
 def verify(torch, dist, world, keys, res, vals=None):

@@ -219,6 +219,33 @@ def test_bench_self_launch_rehearsal_world8():
     assert line["config"]["global_keys"] == 8 << 20
 
 
+@pytest.mark.parametrize("world,pairs", [(2, False), (8, False), (3, True)])
+def test_bench_cabi_engine_rehearsal(world, pairs):
+    """`bench.py --gpus N --engine cabi`: rank 0 drives all N ranks through
+    the C ABI (libsortDistribSortU32 / libsortDistribSortPairsU64U32; here
+    all on the one GPU, device-copy exchanges) while the other ranks keep the
+    barriers; the result is verified on rank 0 and relayed."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import json
+    import os
+    import pathlib
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["BENCH_REHEARSAL"] = "1"
+    cmd = [sys.executable, str(root / "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
+           "--keys-log2", "20", "--engine", "cabi", "--no-variants"] + (["--workload", "c5"] if pairs else [])
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(root))
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == world and line["verified"] is True
+    assert "C-ABI engine" in line["config"]["workload"]
+
+
 def test_bench_single_gpu_line_contract():
     """bench.py at N=1 (small steps): one JSON line with the driver's keys,
     the roofline object (live per-launch pass time), a verified sort, the

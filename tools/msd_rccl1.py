@@ -43,8 +43,12 @@ def main():
         # 2 warm-up + MSD_PROFILE timed steps (kernel totals / steps = the
         # GPU work of one step, by kernel)
         reps = int(os.environ["MSD_PROFILE"])
+        cabi = os.environ.get("MSD_ENGINE") == "cabi"
         for _ in range(2 + reps):
-            distrib.sort_msd(keys, ops, rounds=4)
+            if cabi:
+                D.distrib_sort_u32([keys])
+            else:
+                distrib.sort_msd(keys, ops, rounds=4)
         torch.cuda.synchronize()
         print({"msd_profile_steps": reps, "warmup": 2})
         dist.destroy_process_group()
@@ -58,6 +62,10 @@ def main():
         res["msd_rounds%d_selfcopy_ms" % K] = timed(lambda: distrib.sort_msd(keys, ops, rounds=K))
         res["msd_rounds%d_minus_selfcopy_ms" % K] = res["msd_rounds%d_selfcopy_ms" % K] - res["selfcopy_all_keys_ms"]
         res["msd_rounds%d_via_rccl_ms" % K] = timed(lambda: distrib.sort_msd(keys, ops, rounds=K, self_local=False))
+    # the C-ABI engine (libsortDistribSortU32) on the same keys: one rank over
+    # a one-device RCCL communicator, self pieces as device copies
+    res["cabi_rounds4_selfcopy_ms"] = timed(lambda: D.distrib_sort_u32([keys]))
+    res["cabi_rounds4_minus_selfcopy_ms"] = res["cabi_rounds4_selfcopy_ms"] - res["selfcopy_all_keys_ms"]
     if os.environ.get("MSD_DIGIT8", "1") == "1":
         pylibsort.setDigitBits(8)
         res["digit8_msd_rounds4_selfcopy_ms"] = timed(lambda: distrib.sort_msd(keys, ops, rounds=4))
