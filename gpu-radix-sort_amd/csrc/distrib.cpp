@@ -294,15 +294,24 @@ bool move_pieces(Ctx& c, const std::vector<dplan::Piece>& ps, const std::vector<
     }
   }
   if (net.empty()) return true;
+  // RCCL point-to-point messages are cut into chunks of at most 256 MiB:
+  // measured on the one-GPU box (RCCL 2.26.6, torch's build), a 2 GiB
+  // self-send of u64 keys arrived intact only up to its first 1 GiB
+  // (tools/debug_pairs.py); both sides post the chunks in the same order
+  constexpr uint64_t kChunkBytes = 256ull << 20;
+  const uint64_t chunk = kChunkBytes / esize;
   if (!g_rccl.ok(g_rccl.groupStart(), "ncclGroupStart")) return false;
   bool ok = true;
   for (const dplan::Piece* p : net) {
     RankState& a = c.ranks[p->src];
     RankState& b = c.ranks[p->dst];
-    ok = ok && g_rccl.ok(g_rccl.send(at(src[p->src], p->src_off), p->count, dt, p->dst, c.comms[p->src], a.d->cs),
-                         "ncclSend") &&
-         g_rccl.ok(g_rccl.recv(atw(dst[p->dst], p->dst_off), p->count, dt, p->src, c.comms[p->dst], b.d->cs),
-                   "ncclRecv");
+    for (uint64_t o = 0; ok && o < p->count; o += chunk) {
+      const uint64_t m = std::min(chunk, p->count - o);
+      ok = g_rccl.ok(g_rccl.send(at(src[p->src], p->src_off + o), m, dt, p->dst, c.comms[p->src], a.d->cs),
+                     "ncclSend") &&
+           g_rccl.ok(g_rccl.recv(atw(dst[p->dst], p->dst_off + o), m, dt, p->src, c.comms[p->dst], b.d->cs),
+                     "ncclRecv");
+    }
   }
   return g_rccl.ok(g_rccl.groupEnd(), "ncclGroupEnd") && ok;
 }

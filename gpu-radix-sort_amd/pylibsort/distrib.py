@@ -349,6 +349,17 @@ class _Works:
             w.wait()
 
 
+# RCCL point-to-point messages are posted in chunks of at most 256 MiB (a
+# 2 GiB self-send arrived intact only up to its first 1 GiB on RCCL 2.26.6,
+# tools/debug_pairs.py; the C engine cuts its messages the same way)
+_P2P_CHUNK_BYTES = 256 << 20
+
+
+def _p2p_chunks(t):
+    step = max(1, _P2P_CHUNK_BYTES // t.element_size())
+    return [t[i:i + step] for i in range(0, t.numel(), step)] if t.numel() > step else [t]
+
+
 def _alltoallv_into(recv, send, send_counts, recv_counts, group, async_op=False, self_local=True):
     """alltoallv of contiguous slices into `recv` (pieces in source-rank
     order) as one batch of point-to-point sends/receives (one RCCL group);
@@ -380,9 +391,9 @@ def _alltoallv_into(recv, send, send_counts, recv_counts, group, async_op=False,
                 recv[int(ro[me]):int(ro[me + 1])].copy_(send[int(so[me]):int(so[me + 1])])
             continue
         if ss[i]:
-            ops.append(dist.P2POp(dist.isend, send[int(so[i]):int(so[i + 1])], peer(i), group))
+            ops += [dist.P2POp(dist.isend, c, peer(i), group) for c in _p2p_chunks(send[int(so[i]):int(so[i + 1])])]
         if rs[j]:
-            ops.append(dist.P2POp(dist.irecv, recv[int(ro[j]):int(ro[j + 1])], peer(j), group))
+            ops += [dist.P2POp(dist.irecv, c, peer(j), group) for c in _p2p_chunks(recv[int(ro[j]):int(ro[j + 1])])]
     if not ops:
         return None
     works = _Works(dist.batch_isend_irecv(ops))
@@ -719,9 +730,9 @@ def _exchange_pieces(sends, recvs, group):
     for k in range(R):  # k = 0: a self piece (sort_msdz self_local=False)
         i, j = (me + k) % R, (me - k) % R
         if i in hs:
-            ops_.append(dist.P2POp(dist.isend, hs[i], peer(i), group))
+            ops_ += [dist.P2POp(dist.isend, c, peer(i), group) for c in _p2p_chunks(hs[i])]
         if j in hr:
-            ops_.append(dist.P2POp(dist.irecv, hr[j], peer(j), group))
+            ops_ += [dist.P2POp(dist.irecv, c, peer(j), group) for c in _p2p_chunks(hr[j])]
     if not ops_:
         return None
     works = _Works(dist.batch_isend_irecv(ops_))
