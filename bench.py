@@ -282,7 +282,7 @@ def main():
     # verification outside the timed region: sorted + same multiset (checksums)
     verified = None
     if not args.no_verify and cabi:
-        verified = verify_cabi(torch, shards, res, vshards) if rank == 0 else None
+        verified = verify_cabi(torch, shards, res, vshards if pairs else None) if rank == 0 else None
     elif not args.no_verify:
         verified = verify(torch, dist, world, keys, res, vals)
 
