@@ -819,6 +819,11 @@ __global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ key
   using VT = typename VecOf<K>::type;
   constexpr int PER = VecOf<K>::n;
   const bool vec = valid == TILE && (reinterpret_cast<uintptr_t>(keys + tile_base) % 16) == 0;
+  // TAB tiles start anywhere (a piece of a multi-GPU round's receive buffer,
+  // a hybrid child): their keys are read as the 16-byte words covering them,
+  // masked to the tile (the words stay inside the allocation: it ends on a
+  // 4-byte boundary, and device allocations are 256-byte granular)
+  const bool cover = TAB && !vec && valid > 0;
   VT v[ITEMS / PER];
   if (vec) {
     // the tile's loads go out before the table staging and the barrier
@@ -838,6 +843,18 @@ __global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ key
     for (int j = 0; j < ITEMS / PER; ++j)
 #pragma unroll
       for (int c = 0; c < PER; ++c) atomicAdd(&s_h[cp][op(vec_elem(v[j], c))], 1u);
+  } else if (cover) {
+    const uint64_t a0 = tile_base & ~(uint64_t)(PER - 1), end = tile_base + valid;
+    const VT* vp = reinterpret_cast<const VT*>(keys + a0);
+    const uint32_t nv = (uint32_t)((end - a0 + PER - 1) / PER);
+    for (uint32_t q = tid; q < nv; q += BLOCK) {
+      const VT x = load_count_vec(&vp[q]);
+#pragma unroll
+      for (int c = 0; c < PER; ++c) {
+        const uint64_t i = a0 + (uint64_t)q * PER + c;
+        if (i >= tile_base && i < end) atomicAdd(&s_h[cp][op(vec_elem(x, c))], 1u);
+      }
+    }
   } else {
     for (uint32_t i = tid; i < valid; i += BLOCK) atomicAdd(&s_h[cp][op(keys[tile_base + i])], 1u);
   }
@@ -2998,7 +3015,10 @@ constexpr size_t kHybMinKeys = 1ull << 27;
 // 64-bit keys: the LSD sort needs 8 (16) passes, so the hybrid pays from 2^25
 // keys (tools/hyb_sizes.py: (u64, u32) pairs 2^24 0.91x, 2^25 1.41x, 2^26 2.14x)
 constexpr size_t kHybMinKeys64 = 1ull << 25;
-constexpr size_t kHybMaxKeys = (1ull << 28) + (1ull << 24);
+// (u32 buckets of the top 16 bits: up to ~8.3K keys on average in the
+// 512-thread class; 64-bit keys keep the 2^28 + 2^24 bound of round 2)
+constexpr size_t kHybMaxKeys = (1ull << 29) + (1ull << 23);
+constexpr size_t kHybMaxKeys64 = (1ull << 28) + (1ull << 24);
 // Range sorts (W bits of key - lo, W < 32: 7 LSD passes at the 8-GPU rounds'
 // W = 27, buckets of W - 16 = 11 bits) gain from fewer keys: the round sorts of
 // configs[3]'s schedule (tools/round_sorts.py, 2^29 keys per rank in 4 rounds)
@@ -3037,6 +3057,7 @@ struct HybPieces {
   uint32_t np, nseg;
   uint32_t tiles;       // T0 = sum over pieces of ceil(len / TILE)
   int depths;           // digit passes (the bucket sort covers W - BITS * depths bits)
+  double fill;          // populated segments / nseg (sizes the bucket blocks)
 };
 
 // Depth 0 of a pre-partitioned input: tile t of piece p (first tile w <= t <
@@ -3091,16 +3112,21 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   // of the top digits) are populated, each by n * 2^(W-16) / span keys on
   // average (range rounds of the multi-GPU sort: a W = 27 round spans ~0.8 of
   // 2^27, which the full-width shares would take for skew)
-  const double fill = span ? (double)span / std::ldexp(1.0, W) : 1.0;
+  const double fill = pc ? pc->fill : span ? (double)span / std::ldexp(1.0, W) : 1.0;
   const double mean = (double)n / (NB * fill);
   const double need = mean + 3.5 * std::sqrt(mean);
-  const int cls = need <= 256.0 * 9 ? 0 : need <= 256.0 * 13 ? 1 : need <= 256.0 * 17 ? 2 : 3;
-  static constexpr int kItems1[4] = {9, 13, 17, 19};
+  // class 4 (32-bit keys): 512-thread blocks of 17 keys per thread for
+  // buckets of ~8K keys (full sorts up to 2^29 + 2^23 keys)
+  const int cls = need <= 256.0 * 9 ? 0 : need <= 256.0 * 13 ? 1 : need <= 256.0 * 17 ? 2 :
+                  (need <= 256.0 * 19 || sizeof(K) == 8) ? 3 : 4;
+  static constexpr int kItems1[5] = {9, 13, 17, 19, 34};  // per 256 threads
   // the two blocks' slots (64-bit keys: 512-thread blocks, keys per thread
   // rounded up)
   constexpr int BB = sizeof(K) == 8 ? LIBSORT_BUCKET64_BLOCK : 256;
-  const uint32_t cap1 = (uint32_t)BB * (((uint32_t)kItems1[cls] * 256u + BB - 1) / BB);
-  const uint32_t cap = (uint32_t)BB * (((uint32_t)(kItems1[cls] + 6) * 256u + BB - 1) / BB);
+  const int BBc = cls == 4 ? 512 : BB;
+  const int extra = cls == 4 ? 12 : 6;  // second block: 6 (12) x 256 more slots
+  const uint32_t cap1 = (uint32_t)BBc * (((uint32_t)kItems1[cls] * 256u + BBc - 1) / BBc);
+  const uint32_t cap = (uint32_t)BBc * (((uint32_t)(kItems1[cls] + extra) * 256u + BBc - 1) / BBc);
   const uint32_t T0 = pc ? pc->tiles : (uint32_t)((n + TILE - 1) / TILE);
   // segments of depth k (each child has at most one partial tile)
   auto nseg_at = [&](int k) { return nseg0 << (BITS * k); };
@@ -3279,12 +3305,23 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   LS_BS(I, NB, ctr + 9, NB, nullptr, ctr + 8, olist);      \
   LS_TRY(hipGetLastError());                               \
   LS_BS(I + 6, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr)
+#define LS_BS512(I, G, NBP, CAPN, IL, OV, OL)                                                                 \
+  hipLaunchKernelGGL((k_bucket_sort<BITS, 512, (I), Op, K, V, FIXB>), dim3(G), dim3(512), 0, st, out, out, vout, vout, \
+                     bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
     switch (cls) {
       case 0: LS_BS2(9); break;
       case 1: LS_BS2(13); break;
       case 2: LS_BS2(17); break;
-      default: LS_BS2(19); break;
+      case 3: LS_BS2(19); break;
+      default:
+        if constexpr (sizeof(K) == 4) {
+          LS_BS512(17, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
+          LS_TRY(hipGetLastError());
+          LS_BS512(23, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+        }
+        break;
     }
+#undef LS_BS512
 #undef LS_BS2
 #undef LS_BS
     LS_TRY(hipGetLastError());
@@ -3381,14 +3418,26 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   }
   if (total != n || keep.size() > 65535) return hipErrorInvalidValue;
   const uint32_t K = (uint32_t)keep.size();
-  // digit passes: the fewest that bring the mean bucket (n / (nseg * RADIX^d)
-  // keys, values uniform in each segment) to <= 4096 keys, within `bits`
+  // segment sizes: the largest sets the digit passes, the populated ones the
+  // bucket blocks' size class (a round's last group may span many empty
+  // digits)
+  std::vector<uint64_t> segsize(nseg, 0);
+  for (size_t p : keep) segsize[seg[p]] += len[p];
+  uint64_t maxseg = 0;
+  uint32_t npop = 0;
+  for (uint64_t v : segsize) {
+    maxseg = std::max(maxseg, v);
+    npop += v ? 1u : 0u;
+  }
+  // digit passes: the fewest that bring the largest segment's mean bucket
+  // (its keys / RADIX^d, values uniform within a segment) to <= 8320 keys
+  // (the 512 x 17-key block holds that + 3.5 sigma), within `bits`
   const int hyb = hybrid_mode_for(st);
   int depths = 0;
   if (hyb == 2 ? n >= 1024 : (hyb == 1 && n >= kPiecesMinKeys)) {
     for (int d = 1; d * digit_bits <= bits; ++d) {
       depths = d;
-      if ((double)n / std::ldexp((double)nseg, d * digit_bits) <= 4096.0) break;
+      if ((double)maxseg / std::ldexp(1.0, d * digit_bits) <= 8320.0) break;
     }
     if (((uint64_t)nseg << (digit_bits * depths)) > (1ull << 22)) depths = 0;
   }
@@ -3404,8 +3453,6 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   uint64_t* hg = ws.seg_host + g64;
   uint32_t* ct0 = h32 + 4 * (size_t)K;
   uint32_t* cst = ct0 + nseg + 1;
-  std::vector<uint64_t> segsize(nseg, 0);
-  for (uint32_t i = 0; i < K; ++i) segsize[seg[keep[i]]] += len[keep[i]];
   {
     uint64_t run = 0;
     for (uint32_t s = 0; s < nseg; ++s) {
@@ -3434,7 +3481,7 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
                         st));
   LS_TRY(hipEventRecord(ws.seg_evt, st));
   if (depths > 0) {
-    HybPieces pc{reinterpret_cast<const uint32_t*>(ws.seg_dev), K, nseg, tile, depths};
+    HybPieces pc{reinterpret_cast<const uint32_t*>(ws.seg_dev), K, nseg, tile, depths, (double)npop / nseg};
     bool handled = false;
     NoValue* nv = nullptr;
     if (digit_bits == 4)
@@ -3483,7 +3530,7 @@ hipError_t sort_64_hybrid_or_lsd(Workspace& ws, const uint64_t* kin, uint64_t* k
                                  V* vout, V* vtmp, size_t n, int lo, int hi, int digit_bits, hipStream_t st) {
   const int hyb = hybrid_mode_for(st);
   if (lo == 0 && hi == 64 && (digit_bits == 8 || digit_bits == 4) &&
-      ((hyb == 1 && n >= kHybMinKeys64 && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
+      ((hyb == 1 && n >= kHybMinKeys64 && n <= kHybMaxKeys64) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys64)) &&
       (get_algorithm() == 0 || get_algorithm() == 3) && (const void*)kin != (const void*)ktmp) {
     bool handled = false;
     if (digit_bits == 8)

@@ -498,3 +498,28 @@ def test_graph_capture_skips_the_host_waits(dev, oracle_mod):
         np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
     finally:
         pylibsort.setHybrid(prev)
+
+
+@pytest.mark.parametrize("n", [(1 << 29) + 12345, 400000007])
+def test_hybrid_auto_2pow29_class(dev, n):
+    """Full sorts of 2^28 + 2^24 .. 2^29 + 2^23 keys take the hybrid with
+    the 512-thread bucket blocks (buckets of ~6-8K keys; configs[3]'s 2^29
+    keys per GPU): equal to the LSD sort of the same keys (libsortSetHybrid
+    off), which the parity suite pins bit-exact, and one bucket-sort launch
+    pair ran."""
+    import pylibsort
+    x = dev.populate_u32(n, first=n)
+    out = torch.empty_like(x)
+    tmp = torch.empty_like(x)
+    got, nbs, npass = _sort_counting(dev, x, out=out, tmp=tmp)
+    assert nbs == 2 and npass == 4, (nbs, npass)  # 4 digit passes + the bucket sort, no fallback
+    ref = torch.empty_like(x)
+    prev = pylibsort.setHybrid("off")
+    try:
+        dev.sort_keys_u32(x, out=ref, tmp=tmp)
+    finally:
+        pylibsort.setHybrid(prev)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    del x, out, tmp, ref
+    torch.cuda.empty_cache()
