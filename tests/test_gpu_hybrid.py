@@ -501,7 +501,7 @@ def test_graph_capture_skips_the_host_waits(dev, oracle_mod):
 
 
 @pytest.mark.parametrize("n", [(1 << 29) + 12345, 400000007])
-def test_hybrid_auto_2pow29_class(dev, n):
+def test_hybrid_auto_2pow29_class(dev, bits, n):
     """Full sorts of 2^28 + 2^24 .. 2^29 + 2^23 keys take the hybrid with
     the 512-thread bucket blocks (buckets of ~6-8K keys; configs[3]'s 2^29
     keys per GPU): equal to the LSD sort of the same keys (libsortSetHybrid
@@ -512,7 +512,7 @@ def test_hybrid_auto_2pow29_class(dev, n):
     out = torch.empty_like(x)
     tmp = torch.empty_like(x)
     got, nbs, npass = _sort_counting(dev, x, out=out, tmp=tmp)
-    assert nbs == 2 and npass == 4, (nbs, npass)  # 4 digit passes + the bucket sort, no fallback
+    assert nbs == 2 and npass == 16 // bits, (nbs, npass)  # 16 / bits digit passes + the bucket sort, no fallback
     ref = torch.empty_like(x)
     prev = pylibsort.setHybrid("off")
     try:
