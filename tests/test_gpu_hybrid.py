@@ -512,7 +512,7 @@ def test_hybrid_auto_2pow29_class(dev, bits, n):
     out = torch.empty_like(x)
     tmp = torch.empty_like(x)
     got, nbs, npass = _sort_counting(dev, x, out=out, tmp=tmp)
-    assert nbs == 2 and npass == 16 // bits, (nbs, npass)  # 16 / bits digit passes + the bucket sort, no fallback
+    assert nbs == 1 and npass == 16 // bits, (nbs, npass)  # 16 / bits digit passes + the bucket sort, no fallback
     ref = torch.empty_like(x)
     prev = pylibsort.setHybrid("off")
     try:
