@@ -820,9 +820,11 @@ __global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ key
   constexpr int PER = VecOf<K>::n;
   const bool vec = valid == TILE && (reinterpret_cast<uintptr_t>(keys + tile_base) % 16) == 0;
   // TAB tiles start anywhere (a piece of a multi-GPU round's receive buffer,
-  // a hybrid child): their keys are read as the 16-byte words covering them,
-  // masked to the tile (the words stay inside the allocation: it ends on a
-  // 4-byte boundary, and device allocations are 256-byte granular)
+  // a hybrid child): their keys are read as the 16-byte-ALIGNED words
+  // covering them (aligned in absolute address, not relative to `keys`,
+  // which may itself sit off a 16-byte boundary), masked to the tile.  Those
+  // words never leave the allocation: device allocations start and end on
+  // 16-byte (in fact page) boundaries.
   const bool cover = TAB && !vec && valid > 0;
   VT v[ITEMS / PER];
   if (vec) {
@@ -844,15 +846,17 @@ __global__ __launch_bounds__(BLOCK) void k_tile_counts(const K* __restrict__ key
 #pragma unroll
       for (int c = 0; c < PER; ++c) atomicAdd(&s_h[cp][op(vec_elem(v[j], c))], 1u);
   } else if (cover) {
-    const uint64_t a0 = tile_base & ~(uint64_t)(PER - 1), end = tile_base + valid;
-    const VT* vp = reinterpret_cast<const VT*>(keys + a0);
-    const uint32_t nv = (uint32_t)((end - a0 + PER - 1) / PER);
+    // mis: keys of the first aligned word before the tile
+    const uint32_t mis = (uint32_t)((reinterpret_cast<uintptr_t>(keys + tile_base) & 15u) / sizeof(K));
+    const VT* vp = reinterpret_cast<const VT*>(keys + tile_base - mis);
+    const uint32_t span = valid + mis;
+    const uint32_t nv = (span + PER - 1) / PER;
     for (uint32_t q = tid; q < nv; q += BLOCK) {
       const VT x = load_count_vec(&vp[q]);
 #pragma unroll
       for (int c = 0; c < PER; ++c) {
-        const uint64_t i = a0 + (uint64_t)q * PER + c;
-        if (i >= tile_base && i < end) atomicAdd(&s_h[cp][op(vec_elem(x, c))], 1u);
+        const uint32_t i = q * PER + c;
+        if (i >= mis && i < span) atomicAdd(&s_h[cp][op(vec_elem(x, c))], 1u);
       }
     }
   } else {
