@@ -419,18 +419,46 @@ def _interval_counts(starts, lens, S, R):
     return out
 
 
-def _rebalance(sorted_keys, n_all, ops, group):
-    """Shift keys between ranks so rank r holds global positions [r*S, (r+1)*S)."""
-    R = dist.get_world_size(group)
-    r = dist.get_rank(group)
-    N = int(n_all.sum())
-    S, _ = shard_cut(N, R)
-    offs = np.concatenate([[0], np.cumsum(n_all)[:-1]])
-    M = np.stack([_interval_counts(np.array([offs[s]]), np.array([n_all[s]]), S, R)
-                  for s in range(R)])                       # M[s, d]: keys s sends to d
-    if np.array_equal(np.diag(M), n_all):
-        return sorted_keys  # identical decision on every rank: nothing moves
-    return _alltoallv(sorted_keys, M[r], M[:, r], ops, group)
+def _placement(n_have, R, r):
+    """The equal re-cut (the reference's ceil(N/R) chunks, distrib.go:113)
+    without a copy of the data that stays: rank r's sorted keys hold global
+    positions [G, G + m) (G = keys of the ranks before it), its final shard
+    is [r*S, r*S + L).  One buffer B covers both ranges; the round sorts write
+    straight into it at `off`, and only the overhangs move: sends[d] = (a, b)
+    of B for rank d, recvs[s] = (a, b) of B from rank s (disjoint from the
+    sorted data), view = (a, b) of B that is the shard.  (Sending the whole
+    sorted shard through all_to_all_single would copy it, self part
+    included, at RCCL's ~360 GB/s.)"""
+    n_have = np.asarray(n_have, dtype=np.int64)
+    N = int(n_have.sum())
+    S, cut = shard_cut(N, R)
+    G = np.concatenate([[0], np.cumsum(n_have)])
+    g0, g1 = int(G[r]), int(G[r + 1])
+    s0, s1 = cut[r]
+    lo, hi = min(g0, s0), max(g1, s1)
+    sends, recvs = {}, {}
+    for d in range(R):
+        if d == r:
+            continue
+        x, y = max(g0, cut[d][0]), min(g1, cut[d][1])
+        if y > x:
+            sends[d] = (x - lo, y - lo)
+        x, y = max(int(G[d]), s0), min(int(G[d + 1]), s1)
+        if y > x:
+            recvs[d] = (x - lo, y - lo)
+    return hi - lo, g0 - lo, sends, recvs, (s0 - lo, s1 - lo)
+
+
+def _place(bufs, pl, group):
+    """Moves the overhangs of the placement `pl` (see _placement) for every
+    buffer in `bufs` (keys, and payloads for pairs) and returns the shards."""
+    _, _, sends, recvs, (v0, v1) = pl
+    works = [_exchange_pieces({d: B[a:b] for d, (a, b) in sends.items()},
+                              {s: B[a:b] for s, (a, b) in recvs.items()}, group) for B in bufs]
+    for w in works:
+        if w is not None:
+            w.wait()
+    return [B[v0:v1] for B in bufs]
 
 
 def sort_lsd(keys, ops, group=None, width=8):
@@ -675,7 +703,9 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None
     recv_tot = np.array([int(g.CB[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
     roff = np.concatenate([[0], np.cumsum(recv_tot)])
     recv = ops.empty(int(roff[-1]))
-    out = ops.empty(int(roff[-1]))
+    pl = _placement(est, R, r)                                # the rounds sort straight into the final buffer
+    B = ops.empty(pl[0])
+    out = B[pl[1]:pl[1] + int(roff[-1])]
     # every round's exchange issued now (RCCL's stream runs them back to
     # back); the rank's own piece is a local copy
     works = []
@@ -704,7 +734,7 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None
         _mark(trace, "round %d" % i)
     if not balance:
         return out
-    res = _rebalance(out, est, ops, group)
+    res = _place([B], pl, group)[0]
     _mark(trace, "rebalance")
     return res
 
@@ -796,7 +826,9 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
     b = g.start[r][g.lo]                                       # where group j's keys start in this rank's partition
     recv_tot = np.array([int(C[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
     roff = np.concatenate([[0], np.cumsum(recv_tot)])
-    out = ops.empty(int(roff[-1]))
+    pl = _placement(est, R, r)                                # merges write straight into the final buffer
+    B = ops.empty(pl[0])
+    out = B[pl[1]:pl[1] + int(roff[-1])]
     srt = ops.empty(n)
     cuda = keys.is_cuda
     mg = torch.zeros(R * K, dtype=torch.int32, device=keys.device)
@@ -874,27 +906,9 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
     _mark(trace, "exchanged and merged")
     if not balance:
         return out
-    n_recv = np.array([int(C[:, d::R].sum()) for d in range(R)], dtype=np.int64)
-    res = _rebalance(out, n_recv, ops, group)
+    res = _place([B], pl, group)[0]
     _mark(trace, "rebalance")
     return res
-
-
-def _rebalance_pairs(keys, vals, n_all, ops, group):
-    """_rebalance for (key, payload) pairs: both arrays take the same splits."""
-    R = dist.get_world_size(group)
-    r = dist.get_rank(group)
-    N = int(n_all.sum())
-    S, _ = shard_cut(N, R)
-    offs = np.concatenate([[0], np.cumsum(n_all)[:-1]])
-    M = np.stack([_interval_counts(np.array([offs[s]]), np.array([n_all[s]]), S, R) for s in range(R)])
-    if np.array_equal(np.diag(M), n_all):
-        return keys, vals
-    rk = ops.empty64(int(M[:, r].sum()))
-    rv = ops.empty(int(M[:, r].sum()))
-    _alltoallv_into(rk, keys, M[r], M[:, r], group)
-    _alltoallv_into(rv, vals, M[r], M[:, r], group)
-    return rk, rv
 
 
 def distrib_sort_pairs(keys, vals, ops=None, group=None, rounds=None):
@@ -926,7 +940,10 @@ def _sort_pairs_rounds(keys, vals, ops, group, rounds, self_local=True):
     recv_tot = np.array([int(g.CB[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
     roff = np.concatenate([[0], np.cumsum(recv_tot)])
     T = int(roff[-1])
-    rk, rv, ok_, ov = ops.empty64(T), ops.empty(T), ops.empty64(T), ops.empty(T)
+    rk, rv = ops.empty64(T), ops.empty(T)
+    pl = _placement(est, R, r)                                # round sorts straight into the final buffers
+    BK, BV = ops.empty64(pl[0]), ops.empty(pl[0])
+    ok_, ov = BK[pl[1]:pl[1] + T], BV[pl[1]:pl[1] + T]
     works = []
     for i in range(K):
         ks, kr, vs, vr = {}, {}, {}, {}
@@ -951,7 +968,8 @@ def _sort_pairs_rounds(keys, vals, ops, group, rounds, self_local=True):
         a, z = int(roff[i]), int(roff[i + 1])
         if z > a:
             ops.sort_pairs(rk[a:z], rv[a:z], out_keys=ok_[a:z], out_vals=ov[a:z])
-    return _rebalance_pairs(ok_, ov, est, ops, group)
+    k_, v_ = _place([BK, BV], pl, group)
+    return k_, v_
 
 
 def distrib_sort(keys, ops=None, group=None, schedule="auto", **kw):
