@@ -585,6 +585,9 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
         return false;
     }
   }
+  // rounds inside the rank's output shard are sorted straight into it; the
+  // others into outb, whose pieces move afterwards (dplan::place_rounds)
+  const dplan::Placement pl = dplan::place_rounds(p.roff, p.n_recv, K_);
   // each round sorted on arrival, one host thread per device
   const bool sorted = per_device(c, [&](DevState& d) {
     for (int i = 0; i < K_; ++i)
@@ -595,30 +598,31 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
         if (!ok_hip(hipStreamWaitEvent(d.st, s.ev_x[i], 0), "wait")) return false;
         if (z == a) continue;
         hipError_t e;
+        const size_t q = (size_t)r * K_ + i;
+        K* kdst = pl.direct[q] ? out[r] + pl.out_off[q] : static_cast<K*>(s.outb.p) + a;
+        uint32_t* vdst = pairs ? (pl.direct[q] ? (*vout)[r] + pl.out_off[q] : s.ov.u32() + a) : nullptr;
         if constexpr (sizeof(K) == 4) {
-          const size_t q = (size_t)r * K_ + i;
-          e = sort_pieces_u32(*d.ws, s.recv.u32() + a, s.outb.u32() + a, d.tmp.u32(), z - a, p.p_off[q].data(),
+          e = sort_pieces_u32(*d.ws, s.recv.u32() + a, kdst, d.tmp.u32(), z - a, p.p_off[q].data(),
                               p.p_len[q].data(), p.p_seg[q].data(), p.p_off[q].size(),
                               (uint32_t)(p.hi[(size_t)i * R + r] - p.lo[(size_t)i * R + r]), dplan::kTopShift, bits,
                               d.st);
         } else {
-          e = sort_pairs_u64_u32(*d.ws, static_cast<uint64_t*>(s.recv.p) + a, s.rv.u32() + a,
-                                 static_cast<uint64_t*>(s.outb.p) + a, s.ov.u32() + a, static_cast<uint64_t*>(d.tmp.p),
-                                 d.tmpv.u32(), z - a, 0, 64, bits, d.st);
+          e = sort_pairs_u64_u32(*d.ws, static_cast<uint64_t*>(s.recv.p) + a, s.rv.u32() + a, kdst, vdst,
+                                 static_cast<uint64_t*>(d.tmp.p), d.tmpv.u32(), z - a, 0, 64, bits, d.st);
         }
         if (!ok_hip(e, "round sort")) return false;
       }
     return true;
   });
   if (!sorted) return false;
-  // the equal re-cut into the caller's shards
+  // the equal re-cut: the pieces of the rounds that were not sorted in place
   for (int r = 0; r < R; ++r) {
     RankState& s = c.ranks[r];
     if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !ok_hip(hipEventRecord(s.ev_done, s.d->st), "record"))
       return false;
   }
   if (!comm_waits(c, &RankState::ev_done)) return false;
-  const std::vector<dplan::Piece> cut = dplan::recut_pieces(p.n_recv);
+  const std::vector<dplan::Piece>& cut = pl.moves;
   for (int r = 0; r < R; ++r) {
     src[r] = c.ranks[r].outb.p;
     dst[r] = out[r];

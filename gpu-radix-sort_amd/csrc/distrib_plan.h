@@ -234,6 +234,51 @@ inline DigitPlan digit_plan(const std::vector<std::vector<uint64_t>>& C, const u
   return p;
 }
 
+// The equal re-cut without copying what stays.  Rank r's sorted rounds hold
+// global positions [G_r + roff[r][i], G_r + roff[r][i+1]) (G_r = keys of the
+// ranks before it); its output shard is [min(N, r*S), min(N, (r+1)*S)).  A
+// round that lies inside the shard is sorted straight into the output at
+// out_off (direct); any other round is sorted into the rank's scratch at its
+// roff, and `moves` carries its pieces to the shards they belong to (src_off
+// in the rank's local order, dst_off in the destination shard).
+struct Placement {
+  std::vector<char> direct;       // [R][K]
+  std::vector<uint64_t> out_off;  // [R][K]
+  std::vector<Piece> moves;
+};
+
+inline Placement place_rounds(const std::vector<uint64_t>& roff, const std::vector<uint64_t>& n_recv, int K) {
+  const int R = (int)n_recv.size();
+  uint64_t N = 0;
+  for (uint64_t x : n_recv) N += x;
+  const uint64_t S = shard_size(N, R);
+  auto cut = [&](int d) { return std::min<uint64_t>(N, (uint64_t)d * S); };
+  Placement pl;
+  pl.direct.assign((size_t)R * K, 0);
+  pl.out_off.assign((size_t)R * K, 0);
+  uint64_t G = 0;
+  for (int r = 0; r < R; ++r) {
+    const uint64_t s0 = cut(r), s1 = (r == R - 1) ? N : cut(r + 1);
+    for (int i = 0; i < K; ++i) {
+      const uint64_t a = G + roff[(size_t)r * (K + 1) + i], b = G + roff[(size_t)r * (K + 1) + i + 1];
+      if (b == a) continue;
+      const size_t q = (size_t)r * K + i;
+      if (a >= s0 && b <= s1) {
+        pl.direct[q] = 1;
+        pl.out_off[q] = a - s0;
+        continue;
+      }
+      for (int d = 0; d < R; ++d) {
+        const uint64_t d0 = cut(d), d1 = (d == R - 1) ? N : cut(d + 1);
+        const uint64_t x = std::max(a, d0), y = std::min(b, d1);
+        if (y > x) pl.moves.push_back(Piece{r, d, x - G, x - d0, y - x});
+      }
+    }
+    G += n_recv[r];
+  }
+  return pl;
+}
+
 // ---------------------------------------------------------------------------
 // BSP LSD round ("lsd", the reference's semantics)
 // ---------------------------------------------------------------------------

@@ -81,6 +81,10 @@ static bool run_msd(const Vec& x, int R, int K, double growth) {
     CHECK((int64_t)p.n_recv[r] == est[r], "rank %d receives %llu, plan says %lld", r,
           (unsigned long long)p.n_recv[r], (long long)est[r]);
   }
+  std::vector<Vec> fin(R);
+  const uint64_t S = shard_size(x.size(), R);
+  for (int r = 0; r < R; ++r) fin[r].assign(std::min<uint64_t>(S, x.size() - std::min<uint64_t>(x.size(), r * S)), 0);
+  Placement pl = place_rounds(p.roff, p.n_recv, K);
   for (int i = 0; i < K; ++i) {
     apply(p.rounds[i], part, recv);
     for (int r = 0; r < R; ++r) {
@@ -105,14 +109,17 @@ static bool run_msd(const Vec& x, int R, int K, double growth) {
         covered += m;
       }
       CHECK(covered == z - a, "pieces cover %llu of %llu", (unsigned long long)covered, (unsigned long long)(z - a));
-      std::copy(recv[r].begin() + a, recv[r].begin() + z, out[r].begin() + a);
-      std::sort(out[r].begin() + a, out[r].begin() + z);
+      // the round sorted straight into the output shard (direct), or into
+      // the scratch and moved below
+      const size_t q2 = (size_t)r * K + i;
+      Vec& dst = pl.direct[q2] ? fin[r] : out[r];
+      const uint64_t at = pl.direct[q2] ? pl.out_off[q2] : a;
+      CHECK(at + (z - a) <= dst.size(), "round %d of rank %d placed past its buffer", i, r);
+      std::copy(recv[r].begin() + a, recv[r].begin() + z, dst.begin() + at);
+      std::sort(dst.begin() + at, dst.begin() + at + (z - a));
     }
   }
-  std::vector<Vec> fin(R);
-  const uint64_t S = shard_size(x.size(), R);
-  for (int r = 0; r < R; ++r) fin[r].assign(std::min<uint64_t>(S, x.size() - std::min<uint64_t>(x.size(), r * S)), 0);
-  apply(recut_pieces(p.n_recv), out, fin);
+  apply(pl.moves, out, fin);
   Vec want(x);
   std::sort(want.begin(), want.end());
   std::vector<Vec> ws = split(want, R);
