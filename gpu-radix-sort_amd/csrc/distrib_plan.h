@@ -111,31 +111,6 @@ struct Piece {
   uint64_t src_off, dst_off, count;
 };
 
-// Placement of the per-rank results (rank r holds n_have[r] keys, the
-// concatenation over ranks in rank order is the sorted array) into the equal
-// re-cut: rank d ends with global positions [d*S, (d+1)*S).
-inline std::vector<Piece> recut_pieces(const std::vector<uint64_t>& n_have) {
-  const int R = (int)n_have.size();
-  uint64_t N = 0;
-  for (uint64_t x : n_have) N += x;
-  const uint64_t S = shard_size(N, R);
-  std::vector<Piece> out;
-  uint64_t g = 0;
-  for (int s = 0; s < R; ++s) {
-    uint64_t a = g, left = n_have[s];
-    while (left) {
-      const int d = S ? (int)std::min<uint64_t>(a / S, (uint64_t)R - 1) : R - 1;
-      const uint64_t hi = (d == R - 1) ? a + left : std::min(a + left, (uint64_t)(d + 1) * S);
-      const uint64_t m = hi - a;
-      out.push_back(Piece{s, d, a - g, a - (uint64_t)d * S, m});
-      a += m;
-      left -= m;
-    }
-    g += n_have[s];
-  }
-  return out;
-}
-
 // ---------------------------------------------------------------------------
 // top-digit rounds ("msd"): the exchange is planned on the EXACT counts of the
 // top 8 key bits, which every rank has from its partition pass (a stable
