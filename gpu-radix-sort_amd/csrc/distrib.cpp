@@ -48,6 +48,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -463,33 +464,6 @@ struct Hold {
   }
 };
 
-// fn(device) for every distinct device, each on a host thread of its own
-// (the round sorts wait on the host for small read-backs; one device's waits
-// must not hold another device's issue -- ADVICE r02); inline for one device.
-// A failing thread's message is re-raised on the caller's thread.
-template <typename F>
-bool per_device(Ctx& c, F&& fn) {
-  if (c.uniq.size() == 1) return ok_hip(hipSetDevice(c.uniq[0]->dev), "hipSetDevice") && fn(*c.uniq[0]);
-  std::vector<std::string> err(c.uniq.size());
-  std::vector<char> good(c.uniq.size(), 1);
-  std::vector<std::thread> th;
-  for (size_t u = 0; u < c.uniq.size(); ++u)
-    th.emplace_back([&, u] {
-      DevState& d = *c.uniq[u];
-      if (!ok_hip(hipSetDevice(d.dev), "hipSetDevice") || !fn(d)) {
-        good[u] = 0;
-        err[u] = last_error();
-      }
-    });
-  for (auto& t : th) t.join();
-  for (size_t u = 0; u < good.size(); ++u)
-    if (!good[u]) {
-      set_error(err[u]);
-      return false;
-    }
-  return true;
-}
-
 // Stable partition of every rank's keys (and payloads) by their top 8 bits
 // into part (pv): the count call (per-tile counts + column scan) and the
 // 256 bucket starts' copy to the host are queued first, then the scatter, so
@@ -575,45 +549,106 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
     vsrc[r] = c.ranks[r].pv.p;
     vdst[r] = c.ranks[r].rv.p;
   }
-  for (int i = 0; i < K_; ++i) {
-    if (!move_pieces(c, p.rounds[i], src, dst, sizeof(K), use_rccl, self_rccl) ||
-        (pairs && !move_pieces(c, p.rounds[i], vsrc, vdst, 4, use_rccl, self_rccl)))
-      return false;
-    for (int r = 0; r < R; ++r) {
-      RankState& s = c.ranks[r];
-      if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !ok_hip(hipEventRecord(s.ev_x[i], s.d->cs), "record"))
-        return false;
-    }
-  }
   // rounds inside the rank's output shard are sorted straight into it; the
   // others into outb, whose pieces move afterwards (dplan::place_rounds)
   const dplan::Placement pl = dplan::place_rounds(p.roff, p.n_recv, K_);
-  // each round sorted on arrival, one host thread per device
-  const bool sorted = per_device(c, [&](DevState& d) {
-    for (int i = 0; i < K_; ++i)
-      for (int r = 0; r < R; ++r) {
-        RankState& s = c.ranks[r];
-        if (s.d != &d) continue;
-        const uint64_t a = p.roff[(size_t)r * (K_ + 1) + i], z = p.roff[(size_t)r * (K_ + 1) + i + 1];
-        if (!ok_hip(hipStreamWaitEvent(d.st, s.ev_x[i], 0), "wait")) return false;
-        if (z == a) continue;
-        hipError_t e;
-        const size_t q = (size_t)r * K_ + i;
-        K* kdst = pl.direct[q] ? out[r] + pl.out_off[q] : static_cast<K*>(s.outb.p) + a;
-        uint32_t* vdst = pairs ? (pl.direct[q] ? (*vout)[r] + pl.out_off[q] : s.ov.u32() + a) : nullptr;
-        if constexpr (sizeof(K) == 4) {
-          e = sort_pieces_u32(*d.ws, s.recv.u32() + a, kdst, d.tmp.u32(), z - a, p.p_off[q].data(),
-                              p.p_len[q].data(), p.p_seg[q].data(), p.p_off[q].size(),
-                              (uint32_t)(p.hi[(size_t)i * R + r] - p.lo[(size_t)i * R + r]), dplan::kTopShift, bits,
-                              d.st);
-        } else {
-          e = sort_pairs_u64_u32(*d.ws, static_cast<uint64_t*>(s.recv.p) + a, s.rv.u32() + a, kdst, vdst,
-                                 static_cast<uint64_t*>(d.tmp.p), d.tmpv.u32(), z - a, 0, 64, bits, d.st);
-        }
-        if (!ok_hip(e, "round sort")) return false;
+  // round i of every rank on device d, sorted as soon as it has arrived
+  auto sort_round = [&](DevState& d, int i) -> bool {
+    for (int r = 0; r < R; ++r) {
+      RankState& s = c.ranks[r];
+      if (s.d != &d) continue;
+      const uint64_t a = p.roff[(size_t)r * (K_ + 1) + i], z = p.roff[(size_t)r * (K_ + 1) + i + 1];
+      if (!ok_hip(hipStreamWaitEvent(d.st, s.ev_x[i], 0), "wait")) return false;
+      if (z == a) continue;
+      hipError_t e;
+      const size_t q = (size_t)r * K_ + i;
+      K* kdst = pl.direct[q] ? out[r] + pl.out_off[q] : static_cast<K*>(s.outb.p) + a;
+      uint32_t* vdst = pairs ? (pl.direct[q] ? (*vout)[r] + pl.out_off[q] : s.ov.u32() + a) : nullptr;
+      if constexpr (sizeof(K) == 4) {
+        e = sort_pieces_u32(*d.ws, s.recv.u32() + a, kdst, d.tmp.u32(), z - a, p.p_off[q].data(), p.p_len[q].data(),
+                            p.p_seg[q].data(), p.p_off[q].size(),
+                            (uint32_t)(p.hi[(size_t)i * R + r] - p.lo[(size_t)i * R + r]), dplan::kTopShift, bits,
+                            d.st);
+      } else {
+        e = sort_pairs_u64_u32(*d.ws, static_cast<uint64_t*>(s.recv.p) + a, s.rv.u32() + a, kdst, vdst,
+                               static_cast<uint64_t*>(d.tmp.p), d.tmpv.u32(), z - a, 0, 64, bits, d.st);
       }
+      if (!ok_hip(e, "round sort")) return false;
+    }
     return true;
-  });
+  };
+  // Several devices: one host thread per device sorts its ranks' rounds, each
+  // round as soon as this thread has issued that round's exchange (the round
+  // sorts wait on the host for small read-backs; one device's waits must not
+  // hold another device's issue -- ADVICE r02 -- and round 0's sorts need not
+  // wait for the later rounds' exchange calls).  One device: inline, after
+  // every exchange is issued.
+  std::mutex mu;
+  std::condition_variable cv;
+  int issued = 0;
+  bool stop = false;
+  std::vector<std::string> err(c.uniq.size());
+  std::vector<char> good(c.uniq.size(), 1);
+  std::vector<std::thread> th;
+  // (LIBSORT_DISTRIB_THREADS=1: the threaded path for one device too -- the
+  // one-GPU test box's way into it)
+  static const bool force_threads = [] {
+    const char* e = getenv("LIBSORT_DISTRIB_THREADS");
+    return e && e[0] == '1';
+  }();
+  const bool threaded = c.uniq.size() > 1 || force_threads;
+  if (threaded)
+    for (size_t u = 0; u < c.uniq.size(); ++u)
+      th.emplace_back([&, u] {
+        DevState& d = *c.uniq[u];
+        bool ok = ok_hip(hipSetDevice(d.dev), "hipSetDevice");
+        for (int i = 0; ok && i < K_; ++i) {
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return issued > i || stop; });
+            if (issued <= i) break;  // the exchange failed
+          }
+          ok = sort_round(d, i);
+        }
+        if (!ok) {
+          good[u] = 0;
+          err[u] = last_error();
+        }
+      });
+  bool issue_ok = true;
+  for (int i = 0; issue_ok && i < K_; ++i) {
+    issue_ok = move_pieces(c, p.rounds[i], src, dst, sizeof(K), use_rccl, self_rccl) &&
+               (!pairs || move_pieces(c, p.rounds[i], vsrc, vdst, 4, use_rccl, self_rccl));
+    for (int r = 0; issue_ok && r < R; ++r) {
+      RankState& s = c.ranks[r];
+      issue_ok = ok_hip(hipSetDevice(s.dev), "hipSetDevice") && ok_hip(hipEventRecord(s.ev_x[i], s.d->cs), "record");
+    }
+    if (issue_ok && threaded) {
+      std::lock_guard<std::mutex> lk(mu);
+      issued = i + 1;
+      cv.notify_all();
+    }
+  }
+  if (threaded) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+      cv.notify_all();
+    }
+    for (auto& t : th) t.join();
+  }
+  if (!issue_ok) return false;
+  bool sorted = true;
+  if (threaded) {
+    for (size_t u = 0; u < good.size(); ++u)
+      if (!good[u]) {
+        set_error(err[u]);
+        sorted = false;
+      }
+  } else {
+    sorted = ok_hip(hipSetDevice(c.uniq[0]->dev), "hipSetDevice");
+    for (int i = 0; sorted && i < K_; ++i) sorted = sort_round(*c.uniq[0], i);
+  }
   if (!sorted) return false;
   // the equal re-cut: the pieces of the rounds that were not sorted in place
   for (int r = 0; r < R; ++r) {

@@ -207,3 +207,42 @@ def test_config5_share_over_rccl(D):
         return h.hexdigest()
     assert sha(ko[0], np.uint64) == want["keys"]
     assert sha(vo[0], np.uint32) == want["payloads"]
+
+
+def test_threaded_round_issue(oracle_mod):
+    """The multi-device issue path of the C engine (one host thread per
+    device sorting round i as soon as round i's exchange is issued) on the
+    one-GPU box, forced by LIBSORT_DISTRIB_THREADS=1 in a fresh process: one
+    RCCL rank, 3 ranks sharing the GPU, keys and pairs, against the oracle."""
+    import os
+    import pathlib
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = pathlib.Path(__file__).resolve().parents[1]
+    code = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [%r, %r]
+import pylibsort.device as D
+from oracle import oracle
+x = oracle.pcg((1 << 22) + 999, first=4)
+for R, flags in ((1, 4), (3, 2)):
+    S = -(-x.size // R)
+    sh = [torch.from_numpy(x[r * S:(r + 1) * S].view(np.int32).copy()).cuda() for r in range(R)]
+    outs = D.distrib_sort_u32(sh, flags)
+    got = np.concatenate([o.cpu().numpy().view(np.uint32) for o in outs])
+    assert np.array_equal(got, oracle.sort_u32(x)), R
+    k = (x.astype(np.uint64) << np.uint64(32)) | x.astype(np.uint64)[::-1]
+    v = np.arange(x.size, dtype=np.uint32)
+    ks = [torch.from_numpy(k[r * S:(r + 1) * S].view(np.int64).copy()).cuda() for r in range(R)]
+    vs = [torch.from_numpy(v[r * S:(r + 1) * S].view(np.int32).copy()).cuda() for r in range(R)]
+    ko, vo = D.distrib_sort_pairs_u64_u32(ks, vs, flags)
+    rk, rv = oracle.stable_sort_kv64(k, v)
+    assert np.array_equal(np.concatenate([t.cpu().numpy().view(np.uint64) for t in ko]), rk), R
+    assert np.array_equal(np.concatenate([t.cpu().numpy().view(np.uint32) for t in vo]), rv), R
+print("OK")
+""" % (str(root), str(root / "gpu-radix-sort_amd"))
+    env = dict(os.environ, LIBSORT_DISTRIB_THREADS="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
