@@ -39,8 +39,10 @@ for p in (str(ROOT), str(ROOT / "gpu-radix-sort_amd")):
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 # N>1 engine when --engine auto (the faster of the two
-# on the one-GPU schedule measurement at 2^29 keys per rank)
-DEFAULT_ENGINE = "torch"
+# on the one-GPU schedule measurement at 2^29 keys per rank --
+# profiles/r03h_*: C engine 7.48 ms vs torch engine 7.85 ms in the 8-GPU
+# per-rank shape, 6.52 vs 6.92 ms on uniform keys)
+DEFAULT_ENGINE = "cabi"
 PASS_KERNELS = "tilepass,onesweep,downsweep"  # the roofline kernel candidates (timed-region events)
 
 
@@ -189,8 +191,8 @@ def main():
         # one process drives every GPU through the C ABI (what a C or Go
         # caller binds); the other ranks keep the barriers and the max-over-
         # ranks timing.  Shard r = the same keys rank r holds in torch mode.
-        del keys
-        keys = None
+        # (every rank keeps its own keys too: the torch engine takes over if
+        # the C engine fails its first step)
         devs = [0] * world if rehearsal else list(range(world))
         if rank == 0:
             shards, vshards = [], []
@@ -227,6 +229,23 @@ def main():
         if world > 1:
             dist.barrier()
 
+    engine_note = None
+    if cabi:
+        # first step of the C engine; if it fails on rank 0, every rank
+        # switches to the torch engine (identical decision via all_reduce)
+        failed = 0
+        if rank == 0:
+            try:
+                step()
+            except RuntimeError as e:
+                failed, engine_note = 1, "C-ABI engine failed its first step (%s); torch engine measured" % e
+        flag = torch.tensor([failed], dtype=torch.int32, device="cuda")
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if int(flag.item()):
+            cabi = False
+            engine = "torch"
+            if rank == 0:
+                sys.stderr.write("bench.py: %s\n" % engine_note)
     for _ in range(args.warmup):
         res = step()
     torch.cuda.synchronize()
@@ -428,6 +447,11 @@ def main():
             "variants": variants or None,
             "host_abi": host_abi,
         }
+        if world > 1:
+            line["engine"] = ("cabi: rank 0 drives all %d GPUs through the C ABI" % world if cabi else
+                              "torch: one process per GPU")
+            if engine_note:
+                line["engine_note"] = engine_note
         if rehearsal:
             line["rehearsal"] = "gloo, all ranks on one GPU: exercises the N>1 path, not a measurement"
         print(json.dumps(line), flush=True)
