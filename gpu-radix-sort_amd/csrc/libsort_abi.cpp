@@ -1006,31 +1006,6 @@ LS_BOOL_ENTRY(libsortSegmentCopyU32, const uint32_t* d_src, uint32_t* d_dst, siz
              : 0;
 }
 
-LS_BOOL_ENTRY(libsortPlanHistogramU32, const uint32_t* d_keys, size_t n, uint32_t block, uint32_t stride,
-                                           int64_t* d_out, void* stream) {
-  if (!d_out || block == 0 || (n > 0 && !d_keys)) {
-    set_error("libsortPlanHistogramU32: bad arguments");
-    return 0;
-  }
-  hipStream_t st = as_stream(stream);
-  return with_current_ws(st, [&](Workspace& ws) {
-           return hip_ok(plan_hist_u32(ws, d_keys, n, 12, block, stride, d_out, st), "libsortPlanHistogramU32");
-         })
-             ? 1
-             : 0;
-}
-
-LS_BOOL_ENTRY(libsortPlanRounds, const int64_t* d_rows, uint32_t nranks, uint32_t ld, uint32_t rounds,
-                                     double growth, uint8_t* d_lut, int64_t* d_est, void* stream) {
-  if (!d_rows || !d_lut || !d_est || nranks < 1 || rounds < 1 || nranks * rounds > 256 || ld < 4096) {
-    set_error("libsortPlanRounds: need 1 <= nranks * rounds <= 256 and ld >= 4096");
-    return 0;
-  }
-  return hip_ok(plan_rounds(d_rows, nranks, ld, rounds, growth, d_lut, d_est, as_stream(stream)), "libsortPlanRounds")
-             ? 1
-             : 0;
-}
-
 LS_BOOL_ENTRY(libsortDeltaMaxGapU32, const uint32_t* d_keys, size_t n, uint32_t* d_maxgap, void* stream) {
   if (!d_maxgap || (n > 0 && !d_keys)) {
     set_error("libsortDeltaMaxGapU32: bad arguments");

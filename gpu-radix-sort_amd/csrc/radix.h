@@ -221,19 +221,12 @@ hipError_t segment_copy_u32(Workspace& ws, const uint32_t* src, uint32_t* dst, s
                             const uint64_t* src_off, const uint64_t* dst_off, const uint64_t* len,
                             hipStream_t stream);
 hipError_t populate_device(uint32_t* out, size_t n, uint64_t first, hipStream_t stream);
-// Multi-GPU round plan: sampled 12-bit top-bucket histogram as an int64 row
-// with n appended (d_out: 4097 entries), and the (rank, round) table of
-// sort_msd from the gathered rows (R x ld int64).
-hipError_t plan_hist_u32(Workspace& ws, const uint32_t* keys, size_t n, int bits, uint64_t block, uint64_t stride,
-                         int64_t* d_out, hipStream_t stream);
 // delta-coded sorted runs (the msdz exchange): largest in-group gap, pack
 // (w from the device word), unpack (w from the host), two-run merge
 hipError_t delta_maxgap_u32(const uint32_t* keys, size_t n, uint32_t* d_maxgap, hipStream_t st);
 hipError_t delta_pack_u32(const uint32_t* keys, size_t n, const uint32_t* d_maxgap, uint32_t* out, hipStream_t st);
 hipError_t delta_unpack_u32(const uint32_t* in, size_t n, uint32_t w, uint32_t* keys, hipStream_t st);
 hipError_t merge_u32(const uint32_t* a, size_t na, const uint32_t* b, size_t nb, uint32_t* out, hipStream_t st);
-hipError_t plan_rounds(const int64_t* d_hist, uint32_t R, uint32_t ld, uint32_t K, double growth, uint8_t* d_lut,
-                       int64_t* d_est, hipStream_t stream);
 
 // Cross-stream ordering of a device's workspace (libsort_abi.cpp): a call on
 // stream `st` first waits for the previous call's work on another stream;

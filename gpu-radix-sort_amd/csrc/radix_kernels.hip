@@ -2198,177 +2198,6 @@ __global__ __launch_bounds__(256) void k_merge_u32(const uint32_t* __restrict__ 
 }
 
 // ----------------------------------------------------------------------------
-// multi-GPU round plan (pylibsort.distrib.sort_msd) on the device
-// ----------------------------------------------------------------------------
-
-// Sampled top-bit histogram of the multi-GPU plan: key >> shift over every
-// `stride`-th block of `block` keys, i.e. sampled block sb starts at sb *
-// step (step = stride * block; all keys, step = block, when n < 4 * stride *
-// block, as HipOps.sample).  Workgroup g histograms sampled blocks g, g + G,
-// ... in LDS with 16-byte loads and writes its whole row rows[g][*]: no
-// global atomics and no per-key 64-bit index arithmetic (the first version,
-// one 64-bit div/mod per key and 4096 global atomics per workgroup, took
-// 89 us at 2^28 keys).  k_plan_hist_out sums the rows, out[bins] = n.
-template <int BITS>
-__global__ __launch_bounds__(512) void k_plan_hist(const uint32_t* __restrict__ keys, uint64_t n, uint32_t shift,
-                                                   uint32_t block, uint64_t step, uint64_t nsb, bool full_blocks,
-                                                   uint32_t* __restrict__ rows) {
-  constexpr int BINS = 1 << BITS, T = 512, U = 4;
-  __shared__ uint32_t s_h[BINS];
-  for (int i = threadIdx.x; i < BINS; i += T) s_h[i] = 0u;
-  __syncthreads();
-  const uint32_t G = gridDim.x;
-  if (full_blocks && ((uintptr_t)keys & 15u) == 0 && (block & 3u) == 0 && (step & 3u) == 0) {
-    // this workgroup's sampled blocks blockIdx.x + k * G as one flat range
-    // of 16-byte vectors, U loads in flight per thread
-    const uint32_t per = block >> 2;
-    const uint32_t total = (uint32_t)((nsb - blockIdx.x + G - 1) / G) * per;
-    auto addr = [&](uint32_t q) {
-      const uint64_t sb = blockIdx.x + (uint64_t)(q / per) * G;
-      return reinterpret_cast<const uint4*>(keys + sb * step) + (q % per);
-    };
-    uint32_t q = threadIdx.x;
-    for (; q + (U - 1) * T < total; q += U * T) {
-      uint4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = load_count_vec(addr(q + u * T));
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        atomicAdd(&s_h[(v[u].x >> shift) & (BINS - 1)], 1u);
-        atomicAdd(&s_h[(v[u].y >> shift) & (BINS - 1)], 1u);
-        atomicAdd(&s_h[(v[u].z >> shift) & (BINS - 1)], 1u);
-        atomicAdd(&s_h[(v[u].w >> shift) & (BINS - 1)], 1u);
-      }
-    }
-    for (; q < total; q += T) {
-      const uint4 v = load_count_vec(addr(q));
-      atomicAdd(&s_h[(v.x >> shift) & (BINS - 1)], 1u);
-      atomicAdd(&s_h[(v.y >> shift) & (BINS - 1)], 1u);
-      atomicAdd(&s_h[(v.z >> shift) & (BINS - 1)], 1u);
-      atomicAdd(&s_h[(v.w >> shift) & (BINS - 1)], 1u);
-    }
-  } else {
-    for (uint64_t sb = blockIdx.x; sb < nsb; sb += G) {
-      const uint64_t start = sb * step;
-      const uint32_t len = (uint32_t)umin64((uint64_t)block, n - start);
-      for (uint32_t i = threadIdx.x; i < len; i += T) atomicAdd(&s_h[(keys[start + i] >> shift) & (BINS - 1)], 1u);
-    }
-  }
-  __syncthreads();
-  uint32_t* row = rows + (size_t)blockIdx.x * BINS;
-  for (int i = threadIdx.x; i < BINS; i += T) row[i] = s_h[i];
-}
-
-// Column sums of rows[G][bins] -> out (int64), out[bins] = n.  Block b sums
-// 16 columns: thread (r, c) adds rows r, r + 16, ... of column 16b + c, then
-// the 16 partial sums meet in LDS (rows in parallel, not one column per
-// thread walking all G rows).
-__global__ __launch_bounds__(256) void k_plan_hist_out(const uint32_t* __restrict__ rows, uint32_t G, uint32_t bins,
-                                                       uint64_t n, int64_t* __restrict__ out) {
-  __shared__ uint32_t s_p[16][17];
-  const uint32_t c = threadIdx.x & 15u, r = threadIdx.x >> 4, col = blockIdx.x * 16 + c;
-  uint32_t s = 0;
-  if (col < bins)
-    for (uint32_t g = r; g < G; g += 16) s += rows[(size_t)g * bins + col];
-  s_p[r][c] = s;
-  __syncthreads();
-  if (threadIdx.x < 16 && col < bins) {
-    uint64_t t = 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t += s_p[i][c];
-    out[col] = (int64_t)t;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) out[bins] = (int64_t)n;
-}
-
-// Round plan from the gathered rows H[R][ld] (first 4096 entries = the
-// sampled histograms): bucket b's middle, in rank coordinates x = (cum(b) -
-// G(b)/2) / total * R, gives its rank floor(x); its round is the first i
-// with x - rank < cw[i] (cw = normalised prefix of growth^i), made monotone
-// over the buckets (cumulative max of rank * K + round); lut[b] = round * R +
-// rank; est[r] = estimated keys of rank r.  One block of 1024 threads, 4
-// buckets each.  Same arithmetic as distrib._plan_rounds_t.
-__global__ __launch_bounds__(1024) void k_plan_rounds(const int64_t* __restrict__ H, uint32_t R, uint32_t ld,
-                                                      uint32_t K, double growth, uint8_t* __restrict__ lut,
-                                                      int64_t* __restrict__ est) {
-  constexpr int PER = 4, T = 1024, W = T / kWave;  // T * PER = 4096 buckets
-  __shared__ uint64_t s_w[W];
-  __shared__ double s_cw[256];
-  __shared__ unsigned long long s_est[256];
-  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
-  if (tid == 0) {
-    double acc = 0.0, p = 1.0;
-    for (uint32_t i = 0; i < K; ++i) { s_cw[i] = acc + p; acc += p; p *= growth; }
-    for (uint32_t i = 0; i < K; ++i) s_cw[i] /= acc;
-  }
-  if (tid < 256) s_est[tid] = 0ull;
-  uint64_t g[PER], sum = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    uint64_t c = 0;
-    for (uint32_t r = 0; r < R; ++r) c += (uint64_t)H[(size_t)r * ld + tid * PER + j];
-    g[j] = c;
-    sum += c;
-  }
-  // inclusive block scan of the per-thread sums (wave shuffles + LDS)
-  uint64_t x = sum;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint64_t y = __shfl_up(x, o, kWave);
-    if ((int)lane >= o) x += y;
-  }
-  if (lane == kWave - 1) s_w[w] = x;
-  __syncthreads();
-  uint64_t pre = 0, total = 0;
-  for (uint32_t i = 0; i < W; ++i) {
-    pre += i < w ? s_w[i] : 0ull;
-    total += s_w[i];
-  }
-  const double Td = total ? (double)total : 1.0;
-  uint64_t cum = pre + x - sum;  // exclusive prefix of this thread's first bucket
-  uint32_t code[PER], best = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    cum += g[j];
-    const double xr = ((double)cum - (double)g[j] / 2.0) / Td * (double)R;
-    int64_t rank = (int64_t)floor(xr);
-    if (rank > (int64_t)R - 1) rank = (int64_t)R - 1;
-    if (rank < 0) rank = 0;
-    const double f = xr - (double)rank;
-    uint32_t rnd = 0;
-    while (rnd < K && s_cw[rnd] <= f) ++rnd;  // searchsorted(cw, f, right=True)
-    if (rnd > K - 1) rnd = K - 1;
-    code[j] = (uint32_t)rank * K + rnd;
-    best = max(best, code[j]);
-  }
-  // cumulative max over buckets: per-thread running max, then an exclusive
-  // max-scan of the per-thread maxima
-  uint32_t mx = best;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint32_t y = __shfl_up(mx, o, kWave);
-    if ((int)lane >= o) mx = max(mx, y);
-  }
-  __syncthreads();
-  __shared__ uint32_t s_m[W];
-  if (lane == kWave - 1) s_m[w] = mx;
-  __syncthreads();
-  uint32_t run = 0;
-  for (uint32_t i = 0; i < w; ++i) run = max(run, s_m[i]);
-  const uint32_t prev_lane = __shfl_up(mx, 1, kWave);
-  if (lane > 0) run = max(run, prev_lane);
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    run = max(run, code[j]);
-    const uint32_t rank = run / K, rnd = run % K;
-    lut[tid * PER + j] = (uint8_t)(rnd * R + rank);
-    if (g[j]) atomicAdd(&s_est[rank], (unsigned long long)g[j]);
-  }
-  __syncthreads();
-  if (tid < R) est[tid] = (int64_t)s_est[tid];
-}
-
-// ----------------------------------------------------------------------------
 // PCG32 stream on the device (utils.cu:65-80 + LCG skip-ahead)
 // ----------------------------------------------------------------------------
 __host__ __device__ inline uint64_t pcg_advance(uint64_t state, uint64_t delta) {
@@ -3728,36 +3557,6 @@ hipError_t segment_copy_u32(Workspace& ws, const uint32_t* src, uint32_t* dst, s
   ScopedTimer tm("segcopy", st, total);
   const uint32_t blocks = (uint32_t)std::min<size_t>(nseg, 8192);
   hipLaunchKernelGGL(k_segment_copy, dim3(blocks), dim3(256), 0, st, src, dst, ws.seg_dev, (uint64_t)nseg);
-  return hipGetLastError();
-}
-
-hipError_t plan_hist_u32(Workspace& ws, const uint32_t* keys, size_t n, int bits, uint64_t block, uint64_t stride,
-                         int64_t* d_out, hipStream_t st) {
-  constexpr uint32_t BINS = 4096;
-  if (bits != 12 || block == 0 || block > 0xffffffffull) return hipErrorInvalidValue;
-  const uint64_t nb = n / block;
-  const bool sampled = stride > 1 && nb >= 4 * stride;
-  const uint64_t nsb = sampled ? (nb + stride - 1) / stride : (n + block - 1) / block;
-  const uint64_t step = sampled ? stride * block : block;
-  const uint32_t G = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nsb, (uint64_t)std::max(1, ws.num_cus)));
-  if (ws.hist_tmp_cap < (size_t)G * BINS) {
-    if (ws.hist_tmp) { (void)hipFree(ws.hist_tmp); ws.hist_tmp = nullptr; }
-    ws.hist_tmp_cap = 0;
-    LS_TRY(hipMalloc(&ws.hist_tmp, (size_t)G * BINS * sizeof(uint32_t)));
-    ws.hist_tmp_cap = (size_t)G * BINS;
-  }
-  ScopedTimer tm("histogram", st, n);
-  hipLaunchKernelGGL(k_plan_hist<12>, dim3(G), dim3(512), 0, st, keys, (uint64_t)n, 32u - 12u, (uint32_t)block, step,
-                     nsb, sampled, ws.hist_tmp);
-  LS_TRY(hipGetLastError());
-  hipLaunchKernelGGL(k_plan_hist_out, dim3(BINS / 16), dim3(256), 0, st, ws.hist_tmp, G, BINS, (uint64_t)n, d_out);
-  return hipGetLastError();
-}
-
-hipError_t plan_rounds(const int64_t* d_hist, uint32_t R, uint32_t ld, uint32_t K, double growth, uint8_t* d_lut,
-                       int64_t* d_est, hipStream_t st) {
-  if (R < 1 || R > 256 || K < 1 || R * K > 256 || ld < 4096 || !(growth > 0.0)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_plan_rounds, dim3(1), dim3(1024), 0, st, d_hist, R, ld, K, growth, d_lut, d_est);
   return hipGetLastError();
 }
 

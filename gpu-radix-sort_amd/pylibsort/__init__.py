@@ -74,10 +74,6 @@ _SIGS = [
     ("libsortPartitionLutScatterU64U32", ctypes.c_int,
      [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     ("libsortSegmentCopyU32", ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _u64p, _u64p, _u64p, _vp]),
-    ("libsortPlanHistogramU32", ctypes.c_int,
-     [_vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
-    ("libsortPlanRounds", ctypes.c_int,
-     [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, _vp, _vp, _vp]),
     ("libsortDeltaMaxGapU32", ctypes.c_int, [_vp, ctypes.c_size_t, _vp, _vp]),
     ("libsortDeltaPackU32", ctypes.c_int, [_vp, ctypes.c_size_t, _vp, _vp, _vp]),
     ("libsortDeltaUnpackU32", ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_uint32, _vp, _vp]),

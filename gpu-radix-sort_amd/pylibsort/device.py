@@ -304,33 +304,6 @@ def segment_copy_u32(src, dst, src_off, dst_off, lens):
     return dst
 
 
-def plan_histogram_u32(keys, block=4096, stride=16, out=None):
-    """int64 tensor of 4097: the top-12-bit histogram of every `stride`-th
-    block of `block` keys (all keys when few), then the key count."""
-    _need(keys, _U32, "keys")
-    out = torch.empty(4097, dtype=torch.int64, device=keys.device) if out is None else out
-    _need(out, _U64, "out")
-    _check(_lib().libsortPlanHistogramU32(_ptr(keys), keys.numel(), block, stride, _ptr(out), _stream()),
-           "libsortPlanHistogramU32")
-    return out
-
-
-def plan_rounds(rows, nranks, rounds, growth=1.2, lut=None, est=None):
-    """(lut uint8[4096], est int64[nranks]) of the msd round plan from the
-    gathered int64 rows [nranks, ld >= 4096] (histogram first)."""
-    _need(rows, _U64, "rows")
-    if rows.dim() != 2 or rows.shape[0] != nranks or rows.shape[1] < 4096:
-        raise ValueError("rows must be [nranks, >= 4096]")
-    lut = torch.empty(4096, dtype=torch.uint8, device=rows.device) if lut is None else lut
-    est = torch.empty(nranks, dtype=torch.int64, device=rows.device) if est is None else est
-    _check(_lib().libsortPlanRounds(_ptr(rows), nranks, rows.shape[1], rounds, float(growth), _ptr(lut), _ptr(est),
-                                    _stream()), "libsortPlanRounds")
-    return lut, est
-
-
-DELTA_GROUP = 64
-
-
 def delta_bits(maxgap):
     """Bit width of the coded gaps for a run whose largest in-group gap is maxgap."""
     return int(maxgap).bit_length()

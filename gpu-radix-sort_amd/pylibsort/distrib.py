@@ -7,25 +7,30 @@ and localTest/benchmarks.cpp:70-160 (distribSort) -- whose "exchange" goes
 through host memcpy or files, by device-resident rounds with one
 all_to_all_single (alltoallv) per exchange.
 
-Two schedules, identical final result (rank r holds keys [r*S, (r+1)*S) of the
-globally sorted array, S = ceil(N/R), the reference's equal re-cut):
+Three schedules, identical final result (rank r holds keys [r*S, (r+1)*S)
+of the globally sorted array, S = ceil(N/R), the reference's equal re-cut):
 
   "lsd"  the reference's BSP semantics: per `width`-bit digit, a stable local
          partial sort (gpuPartial on the device), an allgather of the per-rank
          bucket counts, one alltoallv of contiguous slices, and a segment
          gather into bucket-major / rank-minor order.  32/width exchanges.
-  "msd"  range-split rounds: a (sampled) 12-bit histogram of the top key
-         bits (allgather) assigns contiguous key ranges to (rank, round), R x K
-         groups; ONE stable table partition (libsortPartitionLutU32) lays the
-         keys out round-major / destination-minor; K alltoallv exchanges are
+  "msd"  top-digit rounds: every rank partitions its keys stably by the top 8
+         bits (gpuPartial(offset 24, width 8) on the device, split so the 256
+         exact bucket counts reach the host while the scatter runs); the
+         counts are all-gathered and libsort's host plan (plan_digits, the
+         same C code the single-process engine runs) gives each (rank, round)
+         a contiguous digit range; every round's point-to-point exchange is
          issued at once (RCCL's stream runs them back to back) and round i is
-         sorted into its final slice of the output as soon as it has arrived,
-         overlapping the exchange of the later rounds.  The rounds are
-         disjoint key ranges in increasing order, so no merge is needed.  A
-         small alltoallv then shifts the few surplus keys to the neighbours so
-         the shards are exact.  Falls back to "lsd" when one top-12-bit bucket
-         is so large that a rank would receive more than `max_imbalance` x S
-         keys.
+         sorted as soon as it has arrived, straight from its received
+         (source, digit) pieces (libsortSortPiecesU32: no gather, no pass
+         over the top digit) into the rank's final buffer.  The rounds are
+         disjoint key ranges in increasing order, so no merge is needed; the
+         few keys past the equal cut move to the neighbours point to point
+         (no copy of what stays).  Falls back to "lsd" when one digit range
+         would give a rank more than `max_imbalance` x S keys.
+  "msdz" the same partition and plan, but the SENDER sorts each outgoing
+         piece and sends it gap-coded; the receiver decodes and merges (for
+         link-bound world sizes: the bench default at 2 GPUs).
 
 The local operations come from an `ops` backend.  The product backend is
 HipOps (libsort's HIP kernels on torch CUDA tensors).  The CPU tests pass an
@@ -37,7 +42,6 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-HIST_BITS = 12
 # the top-digit rounds partition by key >> TOP_SHIFT (8 bits, 256 digits)
 TOP_BITS = 8
 TOP_SHIFT = 32 - TOP_BITS
@@ -94,14 +98,6 @@ class HipOps:
         bounds = b.cpu().numpy().view(np.uint32).astype(np.int64)
         return out, np.diff(bounds, append=keys.numel())
 
-    def histogram(self, keys, shift, bits):
-        return self.D.histogram_u32(keys, shift, bits)
-
-    def sort_range(self, keys, lo, hi, out=None):
-        """Full sort of keys known to lie in [lo, hi) (fewer passes)."""
-        out = self.empty(keys.numel()) if out is None else out
-        return self.D.sort_keys_range_u32(keys, lo, hi, out=out, tmp=self._scratch(keys.numel()))
-
     def sort_pairs(self, keys, vals, out_keys=None, out_vals=None):
         """Stable sort of (uint64 key, uint32 payload) pairs."""
         n = keys.numel()
@@ -140,58 +136,6 @@ class HipOps:
         n = int(np.sum(lens)) if len(lens) else 0
         return self.D.sort_pieces_u32(keys, off, lens, segs, nseg, TOP_SHIFT, out=out, tmp=self._scratch(n))
 
-    def partition(self, keys, splitters, out=None):
-        out = self.empty(keys.numel()) if out is None else out
-        return self.D.partition_u32(keys, splitters, out=out)[0]
-
-    def partition_lut_pairs(self, keys, vals, lut, shift, nbuckets):
-        """(keys, payloads, bucket starts as host int64) of the stable pair partition."""
-        t = torch.from_numpy(np.ascontiguousarray(lut, dtype=np.uint8)).to(self.device)
-        n = keys.numel()
-        k, v, b = self.D.partition_lut_pairs_u64_u32(keys, vals, t, shift, nbuckets, out_keys=self.empty64(n),
-                                                      out_vals=self.empty(n))
-        return k, v, b.cpu().numpy().view(np.uint32).astype(np.int64)
-
-    def sample_hi(self, keys, stride, block=4096):
-        """High 32-bit words of a block sample of uint64 keys (little endian)."""
-        return self.sample(keys, stride, block).view(torch.int32)[1::2].contiguous()
-
-    def partition_lut(self, keys, lut, shift, nbuckets):
-        """(partitioned keys, bucket starts as host int64 numpy array)."""
-        t = torch.from_numpy(np.ascontiguousarray(lut, dtype=np.uint8)).to(self.device)
-        out, b = self.D.partition_lut_u32(keys, t, shift, nbuckets, out=self.empty(keys.numel()))
-        return out, b.cpu().numpy().view(np.uint32).astype(np.int64)
-
-    def partition_lut_t(self, keys, lut, shift, nbuckets):
-        """As partition_lut with the table and the bucket starts as device
-        tensors (no host synchronisation)."""
-        out, b = self.D.partition_lut_u32(keys, lut.contiguous(), shift, nbuckets, out=self.empty(keys.numel()))
-        return out, b.to(torch.int64) & 0xFFFFFFFF
-
-    def partition_lut_count_t(self, keys, lut, shift, nbuckets):
-        """Count half of the split table partition: bucket starts (int64,
-        device) while nothing has moved yet."""
-        # uint32 starts in an int32 tensor; _sizes_from_starts widens them on
-        # the side stream, so nothing is queued between count and scatter
-        return self.D.partition_lut_count_u32(keys, lut.contiguous(), shift, nbuckets)
-
-    def partition_lut_scatter_t(self, keys, lut, shift, nbuckets):
-        return self.D.partition_lut_scatter_u32(keys, lut.contiguous(), shift, nbuckets, out=self.empty(keys.numel()))
-
-    def partition_lut_pairs_count_t(self, keys, vals, lut, shift, nbuckets):
-        return self.D.partition_lut_pairs_count_u64_u32(keys, vals, lut.contiguous(), shift, nbuckets)
-
-    def partition_lut_pairs_scatter_t(self, keys, vals, lut, shift, nbuckets):
-        n = keys.numel()
-        return self.D.partition_lut_pairs_scatter_u64_u32(keys, vals, lut.contiguous(), shift, nbuckets,
-                                                          out_keys=self.empty64(n), out_vals=self.empty(n))
-
-    def partition_lut_pairs_t(self, keys, vals, lut, shift, nbuckets):
-        n = keys.numel()
-        k, v, b = self.D.partition_lut_pairs_u64_u32(keys, vals, lut.contiguous(), shift, nbuckets,
-                                                      out_keys=self.empty64(n), out_vals=self.empty(n))
-        return k, v, b.to(torch.int64) & 0xFFFFFFFF
-
     def delta_maxgap(self, keys, out):
         return self.D.delta_maxgap_u32(keys, out=out)
 
@@ -203,22 +147,6 @@ class HipOps:
 
     def merge(self, a, b, out):
         return self.D.merge_u32(a, b, out=out)
-
-    def plan_row(self, keys, stride, block=4096):
-        """int64[4097] on the device: sampled top-12-bit histogram + n (one
-        libsort call instead of sample copy + histogram + cat)."""
-        return self.D.plan_histogram_u32(keys, block=block, stride=stride)
-
-    def plan(self, rows, R, K, growth=None):
-        """(lut uint8[4096], est int64[R]) from the gathered rows, on the device."""
-        return self.D.plan_rounds(rows.contiguous(), R, K, GROWTH if growth is None else growth)
-
-    def sample(self, keys, stride, block=4096):
-        """Every `stride`-th block of `block` keys (all keys when few)."""
-        nb = keys.numel() // block
-        if stride <= 1 or nb < 4 * stride:
-            return keys
-        return keys[:nb * block].view(nb, block)[::stride].contiguous().view(-1)
 
     def segment_copy(self, src, dst, so, do, ln):
         return self.D.segment_copy_u32(src, dst, so, do, ln)
@@ -509,44 +437,6 @@ def sort_lsd(keys, ops, group=None, width=8):
     return cur
 
 
-def plan_msd(H, R, hist_bits=HIST_BITS):
-    """Bucket -> rank assignment from the gathered top-bit histograms H[R, 2^b].
-    Returns (splitters, dest_of_bucket, n_recv_per_rank)."""
-    G = H.sum(axis=0)
-    N = int(G.sum())
-    S, _ = shard_cut(N, R)
-    cum = np.concatenate([[0], np.cumsum(G)[:-1]])
-    mid = cum + G // 2
-    dest = np.minimum(mid // max(S, 1), R - 1).astype(np.int64)
-    dest = np.maximum.accumulate(dest)
-    shift = 32 - hist_bits
-    splitters = []
-    for d in range(1, R):
-        idx = np.nonzero(dest >= d)[0]
-        if idx.size == 0:
-            break
-        splitters.append(int(idx[0]) << shift)
-    n_recv = np.array([G[dest == d].sum() for d in range(R)], dtype=np.int64)
-    return splitters, dest, n_recv
-
-
-def _plan_row(ops, keys, stride):
-    """This rank's plan row: the sampled top-bit histogram and its key count
-    (int64, HIST_BITS + 1 entries) -- one libsort call on HipOps."""
-    if hasattr(ops, "plan_row"):
-        return ops.plan_row(keys, stride)
-    h = ops.histogram(ops.sample(keys, stride), 32 - HIST_BITS, HIST_BITS)
-    return torch.cat([h.to(torch.int64), torch.tensor([keys.numel()], dtype=torch.int64, device=h.device)])
-
-
-def _plan(ops, HN, R, K, growth=None):
-    """(lut, est) of the round plan from the gathered rows (device kernel on
-    HipOps, the torch restatement otherwise)."""
-    if hasattr(ops, "plan"):
-        return ops.plan(HN, R, K, growth)
-    return _plan_rounds_t(HN[:, :-1], R, K, growth)
-
-
 def _sizes_from_starts(b_t, n):
     """Bucket sizes (int64) from bucket starts (int64, or uint32 held in an
     int32 tensor), without a host round trip."""
@@ -556,46 +446,6 @@ def _sizes_from_starts(b_t, n):
         sizes[:-1] = b_t[1:] - b_t[:-1]
         sizes[-1:] = n - b_t[-1:]
     return sizes
-
-
-def _plan_rounds_t(H, R, K, growth=None):
-    """plan_rounds on torch tensors, on H's device (the GPU under RCCL, so the
-    plan needs no host round trip).  Returns (lut uint8, est float64)."""
-    G = H.sum(dim=0).to(torch.float64)
-    T = G.sum().clamp(min=1.0)                                 # all-zero histograms -> one group
-    x = (torch.cumsum(G, 0) - G / 2.0) / T * R                 # rank coordinate of each bucket's middle
-    rank = torch.clamp(torch.floor(x).to(torch.int64), max=R - 1)
-    growth = GROWTH if growth is None else growth
-    w = growth ** torch.arange(K, dtype=torch.float64, device=H.device)
-    cw = torch.cumsum(w, 0) / w.sum()
-    rnd = torch.clamp(torch.searchsorted(cw, (x - rank).contiguous(), right=True), max=K - 1)
-    grp = torch.cummax(rank * K + rnd, dim=0).values
-    rank, rnd = grp // K, grp % K
-    lut = (rnd * R + rank).to(torch.uint8)
-    est = torch.zeros(R, dtype=torch.float64, device=H.device).index_add_(0, rank, G)
-    return lut, est
-
-
-def plan_rounds(H, R, K, hist_bits=HIST_BITS, growth=None):
-    """Contiguous top-bit bucket ranges for (rank, round) from the gathered
-    (possibly sampled) histograms H[R, 2^b]: each rank gets about 1/R of the
-    estimated keys, split into K rounds whose sizes grow by `growth` (a small
-    first round keeps the exchange before the first sort short; each later
-    round's exchange hides behind the previous round's sort).  Group of a
-    bucket: rank g // K, round g % K.  Returns (lut, est_per_rank) with lut[b]
-    = round * R + rank (the partition bucket).  numpy wrapper of
-    _plan_rounds_t, which sort_msd runs on the device."""
-    lut, est = _plan_rounds_t(torch.as_tensor(np.asarray(H, dtype=np.int64)), R, K, growth)
-    return lut.numpy(), est.numpy()
-
-
-def _group_range(lut, code, hist_bits=HIST_BITS):
-    """[lo, hi) key range of the contiguous buckets with lut == code (None if empty)."""
-    idx = np.nonzero(lut == code)[0]
-    if idx.size == 0:
-        return None
-    shift = 32 - hist_bits
-    return int(idx[0]) << shift, (int(idx[-1]) + 1) << shift
 
 
 def _mark(trace, label):
@@ -990,5 +840,5 @@ def distrib_sort(keys, ops=None, group=None, schedule="auto", **kw):
     raise ValueError("schedule must be 'auto', 'msd', 'msdz' or 'lsd'")
 
 
-__all__ = ["HipOps", "distrib_sort", "distrib_sort_pairs", "sort_lsd", "sort_msd", "sort_msdz", "plan_msd", "plan_rounds",
+__all__ = ["HipOps", "distrib_sort", "distrib_sort_pairs", "sort_lsd", "sort_msd", "sort_msdz", "plan_digits",
            "shard_cut"]

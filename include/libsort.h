@@ -198,21 +198,6 @@ LIBSORT_API bool libsortSegmentCopyU32(const uint32_t* d_src, uint32_t* d_dst, s
                                        const uint64_t* src_off, const uint64_t* dst_off,
                                        const uint64_t* len, void* stream);
 
-/* Multi-GPU round plan (the "msd" schedule of pylibsort.distrib), on the
- * device so the plan needs no host round trip:
- * libsortPlanHistogramU32 writes the histogram of the top 12 key bits over
- * every `stride`-th block of `block` keys (all keys when there are fewer than
- * 4 * stride blocks) to d_out[0..4096) as int64, and n to d_out[4096];
- * libsortPlanRounds turns the gathered rows (nranks rows of ld >= 4096 int64,
- * the histograms first) into d_lut[4096] (bucket -> round * nranks + rank:
- * contiguous key ranges, about 1/nranks of the keys per rank, rounds growing
- * by `growth`) and d_est[nranks] (estimated keys per rank).
- * nranks * rounds <= 256. */
-LIBSORT_API bool libsortPlanHistogramU32(const uint32_t* d_keys, size_t n, uint32_t block, uint32_t stride,
-                                         int64_t* d_out, void* stream);
-LIBSORT_API bool libsortPlanRounds(const int64_t* d_rows, uint32_t nranks, uint32_t ld, uint32_t rounds,
-                                   double growth, uint8_t* d_lut, int64_t* d_est, void* stream);
-
 /* Delta-coded sorted runs (the "msdz" exchange of pylibsort.distrib for
  * link-bound world sizes).  A sorted uint32 run of n keys is coded in groups
  * of 64: the group's first key (uint32) and its 64 gaps to the previous key in

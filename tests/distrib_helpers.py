@@ -62,11 +62,6 @@ class OracleOps:
         out.copy_(res)
         return out
 
-    def sort_range(self, keys, lo, hi, out=None):
-        x = self._np(keys)
-        assert x.size == 0 or (int(x.min()) >= lo and int(x.max()) < hi), "key outside its round's range"
-        return self.sort(keys, out=out)
-
     def partial_sort(self, keys, offset, width, out=None):
         d, b = self.o.partial_u32(self._np(keys), offset, width)
         return self._t(d), np.diff(b.astype(np.int64), append=keys.numel())

@@ -92,80 +92,6 @@ def test_round_schedules_over_rccl_single_rank():
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
 
 
-@pytest.mark.parametrize("R,K", [(1, 1), (2, 3), (8, 4), (16, 16), (3, 5)])
-@pytest.mark.parametrize("kind", ["uniform", "skew", "zero", "sparse"])
-def test_plan_kernels_match_torch_planner(R, K, kind):
-    """libsortPlanRounds (the device planner sort_msd uses with HipOps) gives
-    the same table as the torch restatement distrib._plan_rounds_t, and
-    libsortPlanHistogramU32 the same row as sample + histogram + count."""
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    import pylibsort.device as D
-    from pylibsort import distrib
-    rng = np.random.default_rng(R * 100 + K)
-    if kind == "uniform":
-        H = rng.integers(0, 1000, (R, 4096))
-    elif kind == "skew":
-        H = rng.integers(0, 3, (R, 4096))
-        H[:, 77] = 100000
-    elif kind == "zero":
-        H = np.zeros((R, 4096), dtype=np.int64)
-    else:
-        H = np.zeros((R, 4096), dtype=np.int64)
-        H[:, rng.integers(0, 4096, 9)] = rng.integers(1, 5000, (R, 9))
-    rows = torch.from_numpy(np.concatenate([H, np.full((R, 1), 123)], axis=1).astype(np.int64)).cuda()
-    lut, est = D.plan_rounds(rows, R, K)
-    lut_ref, est_ref = distrib._plan_rounds_t(rows[:, :-1], R, K)
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(lut.cpu().numpy(), lut_ref.cpu().numpy())
-    np.testing.assert_array_equal(est.cpu().numpy(), est_ref.round().to(torch.int64).cpu().numpy())
-
-
-@pytest.mark.parametrize("n,stride", [(0, 16), (1000, 16), (1 << 20, 16), ((1 << 22) + 5, 16), ((1 << 20), 1)])
-def test_plan_histogram(n, stride):
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    import pylibsort.device as D
-    from oracle import oracle
-    from pylibsort import distrib
-    x = oracle.pcg(n, first=n)
-    t = torch.from_numpy(x.view(np.int32)).cuda()
-    row = D.plan_histogram_u32(t, block=4096, stride=stride).cpu().numpy()
-    ops = distrib.HipOps()
-    s = ops.sample(t, stride).cpu().numpy().view(np.uint32) if n else x
-    ref = np.bincount(s >> 20, minlength=4096) if n else np.zeros(4096, dtype=np.int64)
-    np.testing.assert_array_equal(row[:4096], ref)
-    assert row[4096] == n
-
-
-def _sampled_ref(x, block, stride):
-    """Keys the plan histogram samples: every stride-th block of `block` keys
-    (all keys when there are fewer than 4 * stride whole blocks)."""
-    nb = x.size // block
-    if stride <= 1 or nb < 4 * stride:
-        return x
-    return np.concatenate([x[sb * stride * block:sb * stride * block + block]
-                           for sb in range(-(-nb // stride))])
-
-
-@pytest.mark.parametrize("n,stride,block,offset", [((1 << 22) + 5, 16, 4096, 1), ((1 << 22) + 3, 16, 4096, 3),
-                                                   ((1 << 21) + 7, 8, 1002, 0), ((1 << 21), 8, 1000, 0),
-                                                   (5000, 4, 64, 1)])
-def test_plan_histogram_layouts(n, stride, block, offset):
-    """The plan histogram's scalar paths: a keys pointer off 16-byte alignment
-    (a slice), block sizes that are not multiples of 4, sampled and unsampled."""
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    import pylibsort.device as D
-    from oracle import oracle
-    x = oracle.pcg(n + offset, first=n)
-    t = torch.from_numpy(x.view(np.int32)).cuda()[offset:]
-    row = D.plan_histogram_u32(t, block=block, stride=stride).cpu().numpy()
-    ref = np.bincount(_sampled_ref(x[offset:], block, stride) >> 20, minlength=4096)
-    np.testing.assert_array_equal(row[:4096], ref)
-    assert row[4096] == n
-
-
 def test_bench_self_launch_rehearsal():
     """bench.py's N>1 path end to end as the driver's 8-GPU job starts it
     (`python bench.py --gpus N`, no launcher: the bench starts
