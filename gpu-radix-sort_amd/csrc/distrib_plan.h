@@ -22,9 +22,6 @@
 namespace lsort {
 namespace dplan {
 
-constexpr int kHistBits = 12;                 // top-bit buckets of the round plan
-constexpr int kHistBins = 1 << kHistBits;     // 4096
-constexpr int kLutShift = 32 - kHistBits;     // bucket = key >> 20
 
 // The reference's equal re-cut: S = ceil(N / R) keys per rank.
 inline uint64_t shard_size(uint64_t N, int R) { return R > 0 ? (N + (uint64_t)R - 1) / (uint64_t)R : 0; }
@@ -48,15 +45,17 @@ inline void add_interval_counts(uint64_t a, uint64_t len, uint64_t S, int R, uin
 // ---------------------------------------------------------------------------
 // round plan ("msd"): contiguous top-12-bit bucket ranges -> (rank, round)
 // ---------------------------------------------------------------------------
-// H: R rows of ld >= 4096 int64 (sampled histograms of the top 12 key bits).
-// lut[b] = round * R + rank for bucket b; est[r] = estimated keys of rank r.
+// H: R rows of ld >= bins int64 (per-rank key counts of `bins` top-bit
+// buckets; the digit rounds pass the 256 exact top-8-bit counts).
+// lut[b] = round * R + rank for bucket b; est[r] = keys of rank r.
 // Bucket b's middle in rank coordinates x = (cum(b) - G(b)/2) / total * R
 // gives rank floor(x); its round is the first i with x - rank < cw[i] (cw =
 // normalised prefix of growth^i); rank * K + round is made monotone over the
-// buckets (cumulative max).  The same arithmetic as the device planner
-// (k_plan_rounds) and pylibsort.distrib._plan_rounds_t.
+// buckets (cumulative max).  The one plan both engines run (pylibsort.distrib
+// through libsortDistribPlanDigits; tests/test_distrib_cpu.py checks it
+// against a numpy restatement).
 inline void plan_rounds(const int64_t* H, int R, size_t ld, int K, double growth, uint8_t* lut, int64_t* est,
-                        int bins = kHistBins) {
+                        int bins) {
   std::vector<double> cw(K);
   double acc = 0.0, p = 1.0;
   for (int i = 0; i < K; ++i) {
