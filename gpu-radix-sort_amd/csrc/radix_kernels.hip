@@ -1435,8 +1435,146 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 #ifndef LIBSORT_BUCKET_ATOMIC0
 #define LIBSORT_BUCKET_ATOMIC0 1
 #endif
+// CNT (32-bit keys only, lbits <= 16; the host picks it): a counting sort on
+// chip instead of the LSD steps, bucket_count_place below.
+//
+// bucket_count_place: the bucket's keys (k, slots past len unused) by their
+// low lbits bits v = (key - bias) mod 2^lbits, in 4096 cells c = the top 12
+// bits of v and, when lbits > 12, rb = lbits - 12 residual bits r.  Each cell
+// is one u64 of 3-bit counts, one per residual value: one LDS atomic per key
+// adds 1 << 3r and returns the key's rank among its equals (equal keys are
+// indistinguishable, so atomic order is as good as any); the block scan of
+// the cell totals leaves the cell start in the top 16 bits, and a key's
+// position is start + the counts of the smaller residuals (three masked
+// popcounts) + its rank.  A 3-bit count that reaches 7 (8+ equal keys) would
+// carry: the bucket then places by u32 cell counters and counts, within its
+// cell, the keys that order before it (the loop below; cells average
+// len / 4096 keys).  lbits <= 12 takes the u32 counters directly (a cell is
+// one value: no loop).  Every key is placed in LDS, then the bucket is written
+// out coalesced.  Measured, uniform 2^28 keys in 2^16 buckets (lbits 16):
+// the 4-step LSD kernel ~1.0 ms, this path ~0.5 ms.
+constexpr int kCntCells = 4096;
+__device__ __forceinline__ uint32_t field3_sum(uint64_t w) {
+  constexpr uint64_t B0 = 0x249249249249ull;  // bit 0 of each 3-bit count (16 of them)
+  return (uint32_t)__popcll(w & B0) + 2u * (uint32_t)__popcll(w & (B0 << 1)) +
+         4u * (uint32_t)__popcll(w & (B0 << 2));
+}
+template <int BLOCK, int ITEMS>
+__device__ __forceinline__ void bucket_count_place(const uint32_t (&k)[ITEMS], uint32_t* s_keys, uint64_t* s_cw,
+                                                   uint32_t* s_wsum, uint32_t* s_flag, uint32_t* out,
+                                                   uint32_t start, uint32_t len, uint32_t lbits, uint32_t bias) {
+  constexpr int PER = kCntCells / BLOCK;
+  static_assert(PER >= 1 && kCntCells % BLOCK == 0, "cells per thread");
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  const uint32_t wbase = w * ITEMS * kWave;
+  const uint32_t rb = lbits > 12 ? lbits - 12 : 0u;
+  const uint32_t lmask = (1u << lbits) - 1u, rmask = (1u << rb) - 1u;
+  // cell c's counter at (c % PER) * BLOCK + c / PER: the PER cells a thread
+  // scans are one LDS column, read and written without bank conflicts
+  auto ci = [&](uint32_t c) -> uint32_t { return (c % PER) * BLOCK + c / PER; };
+  auto val = [&](uint32_t x) -> uint32_t { return (x - bias) & lmask; };
+  uint32_t rk[ITEMS];
+  if (rb > 0) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) s_cw[q * BLOCK + tid] = 0ull;
+    if (tid == 0) *s_flag = 0u;
+    __syncthreads();
+    bool ovf = false;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (wbase + j * kWave + lane < len) {
+        const uint32_t v = val(k[j]), sh = 3u * (v & rmask);
+        const uint64_t old = atomicAdd((unsigned long long*)&s_cw[ci(v >> rb)], 1ull << sh);
+        rk[j] = (uint32_t)(old >> sh) & 7u;
+        ovf |= rk[j] == 7u;
+      }
+    if (__any(ovf) && lane == 0) *s_flag = 1u;
+    __syncthreads();
+    if (!*s_flag) {
+      uint64_t cw[PER];
+      uint32_t sum = 0;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        cw[q] = s_cw[q * BLOCK + tid];
+        sum += field3_sum(cw[q]);
+      }
+      uint32_t total;
+      uint32_t run = block_exclusive_scan<BLOCK>(sum, s_wsum, total);
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        s_cw[q * BLOCK + tid] = cw[q] | ((uint64_t)run << 48);
+        run += field3_sum(cw[q]);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j)
+        if (wbase + j * kWave + lane < len) {
+          const uint32_t v = val(k[j]);
+          const uint64_t c = s_cw[ci(v >> rb)];
+          const uint32_t below = field3_sum(c & ((1ull << (3u * (v & rmask))) - 1ull));
+          s_keys[(uint32_t)(c >> 48) + below + rk[j]] = k[j];
+        }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t p = wbase + j * kWave + lane;
+        if (p < len) out[(size_t)start + p] = s_keys[p];
+      }
+      return;
+    }
+    __syncthreads();  // every wave has read the flag before the counters are reused
+  }
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_cw);  // kCntCells + 1 u32 counters
+  auto cj = [&](uint32_t c) -> uint32_t { return c >= (uint32_t)kCntCells ? (uint32_t)kCntCells : ci(c); };
+#pragma unroll
+  for (int q = 0; q < PER; ++q) s_cnt[q * BLOCK + tid] = 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j)
+    if (wbase + j * kWave + lane < len) rk[j] = atomicAdd(&s_cnt[ci(val(k[j]) >> rb)], 1u);
+  __syncthreads();
+  uint32_t c[PER], sum = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    c[q] = s_cnt[q * BLOCK + tid];
+    sum += c[q];
+  }
+  uint32_t total;
+  uint32_t run = block_exclusive_scan<BLOCK>(sum, s_wsum, total);
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    s_cnt[q * BLOCK + tid] = run;
+    run += c[q];
+  }
+  if (tid == 0) s_cnt[kCntCells] = len;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j)
+    if (wbase + j * kWave + lane < len) s_keys[s_cnt[ci(val(k[j]) >> rb)] + rk[j]] = k[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t p = wbase + j * kWave + lane;
+    if (p < len) {
+      const uint32_t x = s_keys[p];
+      uint32_t fin = p;
+      if (rb > 0) {
+        const uint32_t vx = val(x), cell = vx >> rb;
+        const uint32_t a = s_cnt[cj(cell)], e = s_cnt[cj(cell + 1)];
+        uint32_t less = 0;
+        for (uint32_t q = a; q < e; ++q) {
+          const uint32_t vy = val(s_keys[q]);
+          less += (vy < vx) || (vy == vx && q < p) ? 1u : 0u;
+        }
+        fin = a + less;
+      }
+      out[(size_t)start + fin] = x;
+    }
+  }
+}
+
 template <int BITS, int BLOCK, int ITEMS, typename Op = RadixDigit, typename K = uint32_t, typename V = NoValue,
-          int FIX = 0>
+          int FIX = 0, bool CNT = false>
 __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, const V* vin, V* vout,
                                                        const uint32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ blen,
@@ -1462,6 +1600,9 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
   __shared__ uint16_t s_runs[FIX > 0 ? WAVES : 1][kRunList];
   constexpr bool ATOMIC0 = LIBSORT_BUCKET_ATOMIC0 && !HAS_V && FIX == 0;
   __shared__ uint32_t s_acnt[ATOMIC0 ? WAVES : 1][ATOMIC0 ? RADIX : 1];
+  static_assert(!CNT || (sizeof(K) == 4 && !HAS_V && FIX == 0), "counting path: 32-bit keys only");
+  __shared__ uint64_t s_cw[CNT ? kCntCells : 1];
+  __shared__ uint32_t s_flag;
   if (blockIdx.x >= min(*nb, nb_cap)) return;
   const uint32_t b = ilist ? ilist[blockIdx.x] : blockIdx.x;
   const uint32_t start = bstart[b], len = blen[b];
@@ -1574,6 +1715,10 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
     }
   };
   load();
+  if constexpr (CNT) {
+    bucket_count_place<BLOCK, ITEMS>(k, s_keys, s_cw, s_wsum, &s_flag, out, start, len, lbits, bias);
+    return;
+  }
   if constexpr (FIX > 0) {
     const uint32_t fs = lbits > (uint32_t)FIX ? lbits - FIX : 0u;  // keys equal above fs form the runs
     steps(fs, lbits);
@@ -3131,33 +3276,51 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     // 64-bit keys: on-chip steps over the top 16 of the 48 bucket bits, then
     // the tie fix-up (k_bucket_sort FIX)
     constexpr int FIXB = sizeof(K) == 8 ? LIBSORT_BUCKET64_FIX : 0;
+    // 32-bit keys without values, lbits <= 16: the counting placement
+    // (k_bucket_sort CNT); LIBSORT_BUCKET_COUNT=0 keeps the LSD steps (A/B)
+    constexpr bool kCntOk = sizeof(K) == 4 && std::is_same<V, NoValue>::value;
+    static const bool cnt_on = [] {
+      const char* s = getenv("LIBSORT_BUCKET_COUNT");
+      return !(s && s[0] == '0');
+    }();
+    auto launch = [&](auto cnt_c) -> hipError_t {
+      constexpr bool C = decltype(cnt_c)::value;
 #define LS_BS(I, G, NBP, CAPN, IL, OV, OL)                                                                     \
-  hipLaunchKernelGGL((k_bucket_sort<BITS, BB, ((I) * 256 + BB - 1) / BB, Op, K, V, FIXB>), dim3(G), dim3(BB), 0, st, out, \
-                     out, vout, vout, bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
+  hipLaunchKernelGGL((k_bucket_sort<BITS, BB, ((I) * 256 + BB - 1) / BB, Op, K, V, FIXB, C>), dim3(G), dim3(BB), 0, st, \
+                     out, out, vout, vout, bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
 #define LS_BS2(I)                                          \
   LS_BS(I, NB, ctr + 9, NB, nullptr, ctr + 8, olist);      \
   LS_TRY(hipGetLastError());                               \
   LS_BS(I + 6, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr)
-#define LS_BS512(I, G, NBP, CAPN, IL, OV, OL)                                                                 \
-  hipLaunchKernelGGL((k_bucket_sort<BITS, 512, (I), Op, K, V, FIXB>), dim3(G), dim3(512), 0, st, out, out, vout, vout, \
-                     bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
-    switch (cls) {
-      case 0: LS_BS2(9); break;
-      case 1: LS_BS2(13); break;
-      case 2: LS_BS2(17); break;
-      case 3: LS_BS2(19); break;
-      default:
-        if constexpr (sizeof(K) == 4) {
-          LS_BS512(17, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
-          LS_TRY(hipGetLastError());
-          LS_BS512(23, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
-        }
-        break;
+#define LS_BS512(I, G, NBP, CAPN, IL, OV, OL)                                                                    \
+  hipLaunchKernelGGL((k_bucket_sort<BITS, 512, (I), Op, K, V, FIXB, C>), dim3(G), dim3(512), 0, st, out, out, vout, \
+                     vout, bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
+      switch (cls) {
+        case 0: LS_BS2(9); break;
+        case 1: LS_BS2(13); break;
+        case 2: LS_BS2(17); break;
+        case 3: LS_BS2(19); break;
+        default:
+          if constexpr (sizeof(K) == 4) {
+            LS_BS512(17, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
+            LS_TRY(hipGetLastError());
+            LS_BS512(23, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+          }
+          break;
+      }
+      return hipGetLastError();
+    };
+    if constexpr (kCntOk) {
+      if (cnt_on && lbits <= 16)
+        LS_TRY(launch(std::true_type{}));
+      else
+        LS_TRY(launch(std::false_type{}));
+    } else {
+      LS_TRY(launch(std::false_type{}));
     }
 #undef LS_BS512
 #undef LS_BS2
 #undef LS_BS
-    LS_TRY(hipGetLastError());
   }
   return hipSuccess;
 }
