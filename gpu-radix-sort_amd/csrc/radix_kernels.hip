@@ -1441,17 +1441,19 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 // bucket_count_place: the bucket's keys (k, slots past len unused) by their
 // low lbits bits v = (key - bias) mod 2^lbits, in 4096 cells c = the top 12
 // bits of v and, when lbits > 12, rb = lbits - 12 residual bits r.  Each cell
-// is one u64 of 3-bit counts, one per residual value: one LDS atomic per key
-// adds 1 << 3r and returns the key's rank among its equals (equal keys are
-// indistinguishable, so atomic order is as good as any); the block scan of
-// the cell totals leaves the cell start in the top 16 bits, and a key's
+// is one u64 of 3-bit counts, one per residual value, and the cell's key count
+// in the top 16 bits: one LDS atomic per key adds 1 << 3r + 1 << 48 and
+// returns the key's rank among its equals (equal keys are indistinguishable,
+// so atomic order is as good as any); the block scan of the cell counts
+// replaces them with the cell start, and a key's
 // position is start + the counts of the smaller residuals (three masked
 // popcounts) + its rank.  A 3-bit count that reaches 7 (8+ equal keys) would
 // carry: the bucket then places by u32 cell counters and counts, within its
 // cell, the keys that order before it (the loop below; cells average
 // len / 4096 keys).  lbits <= 12 takes the u32 counters directly (a cell is
-// one value: no loop).  Every key is placed in LDS, then the bucket is written
-// out coalesced.  Measured, uniform 2^28 keys in 2^16 buckets (lbits 16):
+// one value: no loop).  Every key is placed in LDS (over the cell words, once
+// the positions are in registers: 32 KB of LDS per block, not 32 KB + the
+// bucket), then the bucket is written out coalesced.  Measured, uniform 2^28 keys in 2^16 buckets (lbits 16):
 // the 4-step LSD kernel ~1.0 ms, this path ~0.5 ms.
 constexpr int kCntCells = 4096;
 __device__ __forceinline__ uint32_t field3_sum(uint64_t w) {
@@ -1459,10 +1461,14 @@ __device__ __forceinline__ uint32_t field3_sum(uint64_t w) {
   return (uint32_t)__popcll(w & B0) + 2u * (uint32_t)__popcll(w & (B0 << 1)) +
          4u * (uint32_t)__popcll(w & (B0 << 2));
 }
+template <int CAP>
+constexpr int cnt_lds_words() {  // u64 words: the cell words, or the fallback's u32 counters + keys
+  return (8 * kCntCells > 4 * (kCntCells + 1) + 4 * CAP ? 8 * kCntCells : 4 * (kCntCells + 1) + 4 * CAP + 7) / 8;
+}
 template <int BLOCK, int ITEMS>
-__device__ __forceinline__ void bucket_count_place(const uint32_t (&k)[ITEMS], uint32_t* s_keys, uint64_t* s_cw,
-                                                   uint32_t* s_wsum, uint32_t* s_flag, uint32_t* out,
-                                                   uint32_t start, uint32_t len, uint32_t lbits, uint32_t bias) {
+__device__ __forceinline__ void bucket_count_place(const uint32_t (&k)[ITEMS], uint64_t* s_cw, uint32_t* s_wsum,
+                                                   uint32_t* s_flag, uint32_t* out, uint32_t start, uint32_t len,
+                                                   uint32_t lbits, uint32_t bias) {
   constexpr int PER = kCntCells / BLOCK;
   static_assert(PER >= 1 && kCntCells % BLOCK == 0, "cells per thread");
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
@@ -1484,7 +1490,7 @@ __device__ __forceinline__ void bucket_count_place(const uint32_t (&k)[ITEMS], u
     for (int j = 0; j < ITEMS; ++j)
       if (wbase + j * kWave + lane < len) {
         const uint32_t v = val(k[j]), sh = 3u * (v & rmask);
-        const uint64_t old = atomicAdd((unsigned long long*)&s_cw[ci(v >> rb)], 1ull << sh);
+        const uint64_t old = atomicAdd((unsigned long long*)&s_cw[ci(v >> rb)], (1ull << sh) + (1ull << 48));
         rk[j] = (uint32_t)(old >> sh) & 7u;
         ovf |= rk[j] == 7u;
       }
@@ -1496,14 +1502,15 @@ __device__ __forceinline__ void bucket_count_place(const uint32_t (&k)[ITEMS], u
 #pragma unroll
       for (int q = 0; q < PER; ++q) {
         cw[q] = s_cw[q * BLOCK + tid];
-        sum += field3_sum(cw[q]);
+        sum += (uint32_t)(cw[q] >> 48);
       }
       uint32_t total;
       uint32_t run = block_exclusive_scan<BLOCK>(sum, s_wsum, total);
 #pragma unroll
       for (int q = 0; q < PER; ++q) {
-        s_cw[q * BLOCK + tid] = cw[q] | ((uint64_t)run << 48);
-        run += field3_sum(cw[q]);
+        const uint32_t n = (uint32_t)(cw[q] >> 48);
+        s_cw[q * BLOCK + tid] = (cw[q] & 0xFFFFFFFFFFFFull) | ((uint64_t)run << 48);
+        run += n;
       }
       __syncthreads();
 #pragma unroll
@@ -1511,9 +1518,13 @@ __device__ __forceinline__ void bucket_count_place(const uint32_t (&k)[ITEMS], u
         if (wbase + j * kWave + lane < len) {
           const uint32_t v = val(k[j]);
           const uint64_t c = s_cw[ci(v >> rb)];
-          const uint32_t below = field3_sum(c & ((1ull << (3u * (v & rmask))) - 1ull));
-          s_keys[(uint32_t)(c >> 48) + below + rk[j]] = k[j];
+          rk[j] += (uint32_t)(c >> 48) + field3_sum(c & ((1ull << (3u * (v & rmask))) - 1ull));
         }
+      __syncthreads();  // the keys take the words' place
+      uint32_t* s_keys = reinterpret_cast<uint32_t*>(s_cw);
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j)
+        if (wbase + j * kWave + lane < len) s_keys[rk[j]] = k[j];
       __syncthreads();
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
@@ -1524,7 +1535,8 @@ __device__ __forceinline__ void bucket_count_place(const uint32_t (&k)[ITEMS], u
     }
     __syncthreads();  // every wave has read the flag before the counters are reused
   }
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_cw);  // kCntCells + 1 u32 counters
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_cw);  // kCntCells + 1 u32 counters, then the keys
+  uint32_t* s_keys = s_cnt + kCntCells + 1;
   auto cj = [&](uint32_t c) -> uint32_t { return c >= (uint32_t)kCntCells ? (uint32_t)kCntCells : ci(c); };
 #pragma unroll
   for (int q = 0; q < PER; ++q) s_cnt[q * BLOCK + tid] = 0u;
@@ -1592,7 +1604,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
   constexpr uint32_t kRunList = FIX > 0 ? 2 * kWave : 1;  // run starts listed per wave (FIX)
   static_assert(RADIX <= BLOCK && CAP < 65536, "one digit per thread; 16-bit wave counters");
   static_assert(FIX == 0 || (sizeof(K) == 8 && FIX % BITS == 0 && FIX <= 32), "tie fix-up: 64-bit keys");
-  __shared__ K s_keys[CAP];
+  __shared__ K s_keys[CNT ? 1 : CAP];
   __shared__ VS s_vals[HAS_V ? CAP : 1];
   __shared__ WaveCount s_whist[WAVES][RADIX];
   __shared__ WaveCount s_off[RADIX <= kWave ? WAVES : 1][RADIX];
@@ -1601,7 +1613,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
   constexpr bool ATOMIC0 = LIBSORT_BUCKET_ATOMIC0 && !HAS_V && FIX == 0;
   __shared__ uint32_t s_acnt[ATOMIC0 ? WAVES : 1][ATOMIC0 ? RADIX : 1];
   static_assert(!CNT || (sizeof(K) == 4 && !HAS_V && FIX == 0), "counting path: 32-bit keys only");
-  __shared__ uint64_t s_cw[CNT ? kCntCells : 1];
+  __shared__ uint64_t s_cw[CNT ? cnt_lds_words<CAP>() : 1];
   __shared__ uint32_t s_flag;
   if (blockIdx.x >= min(*nb, nb_cap)) return;
   const uint32_t b = ilist ? ilist[blockIdx.x] : blockIdx.x;
@@ -1716,7 +1728,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
   };
   load();
   if constexpr (CNT) {
-    bucket_count_place<BLOCK, ITEMS>(k, s_keys, s_cw, s_wsum, &s_flag, out, start, len, lbits, bias);
+    bucket_count_place<BLOCK, ITEMS>(k, s_cw, s_wsum, &s_flag, out, start, len, lbits, bias);
     return;
   }
   if constexpr (FIX > 0) {

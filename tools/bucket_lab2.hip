@@ -562,6 +562,177 @@ __global__ __launch_bounds__(BLOCK) void k_cntFP(const uint32_t* in, uint32_t* o
   }
 }
 
+// ---- cntG: cntF without per-slot guards: buffer loads/stores bounded by the
+// bucket (out-of-range lanes read 0 / are dropped), slots past len count into
+// a dummy cell word and place into dummy LDS slots ----------------------------
+template <int BLOCK, int ITEMS, int NT = 0>
+__global__ __launch_bounds__(BLOCK) void k_cntG(const uint32_t* in, uint32_t* out, const uint32_t* bstart,
+                                                const uint32_t* blen, const uint32_t* nb, uint32_t lbits) {
+  constexpr int CELLS = 4096, PER = CELLS / BLOCK, WSPAN = ITEMS * kWave, CAP = BLOCK * ITEMS;
+  constexpr int WORDS = (CELLS + 1) > (CAP + kWave + 1) / 2 ? (CELLS + 1) : (CAP + kWave + 1) / 2;
+  __shared__ uint64_t s_w[WORDS];
+  __shared__ uint32_t s_wsum[BLOCK / kWave];
+  __shared__ uint32_t s_ovf;
+  if (blockIdx.x >= *nb) return;
+  const uint32_t b = blockIdx.x, start = bstart[b], len = blen[b];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid / 64;
+  const uint32_t wbase = w * WSPAN;
+  const uint32_t rb = lbits - 12, lmask = (1u << lbits) - 1u, rmask = (1u << rb) - 1u;
+  auto ci = [&](uint32_t c) -> uint32_t { return (c % PER) * BLOCK + c / PER; };
+  const auto rin = __builtin_amdgcn_make_buffer_rsrc((void*)(in + start), 0, len * 4u, 0x00020000);
+  const auto rout = __builtin_amdgcn_make_buffer_rsrc((void*)(out + start), 0, len * 4u, 0x00020000);
+  uint32_t k[ITEMS], rk[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j)
+    k[j] = __builtin_amdgcn_raw_buffer_load_b32(rin, (wbase + j * kWave + lane) * 4u, 0, NT);
+#pragma unroll
+  for (int q = 0; q < PER; ++q) s_w[q * BLOCK + tid] = 0ull;
+  if (tid == 0) {
+    s_ovf = 0u;
+    s_w[CELLS] = 0ull;
+  }
+  __syncthreads();
+  bool ovf = false;
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const bool ok = wbase + j * kWave + lane < len;
+    const uint32_t v = k[j] & lmask, sh = 3u * (v & rmask);
+    const uint64_t old = atomicAdd((unsigned long long*)&s_w[ok ? ci(v >> rb) : (uint32_t)CELLS], 1ull << sh);
+    rk[j] = (uint32_t)(old >> sh) & 7u;
+    ovf |= ok && rk[j] == 7u;
+  }
+  if (__any(ovf) && lane == 0) s_ovf = 1u;
+  __syncthreads();
+  if (s_ovf) return;  // (lab: the dup case is not timed with this kernel)
+  uint64_t wv[PER];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    wv[q] = s_w[q * BLOCK + tid];
+    sum += field3_sum(wv[q]);
+  }
+  uint32_t tot;
+  uint32_t run = block_exclusive_scan<BLOCK>(sum, s_wsum, tot);
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    s_w[q * BLOCK + tid] = wv[q] | ((uint64_t)run << 48);
+    run += field3_sum(wv[q]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const bool ok = wbase + j * kWave + lane < len;
+    const uint32_t v = k[j] & lmask;
+    const uint64_t cw = s_w[ok ? ci(v >> rb) : (uint32_t)CELLS];
+    const uint32_t pos = (uint32_t)(cw >> 48) + field3_sum(cw & ((1ull << (3u * (v & rmask))) - 1ull)) + rk[j];
+    rk[j] = ok ? pos : (uint32_t)CAP + lane;
+  }
+  __syncthreads();
+  uint32_t* s_keys = reinterpret_cast<uint32_t*>(s_w);
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) s_keys[rk[j]] = k[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t p = wbase + j * kWave + lane;
+    __builtin_amdgcn_raw_buffer_store_b32(s_keys[p], rout, p * 4u, 0, NT);
+  }
+}
+
+// ---- cntW: the product's bucket_count_place under a waves-per-EU bound ------
+template <int BLOCK, int ITEMS, int WPE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_cntW(
+    const uint32_t* in, uint32_t* out, const uint32_t* bstart, const uint32_t* blen, const uint32_t* nb,
+    uint32_t lbits) {
+  __shared__ uint64_t s_cw[cnt_lds_words<BLOCK * ITEMS>()];
+  __shared__ uint32_t s_wsum[BLOCK / kWave];
+  __shared__ uint32_t s_flag;
+  if (blockIdx.x >= *nb) return;
+  const uint32_t b = blockIdx.x, start = bstart[b], len = blen[b];
+  const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
+  const uint32_t wbase = w * ITEMS * kWave;
+  uint32_t k[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t i = wbase + j * kWave + lane;
+    k[j] = i < len ? load_stream(&in[(size_t)start + i]) : 0xffffffffu;
+  }
+  bucket_count_place<BLOCK, ITEMS>(k, s_cw, s_wsum, &s_flag, out, start, len, lbits, 0u);
+}
+
+// ---- abl: cntF's phases cut at STAGE (0 copy with the same LDS, 1 + atomics,
+// 2 + scan, 3 + placement = cntF without the fallback) ------------------------
+template <int BLOCK, int ITEMS, int STAGE>
+__global__ __launch_bounds__(BLOCK) void k_abl(const uint32_t* in, uint32_t* out, const uint32_t* bstart,
+                                               const uint32_t* blen, const uint32_t* nb, uint32_t lbits) {
+  constexpr int CELLS = 4096, PER = CELLS / BLOCK, WSPAN = ITEMS * kWave;
+  __shared__ uint64_t s_w[cnt_lds_words<BLOCK * ITEMS>()];
+  __shared__ uint32_t s_wsum[BLOCK / kWave];
+  if (blockIdx.x >= *nb) return;
+  const uint32_t b = blockIdx.x, start = bstart[b], len = blen[b];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid / 64;
+  const uint32_t wbase = w * WSPAN;
+  const uint32_t rb = lbits - 12, lmask = (1u << lbits) - 1u, rmask = (1u << rb) - 1u;
+  auto ci = [&](uint32_t c) -> uint32_t { return (c % PER) * BLOCK + c / PER; };
+  uint32_t k[ITEMS], rk[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t i = wbase + j * kWave + lane;
+    k[j] = i < len ? load_stream(&in[(size_t)start + i]) : 0u;
+    rk[j] = i;
+  }
+  if (STAGE >= 1) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) s_w[q * BLOCK + tid] = 0ull;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (wbase + j * kWave + lane < len) {
+        const uint32_t v = k[j] & lmask, sh = 3u * (v & rmask);
+        const uint64_t old = atomicAdd((unsigned long long*)&s_w[ci(v >> rb)], 1ull << sh);
+        rk[j] = STAGE >= 3 ? (uint32_t)(old >> sh) & 7u : rk[j] + ((uint32_t)(old >> sh) & 7u) * 0u + (uint32_t)(old == 0xffffffffffffull);
+      }
+    __syncthreads();
+  }
+  if (STAGE >= 2) {
+    uint64_t wv[PER];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      wv[q] = s_w[q * BLOCK + tid];
+      sum += field3_sum(wv[q]);
+    }
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan<BLOCK>(sum, s_wsum, tot);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      s_w[q * BLOCK + tid] = wv[q] | ((uint64_t)run << 48);
+      run += field3_sum(wv[q]);
+    }
+    __syncthreads();
+  }
+  if (STAGE >= 3) {
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (wbase + j * kWave + lane < len) {
+        const uint32_t v = k[j] & lmask;
+        const uint64_t cw = s_w[ci(v >> rb)];
+        rk[j] += (uint32_t)(cw >> 48) + field3_sum(cw & ((1ull << (3u * (v & rmask))) - 1ull));
+      }
+    __syncthreads();
+  }
+  uint32_t* s_keys = reinterpret_cast<uint32_t*>(s_w);
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j)
+    if (wbase + j * kWave + lane < len) s_keys[rk[j] < len ? rk[j] : 0] = k[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t p = wbase + j * kWave + lane;
+    if (p < len) out[(size_t)start + p] = s_keys[p];
+  }
+}
+
 // ---- copy: the floor (load, through LDS, store) -----------------------------
 template <int BLOCK, int ITEMS>
 __global__ __launch_bounds__(BLOCK) void k_copy(const uint32_t* in, uint32_t* out, const uint32_t* bstart,
@@ -619,6 +790,61 @@ int main(int argc, char** argv) {
   vs.push_back({"cntF 512x9 lbits=16", 4096, 16, [&](uint32_t m) {
     hipLaunchKernelGGL((k_cntF<512, 9>), dim3(m), dim3(512), 0, st, in, out, bs, bl, nb, 16u);
   }});
+#define PRODC(B, I, S) \
+  vs.push_back({"prodCNT " #B "x" #I " S=" #S, S, 16, [&](uint32_t m) { \
+    hipLaunchKernelGGL((k_bucket_sort<4, B, I, RadixDigit, uint32_t, NoValue, 0, true>), dim3(m), dim3(B), 0, st, in, out, \
+                       (const NoValue*)nullptr, (NoValue*)nullptr, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u); \
+  }});
+  vs.push_back({"cntG 256x17", 4096, 16, [&](uint32_t m) {
+    hipLaunchKernelGGL((k_cntG<256, 17>), dim3(m), dim3(256), 0, st, in, out, bs, bl, nb, 16u);
+  }});
+  vs.push_back({"cntG 512x9", 4096, 16, [&](uint32_t m) {
+    hipLaunchKernelGGL((k_cntG<512, 9>), dim3(m), dim3(512), 0, st, in, out, bs, bl, nb, 16u);
+  }});
+  vs.push_back({"cntG 512x8", 4096, 16, [&](uint32_t m) {
+    hipLaunchKernelGGL((k_cntG<512, 8>), dim3(m), dim3(512), 0, st, in, out, bs, bl, nb, 16u);
+  }});
+  vs.push_back({"cntG 512x9 nt", 4096, 16, [&](uint32_t m) {
+    hipLaunchKernelGGL((k_cntG<512, 9, 2>), dim3(m), dim3(512), 0, st, in, out, bs, bl, nb, 16u);
+  }});
+  vs.push_back({"cntG 512x17 S=8192", 8192, 16, [&](uint32_t m) {
+    hipLaunchKernelGGL((k_cntG<512, 17>), dim3(m), dim3(512), 0, st, in, out, bs, bl, nb, 16u);
+  }});
+#define CNTW(B, I, WPE) \
+  vs.push_back({"cntW " #B "x" #I " wpe=" #WPE, 4096, 16, [&](uint32_t m) { \
+    hipLaunchKernelGGL((k_cntW<B, I, WPE>), dim3(m), dim3(B), 0, st, in, out, bs, bl, nb, 16u); \
+  }});
+  CNTW(512, 8, 1)
+  CNTW(512, 8, 6)
+  CNTW(512, 8, 8)
+  CNTW(256, 17, 1)
+  CNTW(256, 17, 5)
+  CNTW(256, 17, 6)
+  CNTW(256, 16, 6)
+#define ABL(B, I, ST) \
+  vs.push_back({"abl " #B "x" #I " stage=" #ST, 4096, 16, [&](uint32_t m) { \
+    hipLaunchKernelGGL((k_abl<B, I, ST>), dim3(m), dim3(B), 0, st, in, out, bs, bl, nb, 16u); \
+  }});
+  ABL(256, 17, 0) ABL(256, 17, 1) ABL(256, 17, 2) ABL(256, 17, 3)
+  ABL(512, 8, 0) ABL(512, 8, 1) ABL(512, 8, 2) ABL(512, 8, 3)
+  PRODC(256, 17, 4096)
+  PRODC(512, 9, 4096)
+  PRODC(512, 8, 4096)
+  PRODC(1024, 5, 4096)
+  PRODC(512, 17, 8192)
+  PRODC(1024, 9, 8192)
+  vs.push_back({"prodCNT 512x9 dup(ovf)", 4096, 16, [&](uint32_t m) {
+    hipLaunchKernelGGL((k_bucket_sort<4, 512, 9, RadixDigit, uint32_t, NoValue, 0, true>), dim3(m), dim3(512), 0, st, in, out,
+                       (const NoValue*)nullptr, (NoValue*)nullptr, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u);
+  }, 0xf0f0u});
+  for (uint32_t g : {512u, 768u, 1024u, 1536u}) {
+    vs.push_back({"cntFP 512x9 g=" + std::to_string(g), 4096, 16, [&, g](uint32_t m) {
+      hipLaunchKernelGGL((k_cntFP<512, 9>), dim3(std::min(m, g)), dim3(512), 0, st, in, out, bs, bl, nb, 16u);
+    }});
+    vs.push_back({"cntFP 256x17 g=" + std::to_string(g), 4096, 16, [&, g](uint32_t m) {
+      hipLaunchKernelGGL((k_cntFP<256, 17>), dim3(std::min(m, g)), dim3(256), 0, st, in, out, bs, bl, nb, 16u);
+    }});
+  }
   vs.push_back({"cntF 1024x5 lbits=16", 4096, 16, [&](uint32_t m) {
     hipLaunchKernelGGL((k_cntF<1024, 5>), dim3(m), dim3(1024), 0, st, in, out, bs, bl, nb, 16u);
   }});
@@ -676,7 +902,17 @@ int main(int argc, char** argv) {
   }});
   const char* filt = argc > 2 ? argv[2] : nullptr;
   for (auto& v : vs) {
-    if (filt && v.name.find(filt) == std::string::npos) continue;
+    if (filt) {  // comma-separated name substrings
+      bool hit = false;
+      std::string f(filt);
+      for (size_t a = 0; a <= f.size();) {
+        size_t e = f.find(',', a);
+        if (e == std::string::npos) e = f.size();
+        if (e > a && v.name.find(f.substr(a, e - a)) != std::string::npos) hit = true;
+        a = e + 1;
+      }
+      if (!hit) continue;
+    }
     const uint32_t m = (uint32_t)(n / v.S);
     hipLaunchKernelGGL(fill, dim3((n + 255) / 256), dim3(256), 0, st, in, n, v.S, v.lbits, v.dup);
     std::vector<uint32_t> hs(m), hl(m, v.S);
