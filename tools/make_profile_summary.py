@@ -103,14 +103,17 @@ if fetch and write:
 # the bucket sort (the MSD hybrid's last step: one HBM read and write per key)
 fetch, write = pmc("FETCH_SIZE", bucketsort), pmc("WRITE_SIZE", bucketsort)
 bs = []
+bs_name = "k_bucket_sort"
 for f in trace:
     for r in csv.DictReader(open(f)):
         if bucketsort(r):
             bs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            nm = r["Kernel_Name"]
+            bs_name = "k_bucket_sort" + nm[nm.find("<"):nm.find(">") + 1].replace("lsort::", "")
 if fetch and write and bs:
     fr = sum(fetch) / len(fetch) * 1024 * 2
     wr = sum(write) / len(write) * 1024
-    rec = {"kernel": "k_bucket_sort<4, 256, 19> (2^16 buckets of the 2^28-key workload)", "cmd": cmd,
+    rec = {"kernel": "%s (2^16 buckets of the 2^28-key workload)" % bs_name, "cmd": cmd,
            "launches": len(bs), "avg_launch_us": sum(bs) / len(bs), "read_bytes_per_launch": fr,
            "write_bytes_per_launch": wr, "algorithmic_bytes_per_launch": 8.0 * KEYS,
            "method": "same runs as %s_pmc_tilepass.json" % tag, "round": tag}
