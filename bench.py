@@ -388,6 +388,8 @@ def main():
                                           "checked equal to the 4-bit sort"}
         if world == 1 and not args.no_variants and args.workload == "c2":
             variants["lsd"] = lsd_variant(torch, pylibsort, D, keys, out, tmp, max(5, args.steps // 2))
+            variants["bucket_lsd_steps"] = bucket_steps_variant(torch, pylibsort, D, keys, out, tmp,
+                                                                max(5, args.steps // 2))
         if world == 1 and not args.no_variants and not args.no_legs and args.workload == "c2" and args.keys_log2 == 28:
             # the other single-GPU configurations, each with its own live
             # per-kernel timings (never `value`)
@@ -528,6 +530,33 @@ def lsd_variant(torch, pylibsort, D, keys, out, tmp, reps):
             "verified_equal_to_value_sort": same,
             "note": "libsortSetHybrid(0): the LSB radix sort of north_star (%d LSD passes at the line's digit width), "
                     "output checked equal to the hybrid sort's" % (32 // pylibsort.getDigitBits())}
+
+
+def bucket_steps_variant(torch, pylibsort, D, keys, out, tmp, reps):
+    """The same hybrid sort with the bucket sort's 4-bit LSD steps on chip
+    (libsortSetBucketMode(0)) instead of the counting placement (12-bit cells
+    with 4-bit residual counts), timed beside the line and checked equal."""
+    ref = out.clone()
+    lib = pylibsort.lib()
+    prev = lib.libsortSetBucketMode(0)
+    try:
+        for _ in range(2):
+            D.sort_keys_u32(keys, out=out, tmp=tmp)
+        torch.cuda.synchronize()
+        same = bool(torch.equal(out, ref))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            D.sort_keys_u32(keys, out=out, tmp=tmp)
+        torch.cuda.synchronize()
+        ms = 1e3 * (time.perf_counter() - t0) / reps
+    finally:
+        lib.libsortSetBucketMode(prev)
+    if not same:
+        raise RuntimeError("bucket-steps variant disagrees with the line's sort")
+    return {"ms_per_step": round(ms, 4), "value": round(keys.numel() / (ms * 1e-3) / 1e9, 3),
+            "verified_equal_to_value_sort": same,
+            "note": "libsortSetBucketMode(0): the bucket sort as four 4-bit LSD steps on chip (ballot ranks) instead "
+                    "of the counting placement; the same 4 MSD digit passes"}
 
 
 def _cpu_model():

@@ -43,7 +43,7 @@ inline void add_interval_counts(uint64_t a, uint64_t len, uint64_t S, int R, uin
 }
 
 // ---------------------------------------------------------------------------
-// round plan ("msd"): contiguous top-12-bit bucket ranges -> (rank, round)
+// round plan ("msd"): contiguous bucket (top-digit) ranges -> (rank, round)
 // ---------------------------------------------------------------------------
 // H: R rows of ld >= bins int64 (per-rank key counts of `bins` top-bit
 // buckets; the digit rounds pass the 256 exact top-8-bit counts).

@@ -364,6 +364,20 @@ int set_hybrid_mode(int m) {
   return g_hybrid.exchange(m);
 }
 
+// On-chip sort of the hybrid's buckets for 32-bit keys without values:
+// 1 = the counting placement (12-bit cells + 4-bit residual counts), 0 = the
+// 4-bit LSD steps.  Initial value from LIBSORT_BUCKET_COUNT (default 1).
+static int env_bucket_mode() {
+  const char* s = getenv("LIBSORT_BUCKET_COUNT");
+  return (s && s[0] == '0') ? 0 : 1;
+}
+static std::atomic<int> g_bucket_mode{env_bucket_mode()};
+int get_bucket_mode() { return g_bucket_mode.load(std::memory_order_relaxed); }
+int set_bucket_mode(int m) {
+  if (m < 0 || m > 1) return -1;
+  return g_bucket_mode.exchange(m);
+}
+
 int get_algorithm() { return g_algorithm.load(std::memory_order_relaxed); }
 int set_algorithm(int a) {
   if (a < 0 || a > 3) return -1;
@@ -1054,6 +1068,7 @@ LIBSORT_EXPORT int libsortGetDigitBits(void) { return g_digit_bits.load(); }
 
 LIBSORT_EXPORT int libsortSetAlgorithm(int algo) { return set_algorithm(algo); }
 LIBSORT_EXPORT int libsortSetHybrid(int mode) { return set_hybrid_mode(mode); }
+LIBSORT_EXPORT int libsortSetBucketMode(int mode) { return set_bucket_mode(mode); }
 
 LIBSORT_EXPORT int libsortSetBoundaryMode(int mode) {
   if (mode != 0 && mode != 1) return -1;

@@ -187,6 +187,8 @@ int set_algorithm(int algo);  // returns the previous value, -1 if invalid
 // LIBSORT_HYBRID.
 int get_hybrid_mode();
 int set_hybrid_mode(int mode);
+int get_bucket_mode();  // 1 = counting placement in the hybrid's u32 bucket sort, 0 = 4-bit LSD steps
+int set_bucket_mode(int mode);
 
 // Host-side choice of the ping-pong pair for the host ABI: returns true when
 // the result of a `passes`-pass sort started from hbuf[0] lands in hbuf[1].

@@ -3007,7 +3007,8 @@ constexpr size_t kHybMinKeys = 1ull << 27;
 constexpr size_t kHybMinKeys64 = 1ull << 25;
 // (u32 buckets of the top 16 bits: up to ~8.3K keys on average in the
 // 512-thread class; 64-bit keys keep the 2^28 + 2^24 bound of round 2)
-constexpr size_t kHybMaxKeys = (1ull << 29) + (1ull << 23);
+constexpr size_t kHybMaxKeys = (1ull << 30) + (1ull << 24);  // keys only (class 5 above 2^29 + 2^23)
+constexpr size_t kHybMaxKeysPairs = (1ull << 29) + (1ull << 23);
 constexpr size_t kHybMaxKeys64 = (1ull << 28) + (1ull << 24);
 // Range sorts (W bits of key - lo, W < 32: 7 LSD passes at the 8-GPU rounds'
 // W = 27, buckets of W - 16 = 11 bits) gain from fewer keys: the round sorts of
@@ -3106,15 +3107,22 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   const double mean = (double)n / (NB * fill);
   const double need = mean + 3.5 * std::sqrt(mean);
   // class 4 (32-bit keys): 512-thread blocks of 17 keys per thread for
-  // buckets of ~8K keys (full sorts up to 2^29 + 2^23 keys)
+  // buckets of ~8K keys (full sorts up to 2^29 + 2^23 keys); class 5 (32-bit
+  // keys without values, the counting placement only): 1024 x 17 for ~16K
+  // keys (2^30-key sorts: configs[2]); without it such a sort takes the LSD
+  // passes.  libsortSetBucketMode(0) / LIBSORT_BUCKET_COUNT=0 keeps the LSD
+  // steps.
+  constexpr bool kCntOk = sizeof(K) == 4 && std::is_same<V, NoValue>::value;
+  const bool cnt = kCntOk && get_bucket_mode() == 1 && W - BITS * DEPTHS <= 16;
   const int cls = need <= 256.0 * 9 ? 0 : need <= 256.0 * 13 ? 1 : need <= 256.0 * 17 ? 2 :
-                  (need <= 256.0 * 19 || sizeof(K) == 8) ? 3 : 4;
-  static constexpr int kItems1[5] = {9, 13, 17, 19, 34};  // per 256 threads
+                  (need <= 256.0 * 19 || sizeof(K) == 8) ? 3 : need <= 256.0 * 34 ? 4 : 5;
+  if (cls == 5 && !cnt) return hipSuccess;  // (not handled: the LSD sort)
+  static constexpr int kItems1[6] = {9, 13, 17, 19, 34, 68};  // per 256 threads
   // the two blocks' slots (64-bit keys: 512-thread blocks, keys per thread
   // rounded up)
   constexpr int BB = sizeof(K) == 8 ? LIBSORT_BUCKET64_BLOCK : 256;
-  const int BBc = cls == 4 ? 512 : BB;
-  const int extra = cls == 4 ? 12 : 6;  // second block: 6 (12) x 256 more slots
+  const int BBc = cls == 5 ? 1024 : cls == 4 ? 512 : BB;
+  const int extra = cls == 5 ? 24 : cls == 4 ? 12 : 6;  // second block: 6 (12, 24) x 256 more slots
   const uint32_t cap1 = (uint32_t)BBc * (((uint32_t)kItems1[cls] * 256u + BBc - 1) / BBc);
   const uint32_t cap = (uint32_t)BBc * (((uint32_t)(kItems1[cls] + extra) * 256u + BBc - 1) / BBc);
   const uint32_t T0 = pc ? pc->tiles : (uint32_t)((n + TILE - 1) / TILE);
@@ -3289,12 +3297,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     // the tie fix-up (k_bucket_sort FIX)
     constexpr int FIXB = sizeof(K) == 8 ? LIBSORT_BUCKET64_FIX : 0;
     // 32-bit keys without values, lbits <= 16: the counting placement
-    // (k_bucket_sort CNT); LIBSORT_BUCKET_COUNT=0 keeps the LSD steps (A/B)
-    constexpr bool kCntOk = sizeof(K) == 4 && std::is_same<V, NoValue>::value;
-    static const bool cnt_on = [] {
-      const char* s = getenv("LIBSORT_BUCKET_COUNT");
-      return !(s && s[0] == '0');
-    }();
+    // (k_bucket_sort CNT, `cnt` above)
     auto launch = [&](auto cnt_c) -> hipError_t {
       constexpr bool C = decltype(cnt_c)::value;
 #define LS_BS(I, G, NBP, CAPN, IL, OV, OL)                                                                     \
@@ -3307,29 +3310,40 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
 #define LS_BS512(I, G, NBP, CAPN, IL, OV, OL)                                                                    \
   hipLaunchKernelGGL((k_bucket_sort<BITS, 512, (I), Op, K, V, FIXB, C>), dim3(G), dim3(512), 0, st, out, out, vout, \
                      vout, bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
+#define LS_BS1024(I, G, NBP, CAPN, IL, OV, OL)                                                                  \
+  hipLaunchKernelGGL((k_bucket_sort<BITS, 1024, (I), Op, K, V, FIXB, C>), dim3(G), dim3(1024), 0, st, out, out, vout, \
+                     vout, bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
       switch (cls) {
         case 0: LS_BS2(9); break;
         case 1: LS_BS2(13); break;
         case 2: LS_BS2(17); break;
         case 3: LS_BS2(19); break;
-        default:
+        case 4:
           if constexpr (sizeof(K) == 4) {
             LS_BS512(17, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
             LS_TRY(hipGetLastError());
             LS_BS512(23, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
           }
           break;
+        default:
+          if constexpr (C) {
+            LS_BS1024(17, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
+            LS_TRY(hipGetLastError());
+            LS_BS1024(23, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+          }
+          break;
       }
       return hipGetLastError();
     };
     if constexpr (kCntOk) {
-      if (cnt_on && lbits <= 16)
+      if (cnt)
         LS_TRY(launch(std::true_type{}));
       else
         LS_TRY(launch(std::false_type{}));
     } else {
       LS_TRY(launch(std::false_type{}));
     }
+#undef LS_BS1024
 #undef LS_BS512
 #undef LS_BS2
 #undef LS_BS
@@ -3522,7 +3536,7 @@ hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t
   // full-width sorts: the MSD hybrid (stable; the payloads travel with the keys)
   const int hyb = hybrid_mode_for(st);
   if (lo == 0 && hi == 32 && (digit_bits == 8 || digit_bits == 4) &&
-      ((hyb == 1 && n >= kHybMinKeys && n <= kHybMaxKeys) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeys)) &&
+      ((hyb == 1 && n >= kHybMinKeys && n <= kHybMaxKeysPairs) || (hyb == 2 && n >= 1024 && n <= kHybMaxKeysPairs)) &&
       (get_algorithm() == 0 || get_algorithm() == 3) && kin != ktmp) {
     bool handled = false;
     if (digit_bits == 8)

@@ -89,6 +89,7 @@ _SIGS = [
     ("libsortGetDigitBits", ctypes.c_int, []),
     ("libsortSetAlgorithm", ctypes.c_int, [ctypes.c_int]),
     ("libsortSetHybrid", ctypes.c_int, [ctypes.c_int]),
+    ("libsortSetBucketMode", ctypes.c_int, [ctypes.c_int]),
     ("libsortSetBoundaryMode", ctypes.c_int, [ctypes.c_int]),
     ("libsortTimingEnable", None, [ctypes.c_bool]),
     ("libsortTimingReset", None, []),

@@ -303,6 +303,17 @@ LIBSORT_API int libsortSetAlgorithm(int algo);
  * Returns the previous value, or -1 if `mode` is invalid. */
 LIBSORT_API int libsortSetHybrid(int mode);
 
+/* The on-chip sort of the hybrid's buckets for 32-bit keys without values
+ * (each bucket: the keys sharing their top 16 bits, sorted on their low 16
+ * or fewer): 1 (default) = a counting sort in LDS -- 4096 cells by the top 12
+ * of those bits, each holding a 3-bit count per value of the remaining 4
+ * (the last 4-bit digit), one atomic per key, positions from the scanned cell
+ * counts; also lets 2^30-key sorts take the hybrid (buckets of ~16K keys);
+ * 0 = 4-bit LSD steps on chip (ballot ranks), and 2^30-key sorts take the
+ * LSD passes.  Initial value from LIBSORT_BUCKET_COUNT.  Returns the previous
+ * value, or -1 if `mode` is invalid. */
+LIBSORT_API int libsortSetBucketMode(int mode);
+
 /* Boundaries returned by gpuPartial / gpuPartialProfile / gpuPartialSort:
  * 0 (default) = for every group g the number of elements whose group is < g
  * (the exclusive prefix every reference caller and test expects:

@@ -23,6 +23,7 @@ int timing_start(const char*, hipStream_t, uint64_t) { return -1; }
 void timing_stop(int, hipStream_t) {}
 int get_algorithm() { return 3; }
 int get_hybrid_mode() { return 0; }
+int get_bucket_mode() { return 1; }
 }  // namespace lsort
 
 using namespace lsort;
@@ -833,6 +834,9 @@ int main(int argc, char** argv) {
   PRODC(1024, 5, 4096)
   PRODC(512, 17, 8192)
   PRODC(1024, 9, 8192)
+  PRODC(1024, 17, 16384)
+  PRODC(512, 34, 16384)
+  PRODC(512, 32, 16384)
   vs.push_back({"prodCNT 512x9 dup(ovf)", 4096, 16, [&](uint32_t m) {
     hipLaunchKernelGGL((k_bucket_sort<4, 512, 9, RadixDigit, uint32_t, NoValue, 0, true>), dim3(m), dim3(512), 0, st, in, out,
                        (const NoValue*)nullptr, (NoValue*)nullptr, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u);

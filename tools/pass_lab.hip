@@ -18,6 +18,7 @@ int timing_start(const char*, hipStream_t, uint64_t) { return -1; }
 void timing_stop(int, hipStream_t) {}
 int get_algorithm() { return 3; }
 int get_hybrid_mode() { return 0; }
+int get_bucket_mode() { return 1; }
 }  // namespace lsort
 
 using namespace lsort;
