@@ -231,12 +231,18 @@ def main():
 
     engine_note = None
     if cabi:
-        # first step of the C engine; if it fails on rank 0, every rank
-        # switches to the torch engine (identical decision via all_reduce)
+        # first step of the C engine, verified; if it fails or its output is
+        # wrong on rank 0 (distinct-device paths run only on a multi-GPU
+        # node), every rank switches to the torch engine (identical decision
+        # via all_reduce)
         failed = 0
         if rank == 0:
             try:
-                step()
+                first = step()
+                torch.cuda.synchronize()
+                if not args.no_verify and not verify_cabi(torch, shards, first, vshards if pairs else None):
+                    failed, engine_note = 1, "C-ABI engine's first step failed verification; torch engine measured"
+                del first
             except RuntimeError as e:
                 failed, engine_note = 1, "C-ABI engine failed its first step (%s); torch engine measured" % e
         flag = torch.tensor([failed], dtype=torch.int32, device="cuda")

@@ -304,6 +304,9 @@ def segment_copy_u32(src, dst, src_off, dst_off, lens):
     return dst
 
 
+DELTA_GROUP = 64  # keys per coded group (radix_kernels.hip kDeltaGroup)
+
+
 def delta_bits(maxgap):
     """Bit width of the coded gaps for a run whose largest in-group gap is maxgap."""
     return int(maxgap).bit_length()
