@@ -299,7 +299,7 @@ def main():
     barrier()
     D.timing_enable(False)
     kern = query(("whist", "onesweep", "upsweep", "scan", "downsweep", "tilecounts", "colscan", "tilepass",
-                  "hybplan", "bucketsort", "partition", "histogram", "segcopy"))
+                  "hybplan", "bucketsort", "partition", "histogram", "segcopy", "rsvsample"))
     for name in kern:
         kern[name]["from"] = "2 steps after the timed region"
     kern.update({name: dict(v, **{"from": "the timed steps"}) for name, v in timed_pass.items()})

@@ -125,6 +125,12 @@ struct Workspace {
   size_t dstream_cap = 0;  // bytes
   hipError_t ensure_dstream(size_t bytes);
 
+  // MSD hybrid, reserved depth 0: the slices the depth-0 pass writes (the
+  // keys plus each slice's sampled slack; rsv_capacity_bound(n) words)
+  uint32_t* rsv = nullptr;
+  size_t rsv_cap = 0;  // words
+  hipError_t ensure_rsv(size_t words);
+
   hipError_t ensure_counts(size_t m);
   hipError_t ensure_hbuf(size_t bytes);
   hipError_t ensure_bounds(size_t m);

@@ -1114,12 +1114,23 @@ __device__ __forceinline__ uint32_t xcd_tile_of_block() {
 // are D[s * RADIX + d] + the column prefix; and the fused next-digit counts
 // go to the next depth's tiles, cut the same way per child (segment * RADIX +
 // digit): child c starts at ncstart[c] and its first tile is nctile0[c].
+// The slice cursors, kRsvCurStride words apart: every depth-0 tile adds to up
+// to 16 of them, ~1M agent-scope adds per 2^28 keys, and same-line atomics
+// serialise (all 128 cursors in 4 lines: the depth-0 pass took 2.7 ms instead
+// of 0.4).  33 lines apart (an odd line count) puts them on different channels.
+constexpr uint32_t kRsvCurStride = 33 * 32;
 struct HybridGeo {
   const uint4* tiles;        // GEO & 1: this depth's tile table
   const uint32_t* ntiles;    // GEO & 1: this depth's tile count (blocks past it exit)
   const uint32_t* ncstart;   // GEO & 2: next depth's child starts
   const uint32_t* nctile0;   // GEO & 2: next depth's first tile per child
   uint8_t* dout;             // 8-bit passes (any GEO): op_next of every written key at its output position, or null
+  // GEO & 4 (reserved placement, keys-only 4-bit depth 0 without a count
+  // pass; sort_hybrid "Reserved depth 0"): slice e = digit * 8 + range, range
+  // = blockIdx.x & 7 (the tile range xcd_tile_of_block gives those blocks)
+  uint32_t* rcur;            // [RADIX * 8] keys reserved in each slice so far
+  const uint32_t* rslice;    // [3][RADIX * 8] slice start | capacity | first next-depth tile
+  uint32_t* rflag;           // set to 1 when a tile's reservation passed its slice's capacity
 };
 
 // The pass kernel of the tile-offset path: the onesweep tile body with the
@@ -1183,11 +1194,18 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   __shared__ __attribute__((aligned(16))) uint8_t s_lut[OpLds<Op>::bytes];
   constexpr bool ATOMIC_RANK = ANY_ORDER && LIBSORT_HYB_ATOMIC_RANK && !HAS_V;
   __shared__ uint32_t s_acnt[ATOMIC_RANK ? WAVES : 1][ATOMIC_RANK ? RADIX : 1];
+  // GEO & 4: the tile's runs go where it reserves them (an agent-scope add
+  // per digit on its range's slice cursor) instead of where a count pass and
+  // a column scan put them; keys only (any order within a run).
+  constexpr bool RSV = (GEO & 4) != 0;
+  static_assert(!RSV || (FUSE && ANY_ORDER && !HAS_V && (GEO & 3) == 0), "reserved placement: keys-only 4-bit depth 0");
+  __shared__ uint32_t s_over;
 
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int w = tid / kWave;
   const uint32_t t = xcd_tile_of_block();
+  const uint32_t rx = blockIdx.x & 7u;  // RSV: the tile's range (t lies in range rx's tiles)
   uint64_t tile_base;
   uint32_t valid, seg = 0;
   if constexpr ((GEO & 1) != 0) {
@@ -1196,6 +1214,11 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
     tile_base = te.x;
     valid = te.y;
     seg = te.z;
+    if (valid == 0) {  // (reserved depth 0: the tiles past a slice's keys)
+      if constexpr (FUSE)
+        if (tid < RADIX) C[(size_t)t * RADIX + tid] = 0u;  // the C_next of the pass after the next
+      return;
+    }
   } else {
     tile_base = (uint64_t)t * TILE;
     valid = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tile_base);
@@ -1208,8 +1231,16 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
     for (int q = 0; q < NEXT / BLOCK; ++q) s_next[tid + q * BLOCK] = 0u;
   }
   // this tile's run offsets (independent of every other tile)
-  uint32_t gofs = 0, ncs = 0, nct = 0;
-  if (tid < RADIX) {
+  uint32_t gofs = 0, ncs = 0, nct = 0, rcap = 0, rsv = 0;
+  if constexpr (RSV) {
+    if (tid == 0) s_over = 0u;
+    if (tid < RADIX) {
+      const uint32_t e = (uint32_t)tid * 8u + rx;
+      ncs = geo.rslice[e];
+      rcap = geo.rslice[RADIX * 8 + e];
+      nct = geo.rslice[2 * RADIX * 8 + e];
+    }
+  } else if (tid < RADIX) {
     gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid] + D[(size_t)seg * RADIX + tid];
     if constexpr (FUSE) C[(size_t)t * RADIX + tid] = 0u;  // the C_next of the pass after the next
     if constexpr (FUSE && (GEO & 2) != 0) {
@@ -1268,6 +1299,11 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   if (tid < RADIX) {
 #pragma unroll
     for (int i = 0; i < WAVES; ++i) cnt_d += s_whist[i][tid];
+    // RSV: the reservation is issued here and its value first used after the
+    // LDS scatter below (the add's round trip overlaps the scan and scatter)
+    if constexpr (RSV)
+      if (cnt_d) rsv = __hip_atomic_fetch_add(&geo.rcur[((uint32_t)tid * 8u + rx) * kRsvCurStride], cnt_d, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
   }
   uint32_t tile_total;
   const uint32_t excl = block_exclusive_scan<BLOCK>(cnt_d, s_wsum, tile_total);
@@ -1280,7 +1316,9 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
       run += c;
     }
     const uint32_t ob = gofs - excl;
-    if constexpr (FUSE && (GEO & 2) != 0) {
+    if constexpr (RSV) {
+      // (after the scatter)
+    } else if constexpr (FUSE && (GEO & 2) != 0) {
       // next depth's tiles are cut per child: position p of child c is in
       // tile nctile0[c] + (p - ncstart[c]) / TILE
       const uint32_t tl = (gofs - ncs) / TILE;
@@ -1306,7 +1344,27 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
       else if constexpr (HAS_V) s_vals[pos] = v[j];
     }
   }
+  if constexpr (RSV) {
+    if (tid < RADIX) {
+      // the run of digit tid lands at [slice start + rsv, + cnt_d) of its
+      // slice; the next depth's tiles are numbered per slice (capacity)
+      if (cnt_d && rsv + cnt_d > rcap) s_over = 1u;
+      gofs = ncs + rsv;
+      const uint32_t ob = gofs - excl;
+      const uint32_t tl = rsv / TILE;
+      s_ob[tid] = make_uint2(ob, ncs + (tl + 1) * TILE - ob);
+      s_tfirst[tid] = nct + tl;
+    }
+  }
   __syncthreads();
+  if constexpr (RSV) {
+    // a slice overflowed (its sampled capacity was short): this tile writes
+    // nothing, the flag sends the whole sort to the fallback (sort_hybrid)
+    if (s_over) {
+      if (tid == 0) __hip_atomic_fetch_or(geo.rflag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+  }
 
   if constexpr (STAGE_V) {
     // keys (remembering each written position's run base), then the values
@@ -1953,6 +2011,187 @@ __global__ __launch_bounds__(256) void k_hyb_expand(const uint32_t* __restrict__
   tiles[t] = make_uint4(ncstart[lo] + k * TILE, min((uint32_t)TILE, nsize[lo] - k * TILE), lo, 0u);
 }
 
+// ---- Reserved depth 0 (sort_hybrid, keys-only 4-bit sorts without values) ----
+// The depth-0 pass places a tile's digit runs by reserving space in slices
+// (k_tile_pass GEO & 4) instead of reading offsets from a count pass + column
+// scan: one HBM read of the keys less.  Slice e = digit d * 8 + range x, range
+// x = the tiles blocks b with b % 8 == x take (xcd_tile_of_block: contiguous).
+// Its capacity comes from a stratified sample of the range; a tile that finds
+// its slice full writes nothing and raises a flag, and the host then runs the
+// LSD sort from the untouched input (sort_hybrid).
+constexpr int kRsvRanges = 8;
+constexpr int kRsvBlocks = 32;    // sampling blocks per range
+constexpr int kRsvPerThread = 4;  // samples per thread
+constexpr uint32_t kRsvSamples = kRsvBlocks * 256 * kRsvPerThread;  // per range (32768)
+// capacity of a slice with s of S samples over a range of N > S keys:
+// (s + 5 sqrt(s) + 24) * N / S, at most N (a range of <= S keys is counted
+// exactly), rounded up to whole tiles (the next depth's tiles start aligned).
+// Over the 16 slices of a range that is at most N (1 + 20/sqrt(S) + 400/S) +
+// 16 TILE = 1.123 N + 16 TILE, so the slices of n keys fit in
+// rsv_capacity_bound(n) words (TILE = 4096).  A slice overflows when its
+// digit's keys exceed the estimate by 5 sigma (~3e-7 per slice on any input:
+// the strata make the sample at least as good as a random one).
+inline size_t rsv_capacity_bound(size_t n) { return n + n / 8 + n / 64 + 8 * 16 * 4096 + 1024; }
+
+__host__ __device__ inline void rsv_range(uint32_t x, uint32_t tiles, uint32_t tile, uint64_t n, uint64_t* k0,
+                                          uint64_t* k1) {
+  const uint32_t q = tiles >> 3, r = tiles & 7u;
+  const uint64_t t0 = (uint64_t)x * q + (x < r ? x : r), t1 = t0 + q + (x < r ? 1u : 0u);
+  *k0 = t0 * tile < n ? t0 * tile : n;
+  *k1 = t1 * tile < n ? t1 * tile : n;
+}
+
+// Grid kRsvRanges * kRsvBlocks: block (x, j) samples range x, writes its
+// digit counts to part[block][RADIX] (sc1) and zeroes part of the next
+// depth's count rows Czero[0, zero_words); the last block sums the samples,
+// sets each slice's start / capacity / first next-depth tile (rslice), the
+// estimated digit sizes (est[RADIX], for the host's skew check), and zeroes
+// the slice cursors.
+template <int RADIX, int TILE, typename Op>
+__global__ __launch_bounds__(256) void k_rsv_sample(const uint32_t* __restrict__ keys, uint32_t n, uint32_t tiles,
+                                                    Op op, uint32_t* part, uint32_t* __restrict__ rslice,
+                                                    uint32_t* __restrict__ rcur, uint32_t* __restrict__ est,
+                                                    uint32_t* __restrict__ Czero, uint32_t zero_words,
+                                                    uint32_t* ticket, uint32_t* __restrict__ ctr, uint32_t nb,
+                                                    bool short_caps) {
+  static_assert(RADIX * kRsvRanges <= 256, "one slice per thread");
+  __shared__ uint32_t s_h[RADIX];
+  __shared__ uint32_t s_wsum[2][4];
+  __shared__ uint32_t s_flag;
+  __shared__ double s_est[RADIX * kRsvRanges];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t x = blockIdx.x / kRsvBlocks, j = blockIdx.x % kRsvBlocks;
+  for (uint32_t i = (blockIdx.x * 256 + tid) * 4; i < zero_words; i += gridDim.x * 256 * 4)
+    *reinterpret_cast<uint4*>(&Czero[i]) = make_uint4(0u, 0u, 0u, 0u);
+  if (tid < RADIX) s_h[tid] = 0u;
+  __syncthreads();
+  uint64_t k0, k1;
+  rsv_range(x, tiles, TILE, n, &k0, &k1);
+  const uint64_t N = k1 - k0;
+#pragma unroll
+  for (int q = 0; q < kRsvPerThread; ++q) {
+    const uint32_t i = (j * 256 + tid) * kRsvPerThread + q;  // sample i of kRsvSamples
+    uint64_t pos;
+    bool ok;
+    if (N <= kRsvSamples) {
+      pos = k0 + i;  // every key once
+      ok = i < N;
+    } else {
+      // stratum i of the range, a hashed point inside it
+      uint32_t h = (i + 1u) * 0x9E3779B1u ^ (x + 1u) * 0x85EBCA77u;
+      h ^= h >> 15;
+      h *= 0x2C1B3C6Du;
+      h ^= h >> 12;
+      pos = k0 + ((uint64_t)i * N + (((uint64_t)h * N) >> 32)) / kRsvSamples;
+      ok = true;
+    }
+    if (ok) atomicAdd(&s_h[op(keys[pos])], 1u);
+  }
+  __syncthreads();
+  if (tid < RADIX) st_agent(&part[(size_t)blockIdx.x * RADIX + tid], s_h[tid]);
+  if (!last_arriver(ticket, gridDim.x, &s_flag)) return;
+  // slice e = d * 8 + x (thread e)
+  const uint32_t e = tid, d = e / kRsvRanges, xr = e % kRsvRanges;
+  uint32_t cap = 0, ntl = 0;
+  double est_e = 0.0;
+  if (e < (uint32_t)(RADIX * kRsvRanges)) {
+    uint32_t s = 0;
+    for (int b = 0; b < kRsvBlocks; ++b) s += ld_agent(&part[(size_t)(xr * kRsvBlocks + b) * RADIX + d]);
+    uint64_t a0, a1;
+    rsv_range(xr, tiles, TILE, n, &a0, &a1);
+    const uint64_t Nx = a1 - a0;
+    if (Nx <= kRsvSamples) {
+      cap = s;
+      est_e = s;
+    } else {
+      const double w = (double)Nx / kRsvSamples;
+      est_e = s * w;
+      const double c = ((double)s + 5.0 * sqrt((double)s) + 24.0) * w;
+      cap = (uint32_t)min((double)Nx, ceil(c));
+    }
+    if (short_caps) cap /= 2;  // (test knob: half the estimate)
+    ntl = (cap + TILE - 1) / TILE;
+    cap = ntl * TILE;
+  }
+  uint32_t tot_c, tot_t;
+  const uint32_t start = block_exclusive_scan<256>(cap, s_wsum[0], tot_c);
+  const uint32_t tile0 = block_exclusive_scan<256>(ntl, s_wsum[1], tot_t);
+  if (e < (uint32_t)(RADIX * kRsvRanges)) {
+    rslice[e] = start;
+    rslice[RADIX * kRsvRanges + e] = cap;
+    rslice[2 * RADIX * kRsvRanges + e] = tile0;
+    rcur[(size_t)e * kRsvCurStride] = 0u;
+    s_est[e] = est_e;
+  }
+  if (tid == 0) rslice[3 * RADIX * kRsvRanges] = tot_t;
+  __syncthreads();
+  if (tid < RADIX) {
+    double sum = 0.0;
+    for (int r = 0; r < kRsvRanges; ++r) sum += s_est[tid * kRsvRanges + r];
+    // est: the host's pinned mirror (read after the stream event that
+    // follows this kernel; no copy kernel in between)
+    __hip_atomic_store(&est[tid], (uint32_t)min(4294967295.0, sum + 0.5), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (tid < 16) ctr[tid] = tid == 9 ? nb : 0u;  // (k_hyb_init's words)
+  if (tid == 0) *ticket = 0u;
+}
+
+// After the reserved depth-0 pass: the next depth's tile table (per slice,
+// numbered by capacity: slice e's tiles are [tile0[e], tile0[e] + ceil(cap /
+// TILE)), the ones past its keys empty), the children's starts in the next
+// depth's (compact) output, their tile ranges and the tile count.  On
+// overflow (*flag) every tile is empty and the next depth's count rows are
+// zeroed, so the later depths do nothing (the host then sorts from the
+// input).  Grid: ceil(bound / 256), bound = the rows the next depth scans.
+template <int RADIX, int TILE>
+__global__ __launch_bounds__(256) void k_rsv_tiles(const uint32_t* __restrict__ rslice,
+                                                   const uint32_t* __restrict__ rcur, const uint32_t* __restrict__ flag,
+                                                   uint32_t bound, uint4* __restrict__ tiles,
+                                                   uint32_t* __restrict__ cstart, uint32_t* __restrict__ ctile0,
+                                                   uint32_t* __restrict__ ntiles, uint32_t* __restrict__ Czero) {
+  constexpr int NS = RADIX * kRsvRanges;
+  __shared__ uint32_t s_t0[NS + 1];
+  const uint32_t tid = threadIdx.x;
+  const bool over = *flag != 0u;
+  if (tid <= (uint32_t)NS) s_t0[tid] = rslice[2 * NS + tid];  // [NS] = the tile count
+  __syncthreads();
+  const uint32_t total = s_t0[NS];
+  if (blockIdx.x == 0 && tid < RADIX) {
+    uint32_t size = 0, before = 0;
+    for (int x = 0; x < kRsvRanges; ++x) size += over ? 0u : rcur[(tid * kRsvRanges + x) * kRsvCurStride];
+    for (uint32_t d = 0; d < (uint32_t)RADIX; ++d) {
+      uint32_t sz = 0;
+      for (int x = 0; x < kRsvRanges; ++x) sz += over ? 0u : rcur[(d * kRsvRanges + x) * kRsvCurStride];
+      before += d < tid ? sz : 0u;
+    }
+    (void)size;
+    cstart[tid] = before;
+    ctile0[tid] = s_t0[tid * kRsvRanges];
+    if (tid == 0) {
+      ctile0[RADIX] = total;
+      *ntiles = over ? 0u : total;
+    }
+  }
+  const uint32_t t = blockIdx.x * 256 + tid;
+  if (t >= bound) return;
+  if (over) {
+#pragma unroll
+    for (int q = 0; q < RADIX; q += 4)
+      *reinterpret_cast<uint4*>(&Czero[(size_t)t * RADIX + q]) = make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (t >= total) return;
+  uint32_t lo = 0, hi = NS;  // largest e with tile0[e] <= t
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (s_t0[mid] <= t) lo = mid; else hi = mid;
+  }
+  const uint32_t k = t - s_t0[lo];
+  const uint32_t keys = over ? 0u : rcur[(size_t)lo * kRsvCurStride];
+  const uint32_t valid = keys > k * TILE ? min((uint32_t)TILE, keys - k * TILE) : 0u;
+  tiles[t] = make_uint4(rslice[lo] + k * TILE, valid, lo / kRsvRanges, 0u);
+}
+
 // bounds[g] = exclusive scan of window 0 (the whole group when width <= 8).
 __global__ __launch_bounds__(256) void k_bounds_from_window(const uint32_t* __restrict__ whist,
                                                             uint32_t ngroups, uint32_t* __restrict__ bounds) {
@@ -2507,6 +2746,15 @@ hipError_t Workspace::ensure_hybrid(size_t words) {
   return hipSuccess;
 }
 
+hipError_t Workspace::ensure_rsv(size_t words) {
+  if (words <= rsv_cap) return hipSuccess;
+  if (rsv) { (void)hipFree(rsv); rsv = nullptr; }
+  rsv_cap = 0;
+  LS_TRY(hipMalloc(&rsv, words * sizeof(uint32_t)));
+  rsv_cap = words;
+  return hipSuccess;
+}
+
 hipError_t Workspace::ensure_dstream(size_t bytes) {
   bytes = (bytes + 64) & ~(size_t)15;  // the count kernel reads whole 16-byte words
   if (bytes <= dstream_cap) return hipSuccess;
@@ -2551,6 +2799,9 @@ void Workspace::release() {
   if (hyb) (void)hipFree(hyb);
   if (dstream) (void)hipFree(dstream);
   dstream = nullptr;
+  if (rsv) (void)hipFree(rsv);
+  rsv = nullptr;
+  rsv_cap = 0;
   dstream_cap = 0;
   if (hyb_host) (void)hipHostFree(hyb_host);
   hyb = hyb_host = nullptr;
@@ -2726,6 +2977,16 @@ hipError_t tiles_colscan(Workspace& ws, uint32_t* C, uint32_t tiles, hipStream_t
 // per key instead of 8 (c5: 5.21 -> 5.02 ms).  Not for 32-bit keys: the byte
 // stores beside 4-byte keys made the u32 pass 1716 -> 2557 us at 2^30 (c3
 // 10.03 -> 12.29 ms).  LIBSORT_DSTREAM=0 turns it off (A/B).
+// Reserved depth 0 (k_rsv_sample + k_tile_pass GEO & 4): the default for
+// keys-only 4-bit hybrid sorts; LIBSORT_HYB_RESERVE=0 keeps the count pass,
+// =short halves every sampled capacity (tests: the overflow fallback).  Read
+// per call (the tests switch it in process).
+inline int rsv_mode() {
+  const char* s = getenv("LIBSORT_HYB_RESERVE");
+  if (!s) return 1;
+  return s[0] == '0' ? 0 : s[0] == 's' ? 2 : 1;
+}
+
 inline bool dstream_on() {
   static const bool on = [] {
     const char* s = getenv("LIBSORT_DSTREAM");
@@ -3126,15 +3387,24 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   const uint32_t cap1 = (uint32_t)BBc * (((uint32_t)kItems1[cls] * 256u + BBc - 1) / BBc);
   const uint32_t cap = (uint32_t)BBc * (((uint32_t)(kItems1[cls] + extra) * 256u + BBc - 1) / BBc);
   const uint32_t T0 = pc ? pc->tiles : (uint32_t)((n + TILE - 1) / TILE);
+  // reserved depth 0 (keys only, 4-bit, in != out: the fallback re-reads in):
+  // no count pass; depth 0 writes slices of ws.rsv (tile rows of depth 1
+  // numbered by slice capacity, at most tb1)
+  constexpr bool kRsvOk = BITS == 4 && sizeof(K) == 4 && std::is_same<V, NoValue>::value;
+  const int rmode = kRsvOk && !pc && DEPTHS > 1 && (const void*)in != (const void*)out ? rsv_mode() : 0;
+  const bool rsv = rmode != 0;
+  const uint32_t tb1 = (uint32_t)((rsv_capacity_bound(n) + TILE - 1) / TILE) + RADIX * kRsvRanges;
+  if (rsv) LS_TRY(ws.ensure_rsv(rsv_capacity_bound(n) + (size_t)16 * kRsvRanges * kRsvCurStride));
   // segments of depth k (each child has at most one partial tile)
   auto nseg_at = [&](int k) { return nseg0 << (BITS * k); };
-  auto tbound = [&](int k) { return k == 0 ? T0 : T0 + nseg_at(k); };
+  auto tbound = [&](int k) { return k == 0 ? T0 : (k == 1 && rsv) ? tb1 : T0 + nseg_at(k); };
   uint32_t TB = 0;
   for (int k = 0; k < DEPTHS; ++k) TB = std::max(TB, tbound(k));
   LS_TRY(ws.ensure_tiles((size_t)TB * RADIX, ((size_t)tp_chunks(TB, BITS) + 1) * RADIX));
   // hybrid block: tiles[2] | segbase | cstart[2] | nsize | ctile0[2] | ntl | counters
   const size_t w_tiles = (size_t)TB * 4;
-  const size_t words = 2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16 + kListCap;
+  constexpr size_t kRsvWords = kRsvRanges * kRsvBlocks * 16 + 3 * 16 * kRsvRanges + 16;
+  const size_t words = 2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16 + kListCap + kRsvWords;
   LS_TRY(ws.ensure_hybrid(words));
   uint32_t* h = ws.hyb;
   uint4* tiles[2] = {reinterpret_cast<uint4*>(h), reinterpret_cast<uint4*>(h + w_tiles)};
@@ -3149,8 +3419,16 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
                       // [13] largest child of depth 0 (pieces), [14] scratch
   h += 16;
   uint32_t* olist = h;  // the buckets over the first block (kListCap)
-  hipLaunchKernelGGL(k_hyb_init, dim3(1), dim3(64), 0, st, ctr, NB);  // one launch, not two memsets (4 fills)
-  LS_TRY(hipGetLastError());
+  h += kListCap;
+  // reserved depth 0: sample partials | slices (start | capacity | first tile,
+  // + the tile count) | cursors | estimated digit sizes; ctr[14] = overflow
+  uint32_t* rpart = h; h += kRsvRanges * kRsvBlocks * 16;
+  uint32_t* rslice = h; h += 3 * 16 * kRsvRanges + 16;
+  uint32_t* rcur = rsv ? ws.rsv + rsv_capacity_bound(n) : nullptr;  // kRsvCurStride apart
+  if (!rsv) {  // (reserved depth 0: k_rsv_sample sets them)
+    hipLaunchKernelGGL(k_hyb_init, dim3(1), dim3(64), 0, st, ctr, NB);  // one launch, not two memsets (4 fills)
+    LS_TRY(hipGetLastError());
+  }
   if (pc) {
     // depth 0's tile table and parent arrays from the piece table
     const uint32_t g = std::max(T0, pc->nseg + 1);
@@ -3165,7 +3443,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
 
   // keys only: the passes may reorder within a run (k_tile_pass ANY_ORDER)
   constexpr bool kAnyOrder = std::is_same<V, NoValue>::value;
-  auto buf = [&](int k) -> K* { return k == 0 ? const_cast<K*>(in) : ((DEPTHS - k) & 1) ? tmp : out; };
+  auto buf = [&](int k) -> K* {
+    return k == 0 ? const_cast<K*>(in) : (k == 1 && rsv) ? reinterpret_cast<K*>(ws.rsv) : ((DEPTHS - k) & 1) ? tmp : out;
+  };
   auto vbuf = [&](int k) -> V* { return k == 0 ? const_cast<V*>(vin) : ((DEPTHS - k) & 1) ? vtmp : vout; };
   for (int k = 0; k < DEPTHS; ++k) {
     const bool last = k == DEPTHS - 1;
@@ -3181,6 +3461,43 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     K* dst = buf(k + 1);
     const V* vsrc = vbuf(k);
     V* vdst = vbuf(k + 1);
+    if constexpr (kRsvOk) {
+      if (k == 0 && rsv) {
+        // Reserved depth 0: sample -> slices; the pass reserves its runs in
+        // them; the next depth's tiles and child starts from the cursors
+        {
+          ScopedTimer tm("rsvsample", st, n);
+          hipLaunchKernelGGL((k_rsv_sample<RADIX, TILE, Op>), dim3(kRsvRanges * kRsvBlocks), dim3(256), 0, st,
+                             reinterpret_cast<const uint32_t*>(in), (uint32_t)n, T0, op, rpart, rslice, rcur,
+                             ws.hyb_host, Cn, tb1 * (uint32_t)RADIX, ws.tticket + 32, ctr, NB, rmode == 2);
+          LS_TRY(hipGetLastError());
+        }
+        LS_TRY(hipEventRecord(ws.hyb_evt, st));
+        HybridGeo g0{nullptr, nullptr, nullptr, nullptr, nullptr, rcur, rslice, ctr + 14};
+        {
+          ScopedTimer tm("tilepass", st, n);
+          hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, true, Op, Op, 4, true>), dim3(T0), dim3(B), 0, st, src,
+                             dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase, Cn, g0);
+          LS_TRY(hipGetLastError());
+        }
+        {
+          ScopedTimer tm("hybplan", st, m);
+          hipLaunchKernelGGL((k_rsv_tiles<RADIX, TILE>), dim3((tb1 + 255) / 256), dim3(256), 0, st, rslice, rcur,
+                             ctr + 14, tb1, tiles[1], cstart[1], ctile0[1], ctr + 1, Cn);
+          LS_TRY(hipGetLastError());
+        }
+        // skew check on the sampled digit sizes (the pass keeps the GPU busy;
+        // it wrote only ws.rsv, so abandoning leaves in intact)
+        LS_TRY(hipEventSynchronize(ws.hyb_evt));
+        uint32_t mx = 0;
+        for (int d = 0; d < RADIX; ++d) mx = std::max(mx, ws.hyb_host[d]);
+        const double share = (double)n / (RADIX * fill);
+        if ((double)mx > 1.25 * share + 4.0 * std::sqrt(share) + 32.0 ||
+            (double)mx / (double)(NB / RADIX) > 0.9 * cap)
+          return hipSuccess;
+        continue;
+      }
+    }
     // counts of this depth: depth 0 reads the keys (pieces: tile by tile from
     // the table); 4-bit deeper depths were counted by the previous pass
     // (fused); 8-bit deeper depths read the keys tile by tile from the table
@@ -3214,7 +3531,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       LS_TRY(hipGetLastError());
       if (last) {
         // the bucket sizes, read back while the last pass runs
-        LS_TRY(hipMemcpyAsync(ws.hyb_host + 20, ctr + 11, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        LS_TRY(hipMemcpyAsync(ws.hyb_host + 20, ctr + 11, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         LS_TRY(hipEventRecord(ws.hyb_evt, st));
       } else if (pc && k == 0) {
         LS_TRY(hipMemcpyAsync(ws.hyb_host + 24, ctr + 13, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -3230,7 +3547,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
         LS_TRY(hipGetLastError());
       }
     }
-    HybridGeo geo{tiles[k & 1], ctr + k, cstart[(k + 1) & 1], ctile0[(k + 1) & 1], nullptr};
+    HybridGeo geo{tiles[k & 1], ctr + k, cstart[(k + 1) & 1], ctile0[(k + 1) & 1], nullptr, nullptr, nullptr, nullptr};
     if (BITS == 8 && dstream && !last) geo.dout = ws.dstream;  // the next depth's digits
     {
       ScopedTimer tm("tilepass", st, n);
@@ -3280,6 +3597,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   // than the second block, or more buckets over the first than its list
   // holds -> the LSD sort of out (any order sorts) instead of the bucket sort
   LS_TRY(hipEventSynchronize(ws.hyb_evt));
+  // reserved depth 0 overflowed (a slice's sample undercounted it): the
+  // later depths did nothing; the caller's LSD sort from the input instead
+  if (rsv && ws.hyb_host[23]) return hipSuccess;
   *handled = true;
   if (ws.hyb_host[21] > kListCap || ws.hyb_host[20] > cap) {
     // pieces: every bit (the segments' own bits vary across out)

@@ -523,3 +523,57 @@ def test_hybrid_auto_2pow29_class(dev, bits, n):
     assert torch.equal(got, ref)
     del x, out, tmp, ref
     torch.cuda.empty_cache()
+
+
+# ---- Reserved depth 0 (keys-only 4-bit sorts: no count pass; the depth-0
+# pass reserves its runs in sampled slices) ----
+
+@pytest.fixture
+def digit4(dev):
+    import pylibsort
+    prev = pylibsort.setDigitBits(4)
+    yield
+    pylibsort.setDigitBits(prev)
+
+
+@pytest.mark.parametrize("reserve", ["0", "1"])
+@pytest.mark.parametrize("kind", ["pcg", "sorted", "four", "deep_skew", "low16_const", "reverse"])
+@pytest.mark.parametrize("n", [1024, 4097, (1 << 18) + 7, (1 << 22) + 5])
+def test_reserved_depth0(dev, oracle_mod, digit4, force, monkeypatch, reserve, kind, n):
+    """Ranges of <= 32768 keys are counted exactly (n <= 2^18 here, and the
+    empty ranges of a 2-tile input), larger ones sampled; both depth-0 forms
+    give the oracle's output."""
+    monkeypatch.setenv("LIBSORT_HYB_RESERVE", reserve)
+    x = _inputs(kind, n, 11 * n + 3)
+    out, nbs = _sort_counting_buckets(dev, _tensor(x))
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+
+
+@pytest.mark.parametrize("n", [(1 << 22) + 5, (1 << 23) + 1])
+def test_reserved_depth0_overflow_falls_back(dev, oracle_mod, digit4, force, monkeypatch, n):
+    """Slices at half their sampled capacity (LIBSORT_HYB_RESERVE=short; sampled
+    ranges, > 32768 keys each, since capacities are whole tiles): the
+    depth-0 tiles that find their slice full write nothing and raise the
+    flag, the later depths do nothing, and the LSD sort of the untouched input
+    runs instead (no bucket sort)."""
+    monkeypatch.setenv("LIBSORT_HYB_RESERVE", "short")
+    x = oracle_mod.pcg(n, first=n + 99)
+    out, nbs = _sort_counting_buckets(dev, _tensor(x))
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+    assert nbs == 0
+    # the next sort on the same workspace is unaffected
+    monkeypatch.setenv("LIBSORT_HYB_RESERVE", "1")
+    out, nbs = _sort_counting_buckets(dev, _tensor(x))
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+    assert nbs == 1
+
+
+def test_reserved_depth0_range_sort(dev, oracle_mod, digit4, force, monkeypatch):
+    """Range sorts (keys in [lo, lo + span)) take the reserved depth 0 too."""
+    monkeypatch.setenv("LIBSORT_HYB_RESERVE", "1")
+    n = (1 << 21) + 9
+    lo = 0x12345678
+    x = (oracle_mod.pcg(n, first=77) % np.uint32(0x5000000)) + np.uint32(lo)
+    out = dev.sort_keys_range_u32(_tensor(x), lo, lo + 0x5000000)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
