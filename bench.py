@@ -495,20 +495,23 @@ def committed_profile(bytes_per_launch):
 
 def step_roofline(n, digit_bits, ms_per_step, kern):
     """The whole N=1 step against HBM: the bytes the
-    hybrid sort actually moves per step -- one count read (4 B/key), 16 /
+    hybrid sort actually moves per step -- one count read (4 B/key; none with
+    the reserved depth 0), 16 /
     digit_bits digit passes and the bucket sort (read + write, 8 B/key each)
     -- and SURVEY.md section 8(d)'s LSD-equivalent figure (32 / digit_bits
     passes x 8 B/key: 64 B/key at 4-bit digits), each / ms_per_step."""
     passes = 16 // digit_bits if "bucketsort" in kern else 32 // digit_bits
-    actual = n * (4.0 + 8.0 * passes + (8.0 if "bucketsort" in kern else 0.0))
+    count = "tilecounts" in kern  # (4-bit keys-only hybrid: reserved depth 0, no count read)
+    actual = n * ((4.0 if count else 0.0) + 8.0 * passes + (8.0 if "bucketsort" in kern else 0.0))
     lsd_eq = n * 8.0 * (32 // digit_bits)
     t = ms_per_step * 1e-3
     return {"actual_bytes_per_key": actual / n, "actual_gbps": round(actual / t / 1e9, 1),
             "actual_frac": round(actual / t / 1e9 / HBM_PEAK_GBPS, 4),
             "lsd_equivalent_bytes_per_key": lsd_eq / n, "lsd_equivalent_gbps": round(lsd_eq / t / 1e9, 1),
             "lsd_equivalent_frac": round(lsd_eq / t / 1e9 / HBM_PEAK_GBPS, 4),
-            "note": "whole step (ms_per_step): actual = count read + %d digit passes%s; lsd_equivalent = "
-                    "SURVEY 8(d) %d LSD passes x 8 B/key" % (passes, " + bucket sort" if "bucketsort" in kern else "",
+            "note": "whole step (ms_per_step): actual = %s%d digit passes%s; lsd_equivalent = "
+                    "SURVEY 8(d) %d LSD passes x 8 B/key" % ("count read + " if count else "", passes,
+                                                            " + bucket sort" if "bucketsort" in kern else "",
                                                             32 // digit_bits)}
 
 
