@@ -44,16 +44,26 @@ def headline(row):
     """The bench's headline pass: 4-bit keys-only RadixDigit k_tile_pass over
     the 2^28-key workload -- the MSD hybrid's four digit passes, whose grids
     are the 65536 tiles plus at most one partial tile per segment (16, 256,
-    4096 segments at depths 1-3)."""
+    4096 segments at depths 1-3), or at depth 1 after the reserved depth 0
+    the slices' capacity tiles (~75K)."""
     name = row.get("Kernel_Name", "")
     if HEADLINE not in name or "BiasedDigit" in name or "LutDigit" in name:
         return False
-    return KEYS // 4096 <= _groups(row) <= KEYS // 4096 + 4096
+    # the hybrid's passes (ANY_ORDER, the last template argument), not the
+    # LSD variant's (variants.lsd runs after the timed steps)
+    if not name.split(">(")[0].endswith("true"):
+        return False
+    # depth 1 after the reserved depth 0: tiles numbered by slice capacity
+    # (radix_kernels.hip rsv_capacity_bound + one partial tile per slice)
+    rsv_bound = (KEYS + KEYS // 8 + KEYS // 64 + 8 * 16 * 4096 + 1024 + 4095) // 4096 + 128
+    return KEYS // 4096 <= _groups(row) <= max(KEYS // 4096 + 4096, rsv_bound)
 
 
 def bucketsort(row):
+    """The headline's bucket sort: the counting placement (CNT, the last
+    template argument), not variants.bucket_lsd_steps' LSD steps."""
     name = row.get("Kernel_Name", "")
-    return "k_bucket_sort<4," in name and _groups(row) == 65536
+    return "k_bucket_sort<4," in name and name.split(">(")[0].endswith("true") and _groups(row) == 65536
 
 
 trace = sorted(glob.glob(str(src / "stats" / "**" / "*kernel_trace.csv"), recursive=True))
@@ -65,14 +75,18 @@ for f in trace:
 durs.sort()
 if durs:
     us = [d for _, d in durs]
-    steps, per = 20, 4  # the command's timed steps, digit passes per sort (MSD hybrid: 16 bits / 4)
-    timed = us[-steps * per:]
+    # the command's warm-up and timed steps, digit passes per sort (MSD hybrid:
+    # 16 bits / 4); the hybrid's launches in trace order are the warm-up
+    # sorts', the timed sorts', then the later steps' and variants'
+    warm, steps, per = 5, 20, 4
+    timed = us[warm * per:(warm + steps) * per]
     rec = {"kernel": "k_tile_pass<4,...> (4-bit keys-only digit pass of the MSD hybrid, 65536+ tiles)", "cmd": cmd,
            "launches": len(timed), "avg_launch_us": sum(timed) / len(timed),
            "all_launches": len(us), "avg_all_us": sum(us) / len(us),
            "min_us": min(us), "max_us": max(us),
-           "note": "avg_launch_us = the last 80 launches (the 20 timed sorts; the warm-up sorts come first in the "
-                   "trace), avg_all_us includes the warm-up"}
+           "note": "avg_launch_us = launches 21-100 of the hybrid's 4-bit passes in trace order (the 20 timed sorts, "
+                   "after the 5 warm-up sorts' 20); avg_all_us = every such launch (warm-up, timed, the 2 breakdown "
+                   "steps, variants.bucket_lsd_steps)"}
     (dst / ("%s_rocprof_tilepass.json" % tag)).write_text(json.dumps(rec, indent=1) + "\n")
     print(json.dumps(rec))
 
