@@ -1103,10 +1103,11 @@ __global__ __launch_bounds__(256) void k_colscan_wide(uint32_t* __restrict__ B, 
 // and merge there instead of leaving two L2s as partial lines (measured on
 // MI355X: 4-bit pass 467 -> 428 us at 2^28 keys; a 256-run scatter probe
 // 1305 -> 603 us).  A bijection for every grid size.
-__device__ __forceinline__ uint32_t xcd_tile_of_block() {
-  const uint32_t g = gridDim.x, q = g >> 3, r = g & 7u, x = blockIdx.x & 7u, i = blockIdx.x >> 3;
+__device__ __forceinline__ uint32_t xcd_tile_of(uint32_t b, uint32_t g) {
+  const uint32_t q = g >> 3, r = g & 7u, x = b & 7u, i = b >> 3;
   return x * q + min(x, r) + i;
 }
+__device__ __forceinline__ uint32_t xcd_tile_of_block() { return xcd_tile_of(blockIdx.x, gridDim.x); }
 
 // Tile geometry of the MSD hybrid (sort_hybrid_u32): at depth k >= 1 the
 // tiles are cut per segment (the keys sharing their top 4k or 8k bits), so
@@ -1204,22 +1205,23 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int w = tid / kWave;
-  const uint32_t t = xcd_tile_of_block();
   const uint32_t rx = blockIdx.x & 7u;  // RSV: the tile's range (t lies in range rx's tiles)
   uint64_t tile_base;
-  uint32_t valid, seg = 0;
+  uint32_t valid, seg = 0, t, row;  // row: the tile's count row (its table entry's w)
   if constexpr ((GEO & 1) != 0) {
-    if (t >= *geo.ntiles) return;  // past this depth's tiles (the grid is a bound)
+    // the grid is a bound: blocks past this depth's tile count exit, and the
+    // XCD-contiguous map is over the count, so every XCD gets its share
+    const uint32_t g = *geo.ntiles;
+    if (blockIdx.x >= g) return;
+    t = xcd_tile_of(blockIdx.x, g);
     const uint4 te = geo.tiles[t];
     tile_base = te.x;
     valid = te.y;
     seg = te.z;
-    if (valid == 0) {  // (reserved depth 0: the tiles past a slice's keys)
-      if constexpr (FUSE)
-        if (tid < RADIX) C[(size_t)t * RADIX + tid] = 0u;  // the C_next of the pass after the next
-      return;
-    }
+    row = te.w;
   } else {
+    t = xcd_tile_of_block();
+    row = t;
     tile_base = (uint64_t)t * TILE;
     valid = (uint32_t)umin64((uint64_t)TILE, (uint64_t)n - tile_base);
   }
@@ -1241,8 +1243,8 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
       nct = geo.rslice[2 * RADIX * 8 + e];
     }
   } else if (tid < RADIX) {
-    gofs = C[(size_t)t * RADIX + tid] + B[(size_t)(t / CH) * RADIX + tid] + D[(size_t)seg * RADIX + tid];
-    if constexpr (FUSE) C[(size_t)t * RADIX + tid] = 0u;  // the C_next of the pass after the next
+    gofs = C[(size_t)row * RADIX + tid] + B[(size_t)(row / CH) * RADIX + tid] + D[(size_t)seg * RADIX + tid];
+    if constexpr (FUSE) C[(size_t)row * RADIX + tid] = 0u;  // the C_next of the pass after the next
     if constexpr (FUSE && (GEO & 2) != 0) {
       // the next depth's child of digit tid (loaded with the offsets, not
       // after the rank where the block would wait for it)
@@ -2008,7 +2010,7 @@ __global__ __launch_bounds__(256) void k_hyb_expand(const uint32_t* __restrict__
     if (ctile0[mid] <= t) lo = mid; else hi = mid;
   }
   const uint32_t k = t - ctile0[lo];
-  tiles[t] = make_uint4(ncstart[lo] + k * TILE, min((uint32_t)TILE, nsize[lo] - k * TILE), lo, 0u);
+  tiles[t] = make_uint4(ncstart[lo] + k * TILE, min((uint32_t)TILE, nsize[lo] - k * TILE), lo, t);
 }
 
 // ---- Reserved depth 0 (sort_hybrid, keys-only 4-bit sorts without values) ----
@@ -2137,11 +2139,13 @@ __global__ __launch_bounds__(256) void k_rsv_sample(const uint32_t* __restrict__
   if (tid == 0) *ticket = 0u;
 }
 
-// After the reserved depth-0 pass: the next depth's tile table (per slice,
-// numbered by capacity: slice e's tiles are [tile0[e], tile0[e] + ceil(cap /
-// TILE)), the ones past its keys empty), the children's starts in the next
-// depth's (compact) output, their tile ranges and the tile count.  On
-// overflow (*flag) every tile is empty and the next depth's count rows are
+// After the reserved depth-0 pass: the next depth's tile table, the
+// children's starts in the next depth's (compact) output, their tile (row)
+// ranges and the tile count.  The count rows are numbered by slice capacity
+// (slice e's rows [row0[e], row0[e] + ceil(cap / TILE)); the fused counts of
+// depth 0 went there); the table lists only the tiles that hold keys, each
+// with its row (entry w), so no block is spent on the capacity slack.  On
+// overflow (*flag) there are no tiles and the next depth's count rows are
 // zeroed, so the later depths do nothing (the host then sorts from the
 // input).  Grid: ceil(bound / 256), bound = the rows the next depth scans.
 template <int RADIX, int TILE>
@@ -2151,26 +2155,31 @@ __global__ __launch_bounds__(256) void k_rsv_tiles(const uint32_t* __restrict__ 
                                                    uint32_t* __restrict__ cstart, uint32_t* __restrict__ ctile0,
                                                    uint32_t* __restrict__ ntiles, uint32_t* __restrict__ Czero) {
   constexpr int NS = RADIX * kRsvRanges;
-  __shared__ uint32_t s_t0[NS + 1];
+  static_assert(NS < 256, "one slice per thread");
+  __shared__ uint32_t s_row0[NS + 1];  // first count row per slice (capacity), [NS] = rows
+  __shared__ uint32_t s_a0[NS + 1];    // first listed tile per slice, [NS] = tiles
+  __shared__ uint32_t s_keys[NS];
+  __shared__ uint32_t s_wsum[4];
   const uint32_t tid = threadIdx.x;
   const bool over = *flag != 0u;
-  if (tid <= (uint32_t)NS) s_t0[tid] = rslice[2 * NS + tid];  // [NS] = the tile count
+  const uint32_t keys = (tid < (uint32_t)NS && !over) ? rcur[(size_t)tid * kRsvCurStride] : 0u;
+  uint32_t listed;
+  const uint32_t a0 = block_exclusive_scan<256>((keys + TILE - 1) / TILE, s_wsum, listed);
+  if (tid <= (uint32_t)NS) s_row0[tid] = rslice[2 * NS + tid];
+  if (tid < (uint32_t)NS) {
+    s_a0[tid] = a0;
+    s_keys[tid] = keys;
+  }
+  if (tid == 0) s_a0[NS] = listed;
   __syncthreads();
-  const uint32_t total = s_t0[NS];
   if (blockIdx.x == 0 && tid < RADIX) {
-    uint32_t size = 0, before = 0;
-    for (int x = 0; x < kRsvRanges; ++x) size += over ? 0u : rcur[(tid * kRsvRanges + x) * kRsvCurStride];
-    for (uint32_t d = 0; d < (uint32_t)RADIX; ++d) {
-      uint32_t sz = 0;
-      for (int x = 0; x < kRsvRanges; ++x) sz += over ? 0u : rcur[(d * kRsvRanges + x) * kRsvCurStride];
-      before += d < tid ? sz : 0u;
-    }
-    (void)size;
+    uint32_t before = 0;
+    for (uint32_t e = 0; e < tid * kRsvRanges; ++e) before += s_keys[e];
     cstart[tid] = before;
-    ctile0[tid] = s_t0[tid * kRsvRanges];
+    ctile0[tid] = s_row0[tid * kRsvRanges];
     if (tid == 0) {
-      ctile0[RADIX] = total;
-      *ntiles = over ? 0u : total;
+      ctile0[RADIX] = s_row0[NS];
+      *ntiles = listed;
     }
   }
   const uint32_t t = blockIdx.x * 256 + tid;
@@ -2180,16 +2189,15 @@ __global__ __launch_bounds__(256) void k_rsv_tiles(const uint32_t* __restrict__ 
     for (int q = 0; q < RADIX; q += 4)
       *reinterpret_cast<uint4*>(&Czero[(size_t)t * RADIX + q]) = make_uint4(0u, 0u, 0u, 0u);
   }
-  if (t >= total) return;
-  uint32_t lo = 0, hi = NS;  // largest e with tile0[e] <= t
+  if (t >= listed) return;
+  uint32_t lo = 0, hi = NS;  // the slice e with a0[e] <= t < a0[e + 1]
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (s_t0[mid] <= t) lo = mid; else hi = mid;
+    if (s_a0[mid] <= t) lo = mid; else hi = mid;
   }
-  const uint32_t k = t - s_t0[lo];
-  const uint32_t keys = over ? 0u : rcur[(size_t)lo * kRsvCurStride];
-  const uint32_t valid = keys > k * TILE ? min((uint32_t)TILE, keys - k * TILE) : 0u;
-  tiles[t] = make_uint4(rslice[lo] + k * TILE, valid, lo / kRsvRanges, 0u);
+  const uint32_t k = t - s_a0[lo];
+  tiles[t] = make_uint4(rslice[lo] + k * TILE, min((uint32_t)TILE, s_keys[lo] - k * TILE), lo / kRsvRanges,
+                        s_row0[lo] + k);
 }
 
 // bounds[g] = exclusive scan of window 0 (the whole group when width <= 8).
@@ -3333,7 +3341,7 @@ __global__ __launch_bounds__(256) void k_hyb_pieces(const uint4* __restrict__ pi
   }
   const uint4 pc = pieces[lo];
   const uint32_t k = t - pc.w;
-  tiles[t] = make_uint4(pc.x + k * TILE, min((uint32_t)TILE, pc.y - k * TILE), pc.z, 0u);
+  tiles[t] = make_uint4(pc.x + k * TILE, min((uint32_t)TILE, pc.y - k * TILE), pc.z, t);
 }
 
 template <int BITS, typename Op, typename K = uint32_t, typename V = NoValue>
