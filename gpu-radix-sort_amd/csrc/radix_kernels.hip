@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   // per digit on its range's slice cursor) instead of where a count pass and
   // a column scan put them; keys only (any order within a run).
   constexpr bool RSV = (GEO & 4) != 0;
-  static_assert(!RSV || (FUSE && ANY_ORDER && !HAS_V && (GEO & 3) == 0), "reserved placement: keys-only 4-bit depth 0");
+  static_assert(!RSV || (ANY_ORDER && !HAS_V && (GEO & 3) == 0), "reserved placement: keys-only depth 0");
   __shared__ uint32_t s_over;
 
   const int tid = threadIdx.x;
@@ -1353,9 +1353,13 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
       if (cnt_d && rsv + cnt_d > rcap) s_over = 1u;
       gofs = ncs + rsv;
       const uint32_t ob = gofs - excl;
-      const uint32_t tl = rsv / TILE;
-      s_ob[tid] = make_uint2(ob, ncs + (tl + 1) * TILE - ob);
-      s_tfirst[tid] = nct + tl;
+      if constexpr (FUSE) {
+        const uint32_t tl = rsv / TILE;
+        s_ob[tid] = make_uint2(ob, ncs + (tl + 1) * TILE - ob);
+        s_tfirst[tid] = nct + tl;
+      } else {
+        s_ob[tid] = ob;
+      }
     }
   }
   __syncthreads();
@@ -2022,18 +2026,24 @@ __global__ __launch_bounds__(256) void k_hyb_expand(const uint32_t* __restrict__
 // its slice full writes nothing and raises a flag, and the host then runs the
 // LSD sort from the untouched input (sort_hybrid).
 constexpr int kRsvRanges = 8;
-constexpr int kRsvBlocks = 32;    // sampling blocks per range
-constexpr int kRsvPerThread = 4;  // samples per thread
-constexpr uint32_t kRsvSamples = kRsvBlocks * 256 * kRsvPerThread;  // per range (32768)
+constexpr int kRsvBlocks = 32;  // sampling blocks per range
+// samples per thread: 4 for 4-bit digits (32768 per range, ~2048 per slice),
+// 16 for 8-bit (131072 per range, ~512 per slice)
+template <int RADIX> constexpr int rsv_per_thread() { return RADIX >= 256 ? 16 : 4; }
+template <int RADIX> constexpr uint32_t rsv_samples() { return kRsvBlocks * 256 * rsv_per_thread<RADIX>(); }
 // capacity of a slice with s of S samples over a range of N > S keys:
 // (s + 5 sqrt(s) + 24) * N / S, at most N (a range of <= S keys is counted
 // exactly), rounded up to whole tiles (the next depth's tiles start aligned).
-// Over the 16 slices of a range that is at most N (1 + 20/sqrt(S) + 400/S) +
-// 16 TILE = 1.123 N + 16 TILE, so the slices of n keys fit in
-// rsv_capacity_bound(n) words (TILE = 4096).  A slice overflows when its
+// Over the RADIX slices of a range that is at most N (1 + 5 sqrt(RADIX / S) +
+// 25 RADIX / S) + RADIX TILE: 4-bit (S = 32768, TILE = 4096) 1.123 N +
+// 16 TILE, 8-bit (S = 131072, TILE = 8192) 1.270 N + 256 TILE, so the slices
+// of n keys fit in rsv_capacity_bound(n) words.  A slice overflows when its
 // digit's keys exceed the estimate by 5 sigma (~3e-7 per slice on any input:
 // the strata make the sample at least as good as a random one).
-inline size_t rsv_capacity_bound(size_t n) { return n + n / 8 + n / 64 + 8 * 16 * 4096 + 1024; }
+inline size_t rsv_capacity_bound(size_t n, int bits) {
+  return bits == 4 ? n + n / 8 + n / 64 + (size_t)8 * 16 * 4096 + 1024
+                   : n + n / 4 + n / 32 + (size_t)8 * 256 * 8192 + 1024;
+}
 
 __host__ __device__ inline void rsv_range(uint32_t x, uint32_t tiles, uint32_t tile, uint64_t n, uint64_t* k0,
                                           uint64_t* k1) {
@@ -2045,10 +2055,11 @@ __host__ __device__ inline void rsv_range(uint32_t x, uint32_t tiles, uint32_t t
 
 // Grid kRsvRanges * kRsvBlocks: block (x, j) samples range x, writes its
 // digit counts to part[block][RADIX] (sc1) and zeroes part of the next
-// depth's count rows Czero[0, zero_words); the last block sums the samples,
-// sets each slice's start / capacity / first next-depth tile (rslice), the
-// estimated digit sizes (est[RADIX], for the host's skew check), and zeroes
-// the slice cursors.
+// depth's count rows Czero[0, zero_words) (4-bit: the fused counts land
+// there); the last block sums the samples, sets each slice's start /
+// capacity / first next-depth row (rslice), the estimated digit sizes (est,
+// the host's pinned mirror), the hybrid's counter words, and zeroes the
+// slice cursors.  Thread d < RADIX of the last block owns slices d * 8 + x.
 template <int RADIX, int TILE, typename Op>
 __global__ __launch_bounds__(256) void k_rsv_sample(const uint32_t* __restrict__ keys, uint32_t n, uint32_t tiles,
                                                     Op op, uint32_t* part, uint32_t* __restrict__ rslice,
@@ -2056,11 +2067,13 @@ __global__ __launch_bounds__(256) void k_rsv_sample(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ Czero, uint32_t zero_words,
                                                     uint32_t* ticket, uint32_t* __restrict__ ctr, uint32_t nb,
                                                     bool short_caps) {
-  static_assert(RADIX * kRsvRanges <= 256, "one slice per thread");
+  static_assert(RADIX <= 256, "one digit per thread");
+  constexpr int NS = RADIX * kRsvRanges;
+  constexpr int PT = rsv_per_thread<RADIX>();
+  constexpr uint32_t S = rsv_samples<RADIX>();
   __shared__ uint32_t s_h[RADIX];
   __shared__ uint32_t s_wsum[2][4];
   __shared__ uint32_t s_flag;
-  __shared__ double s_est[RADIX * kRsvRanges];
   const uint32_t tid = threadIdx.x;
   const uint32_t x = blockIdx.x / kRsvBlocks, j = blockIdx.x % kRsvBlocks;
   for (uint32_t i = (blockIdx.x * 256 + tid) * 4; i < zero_words; i += gridDim.x * 256 * 4)
@@ -2070,121 +2083,142 @@ __global__ __launch_bounds__(256) void k_rsv_sample(const uint32_t* __restrict__
   uint64_t k0, k1;
   rsv_range(x, tiles, TILE, n, &k0, &k1);
   const uint64_t N = k1 - k0;
+  uint32_t kv[PT];
+  bool ok[PT];
 #pragma unroll
-  for (int q = 0; q < kRsvPerThread; ++q) {
-    const uint32_t i = (j * 256 + tid) * kRsvPerThread + q;  // sample i of kRsvSamples
+  for (int q = 0; q < PT; ++q) {
+    const uint32_t i = (j * 256 + tid) * PT + q;  // sample i of S
     uint64_t pos;
-    bool ok;
-    if (N <= kRsvSamples) {
+    if (N <= S) {
       pos = k0 + i;  // every key once
-      ok = i < N;
+      ok[q] = i < N;
     } else {
       // stratum i of the range, a hashed point inside it
       uint32_t h = (i + 1u) * 0x9E3779B1u ^ (x + 1u) * 0x85EBCA77u;
       h ^= h >> 15;
       h *= 0x2C1B3C6Du;
       h ^= h >> 12;
-      pos = k0 + ((uint64_t)i * N + (((uint64_t)h * N) >> 32)) / kRsvSamples;
-      ok = true;
+      pos = k0 + ((uint64_t)i * N + (((uint64_t)h * N) >> 32)) / S;
+      ok[q] = true;
     }
-    if (ok) atomicAdd(&s_h[op(keys[pos])], 1u);
+    kv[q] = ok[q] ? keys[pos] : 0u;  // (all loads issued before the first atomic)
   }
+#pragma unroll
+  for (int q = 0; q < PT; ++q)
+    if (ok[q]) atomicAdd(&s_h[op(kv[q])], 1u);
   __syncthreads();
   if (tid < RADIX) st_agent(&part[(size_t)blockIdx.x * RADIX + tid], s_h[tid]);
   if (!last_arriver(ticket, gridDim.x, &s_flag)) return;
-  // slice e = d * 8 + x (thread e)
-  const uint32_t e = tid, d = e / kRsvRanges, xr = e % kRsvRanges;
-  uint32_t cap = 0, ntl = 0;
-  double est_e = 0.0;
-  if (e < (uint32_t)(RADIX * kRsvRanges)) {
-    uint32_t s = 0;
-    for (int b = 0; b < kRsvBlocks; ++b) s += ld_agent(&part[(size_t)(xr * kRsvBlocks + b) * RADIX + d]);
-    uint64_t a0, a1;
-    rsv_range(xr, tiles, TILE, n, &a0, &a1);
-    const uint64_t Nx = a1 - a0;
-    if (Nx <= kRsvSamples) {
-      cap = s;
-      est_e = s;
-    } else {
-      const double w = (double)Nx / kRsvSamples;
-      est_e = s * w;
-      const double c = ((double)s + 5.0 * sqrt((double)s) + 24.0) * w;
-      cap = (uint32_t)min((double)Nx, ceil(c));
+  uint32_t cap[kRsvRanges], ntl[kRsvRanges], scap = 0, stl = 0;
+  double est_d = 0.0;
+#pragma unroll
+  for (int xr = 0; xr < kRsvRanges; ++xr) {
+    cap[xr] = ntl[xr] = 0u;
+    if (tid < (uint32_t)RADIX) {
+      uint32_t sc = 0;
+      for (int b = 0; b < kRsvBlocks; ++b) sc += ld_agent(&part[(size_t)(xr * kRsvBlocks + b) * RADIX + tid]);
+      uint64_t a0, a1;
+      rsv_range(xr, tiles, TILE, n, &a0, &a1);
+      const uint64_t Nx = a1 - a0;
+      uint32_t c;
+      if (Nx <= S) {
+        c = sc;
+        est_d += sc;
+      } else {
+        const double w = (double)Nx / S;
+        est_d += sc * w;
+        c = (uint32_t)min((double)Nx, ceil(((double)sc + 5.0 * sqrt((double)sc) + 24.0) * w));
+      }
+      if (short_caps) c /= 2;  // (test knob: half the estimate)
+      ntl[xr] = (c + TILE - 1) / TILE;
+      cap[xr] = ntl[xr] * TILE;
+      scap += cap[xr];
+      stl += ntl[xr];
     }
-    if (short_caps) cap /= 2;  // (test knob: half the estimate)
-    ntl = (cap + TILE - 1) / TILE;
-    cap = ntl * TILE;
   }
   uint32_t tot_c, tot_t;
-  const uint32_t start = block_exclusive_scan<256>(cap, s_wsum[0], tot_c);
-  const uint32_t tile0 = block_exclusive_scan<256>(ntl, s_wsum[1], tot_t);
-  if (e < (uint32_t)(RADIX * kRsvRanges)) {
-    rslice[e] = start;
-    rslice[RADIX * kRsvRanges + e] = cap;
-    rslice[2 * RADIX * kRsvRanges + e] = tile0;
-    rcur[(size_t)e * kRsvCurStride] = 0u;
-    s_est[e] = est_e;
-  }
-  if (tid == 0) rslice[3 * RADIX * kRsvRanges] = tot_t;
-  __syncthreads();
-  if (tid < RADIX) {
-    double sum = 0.0;
-    for (int r = 0; r < kRsvRanges; ++r) sum += s_est[tid * kRsvRanges + r];
+  uint32_t start = block_exclusive_scan<256>(scap, s_wsum[0], tot_c);
+  uint32_t row0 = block_exclusive_scan<256>(stl, s_wsum[1], tot_t);
+  if (tid < (uint32_t)RADIX) {
+#pragma unroll
+    for (int xr = 0; xr < kRsvRanges; ++xr) {
+      const uint32_t e = tid * kRsvRanges + xr;
+      rslice[e] = start;
+      rslice[NS + e] = cap[xr];
+      rslice[2 * NS + e] = row0;
+      rcur[(size_t)e * kRsvCurStride] = 0u;
+      start += cap[xr];
+      row0 += ntl[xr];
+    }
     // est: the host's pinned mirror (read after the stream event that
     // follows this kernel; no copy kernel in between)
-    __hip_atomic_store(&est[tid], (uint32_t)min(4294967295.0, sum + 0.5), __ATOMIC_RELAXED,
+    __hip_atomic_store(&est[tid], (uint32_t)min(4294967295.0, est_d + 0.5), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  if (tid == 0) rslice[3 * NS] = tot_t;
   if (tid < 16) ctr[tid] = tid == 9 ? nb : 0u;  // (k_hyb_init's words)
   if (tid == 0) *ticket = 0u;
 }
 
 // After the reserved depth-0 pass: the next depth's tile table, the
 // children's starts in the next depth's (compact) output, their tile (row)
-// ranges and the tile count.  The count rows are numbered by slice capacity
-// (slice e's rows [row0[e], row0[e] + ceil(cap / TILE)); the fused counts of
-// depth 0 went there); the table lists only the tiles that hold keys, each
-// with its row (entry w), so no block is spent on the capacity slack.  On
-// overflow (*flag) there are no tiles and the next depth's count rows are
-// zeroed, so the later depths do nothing (the host then sorts from the
-// input).  Grid: ceil(bound / 256), bound = the rows the next depth scans.
-template <int RADIX, int TILE>
+// ranges and the tile count.  FUSED (4-bit): the count rows are numbered by
+// slice capacity (slice e's rows [row0[e], row0[e] + ceil(cap / TILE)); the
+// fused counts of depth 0 went there), each listed tile carries its row
+// (entry w); otherwise (8-bit: the next depth's counts are read from the
+// table) row = the tile's index.  Only the tiles that hold keys are listed,
+// so no block is spent on the capacity slack.  On overflow (*flag) there are
+// no tiles and (FUSED) the next depth's count rows are zeroed, so the later
+// depths do nothing (the host then sorts from the input).  Grid: ceil(bound
+// / 256), bound = the rows the next depth scans.
+template <int RADIX, int TILE, bool FUSED>
 __global__ __launch_bounds__(256) void k_rsv_tiles(const uint32_t* __restrict__ rslice,
                                                    const uint32_t* __restrict__ rcur, const uint32_t* __restrict__ flag,
                                                    uint32_t bound, uint4* __restrict__ tiles,
                                                    uint32_t* __restrict__ cstart, uint32_t* __restrict__ ctile0,
                                                    uint32_t* __restrict__ ntiles, uint32_t* __restrict__ Czero) {
   constexpr int NS = RADIX * kRsvRanges;
-  static_assert(NS < 256, "one slice per thread");
+  static_assert(RADIX <= 256, "one digit per thread");
   __shared__ uint32_t s_row0[NS + 1];  // first count row per slice (capacity), [NS] = rows
   __shared__ uint32_t s_a0[NS + 1];    // first listed tile per slice, [NS] = tiles
   __shared__ uint32_t s_keys[NS];
-  __shared__ uint32_t s_wsum[4];
+  __shared__ uint32_t s_wsum[2][4];
   const uint32_t tid = threadIdx.x;
   const bool over = *flag != 0u;
-  const uint32_t keys = (tid < (uint32_t)NS && !over) ? rcur[(size_t)tid * kRsvCurStride] : 0u;
-  uint32_t listed;
-  const uint32_t a0 = block_exclusive_scan<256>((keys + TILE - 1) / TILE, s_wsum, listed);
-  if (tid <= (uint32_t)NS) s_row0[tid] = rslice[2 * NS + tid];
-  if (tid < (uint32_t)NS) {
-    s_a0[tid] = a0;
-    s_keys[tid] = keys;
+  uint32_t keys[kRsvRanges], nl = 0, dk = 0;
+#pragma unroll
+  for (int xr = 0; xr < kRsvRanges; ++xr) {
+    const uint32_t e = tid * kRsvRanges + xr;
+    keys[xr] = (tid < (uint32_t)RADIX && !over) ? rcur[(size_t)e * kRsvCurStride] : 0u;
+    nl += (keys[xr] + TILE - 1) / TILE;
+    dk += keys[xr];
+  }
+  uint32_t listed, total_keys;
+  uint32_t a0 = block_exclusive_scan<256>(nl, s_wsum[0], listed);
+  const uint32_t before = block_exclusive_scan<256>(dk, s_wsum[1], total_keys);
+  for (uint32_t e = tid; e <= (uint32_t)NS; e += 256) s_row0[e] = rslice[2 * NS + e];
+  if (tid < (uint32_t)RADIX) {
+#pragma unroll
+    for (int xr = 0; xr < kRsvRanges; ++xr) {
+      const uint32_t e = tid * kRsvRanges + xr;
+      s_a0[e] = a0;
+      s_keys[e] = keys[xr];
+      a0 += (keys[xr] + TILE - 1) / TILE;
+    }
   }
   if (tid == 0) s_a0[NS] = listed;
   __syncthreads();
-  if (blockIdx.x == 0 && tid < RADIX) {
-    uint32_t before = 0;
-    for (uint32_t e = 0; e < tid * kRsvRanges; ++e) before += s_keys[e];
+  if (blockIdx.x == 0 && tid < (uint32_t)RADIX) {
     cstart[tid] = before;
-    ctile0[tid] = s_row0[tid * kRsvRanges];
+    ctile0[tid] = FUSED ? s_row0[tid * kRsvRanges] : s_a0[tid * kRsvRanges];
     if (tid == 0) {
-      ctile0[RADIX] = s_row0[NS];
+      ctile0[RADIX] = FUSED ? s_row0[NS] : listed;  // (RADIX may equal the block: not thread RADIX's)
       *ntiles = listed;
     }
   }
   const uint32_t t = blockIdx.x * 256 + tid;
   if (t >= bound) return;
-  if (over) {
+  if (FUSED && over) {
 #pragma unroll
     for (int q = 0; q < RADIX; q += 4)
       *reinterpret_cast<uint4*>(&Czero[(size_t)t * RADIX + q]) = make_uint4(0u, 0u, 0u, 0u);
@@ -2197,7 +2231,7 @@ __global__ __launch_bounds__(256) void k_rsv_tiles(const uint32_t* __restrict__ 
   }
   const uint32_t k = t - s_a0[lo];
   tiles[t] = make_uint4(rslice[lo] + k * TILE, min((uint32_t)TILE, s_keys[lo] - k * TILE), lo / kRsvRanges,
-                        s_row0[lo] + k);
+                        FUSED ? s_row0[lo] + k : t);
 }
 
 // bounds[g] = exclusive scan of window 0 (the whole group when width <= 8).
@@ -3398,11 +3432,11 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   // reserved depth 0 (keys only, 4-bit, in != out: the fallback re-reads in):
   // no count pass; depth 0 writes slices of ws.rsv (tile rows of depth 1
   // numbered by slice capacity, at most tb1)
-  constexpr bool kRsvOk = BITS == 4 && sizeof(K) == 4 && std::is_same<V, NoValue>::value;
+  constexpr bool kRsvOk = sizeof(K) == 4 && std::is_same<V, NoValue>::value;
   const int rmode = kRsvOk && !pc && DEPTHS > 1 && (const void*)in != (const void*)out ? rsv_mode() : 0;
   const bool rsv = rmode != 0;
-  const uint32_t tb1 = (uint32_t)((rsv_capacity_bound(n) + TILE - 1) / TILE) + RADIX * kRsvRanges;
-  if (rsv) LS_TRY(ws.ensure_rsv(rsv_capacity_bound(n) + (size_t)16 * kRsvRanges * kRsvCurStride));
+  const uint32_t tb1 = (uint32_t)((rsv_capacity_bound(n, BITS) + TILE - 1) / TILE) + RADIX * kRsvRanges;
+  if (rsv) LS_TRY(ws.ensure_rsv(rsv_capacity_bound(n, BITS) + (size_t)RADIX * kRsvRanges * kRsvCurStride));
   // segments of depth k (each child has at most one partial tile)
   auto nseg_at = [&](int k) { return nseg0 << (BITS * k); };
   auto tbound = [&](int k) { return k == 0 ? T0 : (k == 1 && rsv) ? tb1 : T0 + nseg_at(k); };
@@ -3411,7 +3445,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   LS_TRY(ws.ensure_tiles((size_t)TB * RADIX, ((size_t)tp_chunks(TB, BITS) + 1) * RADIX));
   // hybrid block: tiles[2] | segbase | cstart[2] | nsize | ctile0[2] | ntl | counters
   const size_t w_tiles = (size_t)TB * 4;
-  constexpr size_t kRsvWords = kRsvRanges * kRsvBlocks * 16 + 3 * 16 * kRsvRanges + 16;
+  constexpr size_t kRsvWords = kRsvRanges * kRsvBlocks * RADIX + 3 * RADIX * kRsvRanges + 16;
   const size_t words = 2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16 + kListCap + kRsvWords;
   LS_TRY(ws.ensure_hybrid(words));
   uint32_t* h = ws.hyb;
@@ -3430,9 +3464,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   h += kListCap;
   // reserved depth 0: sample partials | slices (start | capacity | first tile,
   // + the tile count) | cursors | estimated digit sizes; ctr[14] = overflow
-  uint32_t* rpart = h; h += kRsvRanges * kRsvBlocks * 16;
-  uint32_t* rslice = h; h += 3 * 16 * kRsvRanges + 16;
-  uint32_t* rcur = rsv ? ws.rsv + rsv_capacity_bound(n) : nullptr;  // kRsvCurStride apart
+  uint32_t* rpart = h; h += kRsvRanges * kRsvBlocks * RADIX;
+  uint32_t* rslice = h; h += 3 * RADIX * kRsvRanges + 16;
+  uint32_t* rcur = rsv ? ws.rsv + rsv_capacity_bound(n, BITS) : nullptr;  // kRsvCurStride apart
   if (!rsv) {  // (reserved depth 0: k_rsv_sample sets them)
     hipLaunchKernelGGL(k_hyb_init, dim3(1), dim3(64), 0, st, ctr, NB);  // one launch, not two memsets (4 fills)
     LS_TRY(hipGetLastError());
@@ -3477,21 +3511,22 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
           ScopedTimer tm("rsvsample", st, n);
           hipLaunchKernelGGL((k_rsv_sample<RADIX, TILE, Op>), dim3(kRsvRanges * kRsvBlocks), dim3(256), 0, st,
                              reinterpret_cast<const uint32_t*>(in), (uint32_t)n, T0, op, rpart, rslice, rcur,
-                             ws.hyb_host, Cn, tb1 * (uint32_t)RADIX, ws.tticket + 32, ctr, NB, rmode == 2);
+                             ws.hyb_host, Cn, BITS == 4 ? tb1 * (uint32_t)RADIX : 0u, ws.tticket + 32, ctr, NB,
+                             rmode == 2);
           LS_TRY(hipGetLastError());
         }
         LS_TRY(hipEventRecord(ws.hyb_evt, st));
         HybridGeo g0{nullptr, nullptr, nullptr, nullptr, nullptr, rcur, rslice, ctr + 14};
         {
           ScopedTimer tm("tilepass", st, n);
-          hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, true, Op, Op, 4, true>), dim3(T0), dim3(B), 0, st, src,
-                             dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase, Cn, g0);
+          hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 4, true>), dim3(T0), dim3(B), 0, st,
+                             src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase, Cn, g0);
           LS_TRY(hipGetLastError());
         }
         {
           ScopedTimer tm("hybplan", st, m);
-          hipLaunchKernelGGL((k_rsv_tiles<RADIX, TILE>), dim3((tb1 + 255) / 256), dim3(256), 0, st, rslice, rcur,
-                             ctr + 14, tb1, tiles[1], cstart[1], ctile0[1], ctr + 1, Cn);
+          hipLaunchKernelGGL((k_rsv_tiles<RADIX, TILE, BITS == 4>), dim3((tb1 + 255) / 256), dim3(256), 0, st, rslice,
+                             rcur, ctr + 14, tb1, tiles[1], cstart[1], ctile0[1], ctr + 1, Cn);
           LS_TRY(hipGetLastError());
         }
         // skew check on the sampled digit sizes (the pass keeps the GPU busy;

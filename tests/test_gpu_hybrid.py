@@ -536,6 +536,14 @@ def digit4(dev):
     pylibsort.setDigitBits(prev)
 
 
+@pytest.fixture
+def digit8(dev):
+    import pylibsort
+    prev = pylibsort.setDigitBits(8)
+    yield
+    pylibsort.setDigitBits(prev)
+
+
 @pytest.mark.parametrize("reserve", ["0", "1"])
 @pytest.mark.parametrize("kind", ["pcg", "sorted", "four", "deep_skew", "low16_const", "reverse"])
 @pytest.mark.parametrize("n", [1024, 4097, (1 << 18) + 7, (1 << 22) + 5])
@@ -566,6 +574,28 @@ def test_reserved_depth0_overflow_falls_back(dev, oracle_mod, digit4, force, mon
     out, nbs = _sort_counting_buckets(dev, _tensor(x))
     np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
     assert nbs == 1
+
+
+@pytest.mark.parametrize("reserve", ["0", "1"])
+@pytest.mark.parametrize("kind", ["pcg", "sorted", "four", "low16_const"])
+@pytest.mark.parametrize("n", [1024, 8193, (1 << 20) + 7, (1 << 23) + 5])
+def test_reserved_depth0_digit8(dev, oracle_mod, digit8, force, monkeypatch, reserve, kind, n):
+    """8-bit digits: 2048 slices (256 digits x 8 ranges), 131072 samples per
+    range (ranges of <= 131072 keys counted exactly); the next depth's counts
+    are read from its (compacted) tile table."""
+    monkeypatch.setenv("LIBSORT_HYB_RESERVE", reserve)
+    x = _inputs(kind, n, 13 * n + 1)
+    out, nbs = _sort_counting_buckets(dev, _tensor(x))
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+
+
+def test_reserved_depth0_digit8_overflow_falls_back(dev, oracle_mod, digit8, force, monkeypatch):
+    monkeypatch.setenv("LIBSORT_HYB_RESERVE", "short")
+    n = (1 << 26) + 1  # slices of ~32K keys: half of it, in whole 8192-key tiles, is short
+    x = oracle_mod.pcg(n, first=n + 7)
+    out, nbs = _sort_counting_buckets(dev, _tensor(x))
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+    assert nbs == 0
 
 
 def test_reserved_depth0_range_sort(dev, oracle_mod, digit4, force, monkeypatch):
