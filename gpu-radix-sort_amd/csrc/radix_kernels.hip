@@ -1120,6 +1120,14 @@ __device__ __forceinline__ uint32_t xcd_tile_of_block() { return xcd_tile_of(blo
 // serialise (all 128 cursors in 4 lines: the depth-0 pass took 2.7 ms instead
 // of 0.4).  33 lines apart (an odd line count) puts them on different channels.
 constexpr uint32_t kRsvCurStride = 33 * 32;
+// Word of slice e = digit * 8 + range's cursor.  8-bit digits: digits 2i and
+// 2i + 1 of a range share one 64-bit word (low / high half), so a tile makes
+// 128 adds instead of 256 (the halves never carry: a slice holds < 2^32 keys).
+__host__ __device__ inline size_t rsv_cur_index(uint32_t e, int radix) {
+  if (radix < 256) return (size_t)e * kRsvCurStride;
+  const uint32_t d = e / 8u, x = e % 8u;
+  return ((size_t)(d >> 1) * 8u + x) * kRsvCurStride + (d & 1u);
+}
 struct HybridGeo {
   const uint4* tiles;        // GEO & 1: this depth's tile table
   const uint32_t* ntiles;    // GEO & 1: this depth's tile count (blocks past it exit)
@@ -1234,6 +1242,7 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   }
   // this tile's run offsets (independent of every other tile)
   uint32_t gofs = 0, ncs = 0, nct = 0, rcap = 0, rsv = 0;
+  unsigned long long rsv64 = 0;  // RSV, 8-bit: the old value of an even digit's pair word
   if constexpr (RSV) {
     if (tid == 0) s_over = 0u;
     if (tid < RADIX) {
@@ -1303,9 +1312,19 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
     for (int i = 0; i < WAVES; ++i) cnt_d += s_whist[i][tid];
     // RSV: the reservation is issued here and its value first used after the
     // LDS scatter below (the add's round trip overlaps the scan and scatter)
-    if constexpr (RSV)
-      if (cnt_d) rsv = __hip_atomic_fetch_add(&geo.rcur[((uint32_t)tid * 8u + rx) * kRsvCurStride], cnt_d, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (RSV) {
+      if constexpr (RADIX >= 256) {
+        // (waves 0 .. RADIX / 64 - 1 whole: every lane takes part)
+        const uint32_t odd = __shfl_down(cnt_d, 1);
+        if ((tid & 1) == 0 && (cnt_d | odd))
+          rsv64 = __hip_atomic_fetch_add(
+              reinterpret_cast<unsigned long long*>(&geo.rcur[rsv_cur_index((uint32_t)tid * 8u + rx, RADIX)]),
+              (unsigned long long)cnt_d | ((unsigned long long)odd << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else if (cnt_d) {
+        rsv = __hip_atomic_fetch_add(&geo.rcur[rsv_cur_index((uint32_t)tid * 8u + rx, RADIX)], cnt_d,
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
   uint32_t tile_total;
   const uint32_t excl = block_exclusive_scan<BLOCK>(cnt_d, s_wsum, tile_total);
@@ -1347,6 +1366,11 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
     }
   }
   if constexpr (RSV) {
+    if constexpr (RADIX >= 256)
+      if (tid < RADIX) {
+        const uint32_t hi = __shfl_up((uint32_t)(rsv64 >> 32), 1);
+        rsv = (tid & 1) ? hi : (uint32_t)rsv64;
+      }
     if (tid < RADIX) {
       // the run of digit tid lands at [slice start + rsv, + cnt_d) of its
       // slice; the next depth's tiles are numbered per slice (capacity)
@@ -2146,7 +2170,7 @@ __global__ __launch_bounds__(256) void k_rsv_sample(const uint32_t* __restrict__
       rslice[e] = start;
       rslice[NS + e] = cap[xr];
       rslice[2 * NS + e] = row0;
-      rcur[(size_t)e * kRsvCurStride] = 0u;
+      rcur[rsv_cur_index(e, RADIX)] = 0u;
       start += cap[xr];
       row0 += ntl[xr];
     }
@@ -2189,7 +2213,7 @@ __global__ __launch_bounds__(256) void k_rsv_tiles(const uint32_t* __restrict__ 
 #pragma unroll
   for (int xr = 0; xr < kRsvRanges; ++xr) {
     const uint32_t e = tid * kRsvRanges + xr;
-    keys[xr] = (tid < (uint32_t)RADIX && !over) ? rcur[(size_t)e * kRsvCurStride] : 0u;
+    keys[xr] = (tid < (uint32_t)RADIX && !over) ? rcur[rsv_cur_index(e, RADIX)] : 0u;
     nl += (keys[xr] + TILE - 1) / TILE;
     dk += keys[xr];
   }
@@ -3436,7 +3460,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   const int rmode = kRsvOk && !pc && DEPTHS > 1 && (const void*)in != (const void*)out ? rsv_mode() : 0;
   const bool rsv = rmode != 0;
   const uint32_t tb1 = (uint32_t)((rsv_capacity_bound(n, BITS) + TILE - 1) / TILE) + RADIX * kRsvRanges;
-  if (rsv) LS_TRY(ws.ensure_rsv(rsv_capacity_bound(n, BITS) + (size_t)RADIX * kRsvRanges * kRsvCurStride));
+  // the cursors after the slices, 256-byte aligned (8-bit: 64-bit adds)
+  const size_t rcur_off = (rsv_capacity_bound(n, BITS) + 63) & ~(size_t)63;
+  if (rsv) LS_TRY(ws.ensure_rsv(rcur_off + (size_t)RADIX * kRsvRanges * kRsvCurStride));
   // segments of depth k (each child has at most one partial tile)
   auto nseg_at = [&](int k) { return nseg0 << (BITS * k); };
   auto tbound = [&](int k) { return k == 0 ? T0 : (k == 1 && rsv) ? tb1 : T0 + nseg_at(k); };
@@ -3466,7 +3492,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   // + the tile count) | cursors | estimated digit sizes; ctr[14] = overflow
   uint32_t* rpart = h; h += kRsvRanges * kRsvBlocks * RADIX;
   uint32_t* rslice = h; h += 3 * RADIX * kRsvRanges + 16;
-  uint32_t* rcur = rsv ? ws.rsv + rsv_capacity_bound(n, BITS) : nullptr;  // kRsvCurStride apart
+  uint32_t* rcur = rsv ? ws.rsv + rcur_off : nullptr;  // kRsvCurStride apart
   if (!rsv) {  // (reserved depth 0: k_rsv_sample sets them)
     hipLaunchKernelGGL(k_hyb_init, dim3(1), dim3(64), 0, st, ctr, NB);  // one launch, not two memsets (4 fills)
     LS_TRY(hipGetLastError());

@@ -18,6 +18,6 @@ import json, sys
 d = json.load(open(sys.argv[1])); k = d["kernels"]
 print("%-40s %7.3f Gkeys/s %7.4f ms  counts %6.1f  pass %6.1f  bucket %6.1f  8-bit %6.4f ms" % (
     sys.argv[1].split("/")[-1], d["value"], d["ms_per_step"], k.get("tilecounts", {}).get("avg_us", 0.0),
-    k["tilepass"]["avg_us"], k.get("bucketsort", {}).get("avg_us", 0.0), d["variants"]["digit8"]["ms_per_step"]))
+    k["tilepass"]["avg_us"], k.get("bucketsort", {}).get("avg_us", 0.0), (d.get("variants") or {}).get("digit8", {}).get("ms_per_step", 0.0)))
 PY
 done
