@@ -10,12 +10,14 @@ c2 (default; the bench line): configs[1] = "256M uint32, 4-bit digits,
     of providedGpu).
     N>1 = configs[3] ("2^32 uint32 sharded 8xMI355X"): 2^29 keys per GPU
     (2^32 at N=8); rank r holds keys [r*2^29, (r+1)*2^29) of the same stream
-    (weak scaling); one step = one distributed sort (pylibsort.distrib,
-    schedule "auto": one table partition, range-split RCCL point-to-point
-    rounds overlapped with the per-round sorts -- "msd" at 4 and 8 GPUs,
-    "msdz" at 2, the same rounds sorted before sending and exchanged
-    gap-coded) ending with rank r holding keys [r*S, (r+1)*S) of the sorted
-    array.  `python bench.py --gpus N` with no launcher starts its N ranks
+    (weak scaling); one step = one distributed sort ending with rank r holding
+    keys [r*S, (r+1)*S) of the sorted array.  Default engine (--engine auto =
+    cabi): rank 0 drives every GPU through the C ABI (libsortDistribSortU32:
+    top-digit partition, K = 4 RCCL point-to-point rounds overlapped with the
+    round sorts), its first step verified before timing; --engine torch: one
+    process per GPU (pylibsort.distrib, schedule "auto": "msd" at 4 and 8
+    GPUs, "msdz" at 2 -- the same rounds sorted before sending and exchanged
+    gap-coded).  `python bench.py --gpus N` with no launcher starts its N ranks
     itself: torch.distributed.run as a CHILD process (no exec), rank 0's JSON
     line relayed, non-zero exit if any rank fails.
 c3: configs[2], 2^30 keys, 8-bit digits, one GPU.

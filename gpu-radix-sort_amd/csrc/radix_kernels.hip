@@ -1134,8 +1134,8 @@ struct HybridGeo {
   const uint32_t* ncstart;   // GEO & 2: next depth's child starts
   const uint32_t* nctile0;   // GEO & 2: next depth's first tile per child
   uint8_t* dout;             // 8-bit passes (any GEO): op_next of every written key at its output position, or null
-  // GEO & 4 (reserved placement, keys-only 4-bit depth 0 without a count
-  // pass; sort_hybrid "Reserved depth 0"): slice e = digit * 8 + range, range
+  // GEO & 4 (reserved placement, keys-only depth 0 without a count pass;
+  // sort_hybrid "Reserved depth 0"): slice e = digit * 8 + range, range
   // = blockIdx.x & 7 (the tile range xcd_tile_of_block gives those blocks)
   uint32_t* rcur;            // [RADIX * 8] keys reserved in each slice so far
   const uint32_t* rslice;    // [3][RADIX * 8] slice start | capacity | first next-depth tile
@@ -2041,7 +2041,7 @@ __global__ __launch_bounds__(256) void k_hyb_expand(const uint32_t* __restrict__
   tiles[t] = make_uint4(ncstart[lo] + k * TILE, min((uint32_t)TILE, nsize[lo] - k * TILE), lo, t);
 }
 
-// ---- Reserved depth 0 (sort_hybrid, keys-only 4-bit sorts without values) ----
+// ---- Reserved depth 0 (sort_hybrid, keys-only 32-bit sorts: 4- and 8-bit digits) ----
 // The depth-0 pass places a tile's digit runs by reserving space in slices
 // (k_tile_pass GEO & 4) instead of reading offsets from a count pass + column
 // scan: one HBM read of the keys less.  Slice e = digit d * 8 + range x, range
@@ -3044,7 +3044,7 @@ hipError_t tiles_colscan(Workspace& ws, uint32_t* C, uint32_t tiles, hipStream_t
 // stores beside 4-byte keys made the u32 pass 1716 -> 2557 us at 2^30 (c3
 // 10.03 -> 12.29 ms).  LIBSORT_DSTREAM=0 turns it off (A/B).
 // Reserved depth 0 (k_rsv_sample + k_tile_pass GEO & 4): the default for
-// keys-only 4-bit hybrid sorts; LIBSORT_HYB_RESERVE=0 keeps the count pass,
+// keys-only 32-bit hybrid sorts; LIBSORT_HYB_RESERVE=0 keeps the count pass,
 // =short halves every sampled capacity (tests: the overflow fallback).  Read
 // per call (the tests switch it in process).
 inline int rsv_mode() {
@@ -3453,7 +3453,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   const uint32_t cap1 = (uint32_t)BBc * (((uint32_t)kItems1[cls] * 256u + BBc - 1) / BBc);
   const uint32_t cap = (uint32_t)BBc * (((uint32_t)(kItems1[cls] + extra) * 256u + BBc - 1) / BBc);
   const uint32_t T0 = pc ? pc->tiles : (uint32_t)((n + TILE - 1) / TILE);
-  // reserved depth 0 (keys only, 4-bit, in != out: the fallback re-reads in):
+  // reserved depth 0 (32-bit keys only, in != out: the fallback re-reads in):
   // no count pass; depth 0 writes slices of ws.rsv (tile rows of depth 1
   // numbered by slice capacity, at most tb1)
   constexpr bool kRsvOk = sizeof(K) == 4 && std::is_same<V, NoValue>::value;

@@ -86,9 +86,10 @@ LIBSORT_API bool gpuPartialSort(uint32_t* h_in, uint32_t* boundaries, size_t h_i
  * MSD hybrid (libsortSetHybrid) waits on the host for two small read-backs
  * while its first and last digit passes run.  Under stream capture (HIP
  * graphs) the hybrid is never taken, so a captured call never waits.  With
- * 4-bit digits and d_in != d_out the hybrid's first pass places its runs in
- * sampled slices of a cached per-device buffer of ~1.14 n keys instead of
- * reading the keys twice (LIBSORT_HYB_RESERVE=0: the count pass instead). */
+ * d_in != d_out the hybrid's first pass places its runs in sampled slices of
+ * a cached per-device buffer of ~1.14 n (4-bit digits) / ~1.28 n (8-bit) keys
+ * instead of reading the keys twice (LIBSORT_HYB_RESERVE=0: the count pass
+ * instead). */
 LIBSORT_API bool libsortSortKeysU32(const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp,
                                     size_t n, uint32_t offset, uint32_t width,
                                     uint32_t* d_boundaries, void* stream);
