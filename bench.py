@@ -242,6 +242,8 @@ def main():
             try:
                 first = step()
                 torch.cuda.synchronize()
+                if os.environ.get("BENCH_CABI_FAULT") == "1":  # rehearsal of the fallback (tests only)
+                    (first[0] if pairs else first)[0][:1] = 0 if pairs else -1
                 if not args.no_verify and not verify_cabi(torch, shards, first, vshards if pairs else None):
                     failed, engine_note = 1, "C-ABI engine's first step failed verification; torch engine measured"
                 del first

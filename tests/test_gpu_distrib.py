@@ -170,6 +170,34 @@ def test_bench_cabi_engine_rehearsal(world, pairs):
     line = json.loads(lines[0])
     assert line["n_gpus"] == world and line["verified"] is True
     assert "C-ABI engine" in line["config"]["workload"]
+    assert "engine_note" not in line and line["engine"].startswith("cabi")
+
+
+def test_bench_cabi_bad_first_step_falls_back_to_torch():
+    """The C engine's first step is verified before it is timed (its
+    distinct-device paths only run on a multi-GPU node): a wrong result
+    (BENCH_CABI_FAULT=1 corrupts one key of it) hands the measurement to the
+    torch engine on every rank, and the line says so."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import json
+    import os
+    import pathlib
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["BENCH_REHEARSAL"] = "1"
+    env["BENCH_CABI_FAULT"] = "1"
+    cmd = [sys.executable, str(root / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--keys-log2", "20", "--engine", "cabi", "--no-variants"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(root))
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["verified"] is True
+    assert "failed verification" in line["engine_note"] and not line["engine"].startswith("cabi")
 
 
 def test_bench_single_gpu_line_contract():
