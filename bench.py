@@ -5,25 +5,31 @@
 
 c2 (default; the bench line): configs[1] = "256M uint32, 4-bit digits,
     gpuFullSort on 1 MI355X": 2^28 keys of the reference populateInput stream
-    (generated on the GPU by skip-ahead), one step = one full 32-bit LSD sort
+    (generated on the GPU by skip-ahead), one step = one full 32-bit sort
     through the libsort C ABI (libsortSortKeysU32 = the device-resident form
-    of providedGpu).
+    of providedGpu): the MSD hybrid, i.e. four 4-bit digit passes from the top
+    digit down (the first with reserved runs, no count pass) and the on-chip
+    sort of every 16-bit bucket; `variants.lsd` times
+    the plain 8-pass LSD sort.
     N>1 = configs[3] ("2^32 uint32 sharded 8xMI355X"): 2^29 keys per GPU
     (2^32 at N=8); rank r holds keys [r*2^29, (r+1)*2^29) of the same stream
     (weak scaling); one step = one distributed sort ending with rank r holding
-    keys [r*S, (r+1)*S) of the sorted array.  Default engine (--engine auto =
-    cabi): rank 0 drives every GPU through the C ABI (libsortDistribSortU32:
-    top-digit partition, K = 4 RCCL point-to-point rounds overlapped with the
-    round sorts), its first step verified before timing; --engine torch: one
-    process per GPU (pylibsort.distrib, schedule "auto": "msd" at 4 and 8
-    GPUs, "msdz" at 2 -- the same rounds sorted before sending and exchanged
-    gap-coded).  `python bench.py --gpus N` with no launcher starts its N ranks
+    keys [r*S, (r+1)*S) of the sorted array.  Engine (--engine auto): at 4
+    and 8 GPUs the C engine -- rank 0 drives every GPU through the C ABI
+    (libsortDistribSortU32: top-digit partition, K = 4 RCCL point-to-point
+    rounds overlapped with the round sorts), its first step verified before
+    timing; at 2 GPUs the torch engine -- one process per GPU
+    (pylibsort.distrib, schedule "msdz": the same rounds sorted before
+    sending and exchanged gap-coded, since one xGMI link carries half of
+    every shard).  `python bench.py --gpus N` with no launcher starts its N ranks
     itself: torch.distributed.run as a CHILD process (no exec), rank 0's JSON
     line relayed, non-zero exit if any rank fails.
 c3: configs[2], 2^30 keys, 8-bit digits, one GPU.
 c5: configs[4], stable (u64 key, u32 payload) sort, 2^28 pairs per GPU (2^31
     on 8 GPUs); key = (draw 2i << 32) | draw 2i+1 of the stream, payload = the
-    global index; N>1 runs pylibsort.distrib.distrib_sort_pairs.
+    global index; N>1 runs the C pair engine (libsortDistribSortPairsU64U32)
+    at 4 and 8 GPUs and pylibsort.distrib.distrib_sort_pairs at 2 (the same
+    engine choice as c2).
 
 Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 """
@@ -40,11 +46,15 @@ for p in (str(ROOT), str(ROOT / "gpu-radix-sort_amd")):
         sys.path.insert(0, p)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-# N>1 engine when --engine auto (the faster of the two
-# on the one-GPU schedule measurement at 2^29 keys per rank --
-# profiles/r03h_*: C engine 7.48 ms vs torch engine 7.85 ms in the 8-GPU
-# per-rank shape, 6.52 vs 6.92 ms on uniform keys)
-DEFAULT_ENGINE = "cabi"
+# N>1 engine when --engine auto.  N >= 4: the C engine,
+# the faster of the two on the one-GPU schedule measurement at 2^29 keys per
+# rank (profiles/r03w_msd_schedule_2pow29_shape8.txt: 6.56 vs 6.71 ms in the
+# 8-GPU per-rank shape; profiles/r04*_msd_schedule_* for this round).  N = 2:
+# the torch engine, whose "msdz" schedule sends the rounds gap-coded (~9.5 of
+# 32 bits per key) -- two GPUs share ONE xGMI link, so the link, not the GPU
+# work, bounds that step, and only the torch engine has the coded exchange.
+def default_engine(world):
+    return "torch" if world == 2 else "cabi"
 PASS_KERNELS = "tilepass,onesweep,downsweep"  # the roofline kernel candidates (timed-region events)
 
 
@@ -62,7 +72,8 @@ def parse():
     ap.add_argument("--engine", default="auto", choices=["auto", "torch", "cabi"],
                     help="N>1: torch = one process per GPU (pylibsort.distrib over torch.distributed); cabi = rank "
                          "0 drives every GPU through the C ABI (libsortDistribSortU32 / ...PairsU64U32, the "
-                         "single-process RCCL engine C and Go callers bind); auto = DEFAULT_ENGINE")
+                         "single-process RCCL engine C and Go callers bind); auto = torch at 2 GPUs (the delta-coded "
+                         "msdz exchange), cabi otherwise")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=28,
                     help="keys of the providedCpu baseline sample (BASELINE.md section 3: 2^28)")
@@ -186,7 +197,7 @@ def main():
         tmp = torch.empty_like(keys)
     torch.cuda.synchronize()
     ops = distrib.HipOps() if world > 1 else None
-    engine = DEFAULT_ENGINE if args.engine == "auto" else args.engine
+    engine = default_engine(world) if args.engine == "auto" else args.engine
     cabi = world > 1 and engine == "cabi"
     shards = vshards = None
     if cabi:

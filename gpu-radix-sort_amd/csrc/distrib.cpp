@@ -168,6 +168,7 @@ struct RankState {
   int dev = -1;
   DevState* d = nullptr;
   DBuf bounds, part, pv, recv, rv, outb, ov, alt;  // pv / rv / ov: pair payloads
+  DBuf mm;                                          // smallest and largest key (range partition)
   DBuf hin, hout;  // staging of the host-pointer entry point
   hipEvent_t ev_part = nullptr, ev_bounds = nullptr, ev_done = nullptr;
   hipEvent_t ev_x[kMaxRounds] = {};
@@ -179,13 +180,14 @@ struct Ctx {
   std::vector<RankState> ranks;
   std::vector<ncclComm_t> comms;               // RCCL communicator of each rank (distinct devices only)
   uint32_t* h_bounds = nullptr;                // pinned: R x 256 bucket starts
+  uint64_t* h_mm = nullptr;                    // pinned: R x (min, max) keys
   bool distinct = false;
 
   ~Ctx() {
     for (ncclComm_t c : comms)
       if (c && g_rccl.loaded) (void)g_rccl.commDestroy(c);
     for (auto& r : ranks) {
-      for (DBuf* b : {&r.bounds, &r.part, &r.pv, &r.recv, &r.rv, &r.outb, &r.ov, &r.alt, &r.hin, &r.hout})
+      for (DBuf* b : {&r.bounds, &r.part, &r.pv, &r.recv, &r.rv, &r.outb, &r.ov, &r.alt, &r.mm, &r.hin, &r.hout})
         b->release();
       (void)hipSetDevice(r.dev);
       for (hipEvent_t e : {r.ev_part, r.ev_bounds, r.ev_done})
@@ -204,6 +206,7 @@ struct Ctx {
       if (u->ev_comp) (void)hipEventDestroy(u->ev_comp);
     }
     if (h_bounds) (void)hipHostFree(h_bounds);
+    if (h_mm) (void)hipHostFree(h_mm);
   }
 
   bool init(const std::vector<int>& d) {
@@ -246,9 +249,10 @@ struct Ctx {
         if (!ok_hip(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate")) return false;
       for (hipEvent_t& e : s.ev_x)
         if (!ok_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate")) return false;
-      if (!s.bounds.ensure(s.dev, dplan::kTopDigits * 4)) return false;
+      if (!s.bounds.ensure(s.dev, dplan::kTopDigits * 4) || !s.mm.ensure(s.dev, 2 * sizeof(uint64_t))) return false;
     }
-    return ok_hip(hipHostMalloc(&h_bounds, (size_t)R * dplan::kTopDigits * sizeof(uint32_t), 0), "hipHostMalloc");
+    return ok_hip(hipHostMalloc(&h_bounds, (size_t)R * dplan::kTopDigits * sizeof(uint32_t), 0), "hipHostMalloc") &&
+           ok_hip(hipHostMalloc(&h_mm, (size_t)R * 2 * sizeof(uint64_t), 0), "hipHostMalloc");
   }
 
   bool ensure_comms() {
@@ -372,6 +376,7 @@ bool run_lsd(Ctx& c, const std::vector<const uint32_t*>& in, const std::vector<u
       RankState& s = c.ranks[r];
       if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice")) return false;
       if (n_cur[r]) {
+        ScopedTimer tm("lsdround", s.d->st, n_cur[r]);  // (the tests check which schedule ran)
         if (!ok_hip(sort_u32(*s.d->ws, cur[r], s.part.u32(), s.d->tmp.u32(), n_cur[r], step * W, step * W + W, bits,
                              s.bounds.u32(), s.d->st),
                     "local partial sort"))
@@ -464,14 +469,26 @@ struct Hold {
   }
 };
 
-// Stable partition of every rank's keys (and payloads) by their top 8 bits
+// The partition digit of the rounds: the top 8 key bits (table partition with
+// the identity table), or -- when those leave the keys in too few digits
+// (a narrow key range: IDs, timestamps, keys below 2^26 at 8 ranks; ADVICE
+// r03) -- the 8-bit digit (key - bias) >> shift over the populated range
+// [bias = smallest key, largest key] (range partition).  Either way the
+// digits are monotone in the key, so the rounds stay disjoint key ranges.
+struct PartDigit {
+  bool range = false;
+  uint64_t bias = 0;
+  int shift = dplan::kTopShift;  // keys of one digit share the bits above `shift` of key - bias
+};
+
+// Stable partition of every rank's keys (and payloads) by the digit `pd`
 // into part (pv): the count call (per-tile counts + column scan) and the
 // 256 bucket starts' copy to the host are queued first, then the scatter, so
 // the host reads the counts while the data moves.  C[r][g] = rank r's keys
 // in digit g.
 template <typename K>
 bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<const uint32_t*>* vin,
-                   const std::vector<uint64_t>& n, std::vector<std::vector<uint64_t>>& C) {
+                   const std::vector<uint64_t>& n, std::vector<std::vector<uint64_t>>& C, const PartDigit& pd) {
   const int R = (int)c.ranks.size();
   constexpr int NB = dplan::kTopDigits;
   for (int r = 0; r < R; ++r) {
@@ -484,11 +501,15 @@ bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<co
     if (n[r]) {
       hipError_t e1, e2;
       if constexpr (sizeof(K) == 4) {
-        e1 = partition_lut_u32(ws, in[r], nullptr, n[r], lut, dplan::kTopShift, NB, s.bounds.u32(), s.d->st,
-                               kPartCount);
+        e1 = pd.range ? partition_range_u32(ws, in[r], nullptr, n[r], (uint32_t)pd.bias, pd.shift, s.bounds.u32(),
+                                            s.d->st, kPartCount)
+                      : partition_lut_u32(ws, in[r], nullptr, n[r], lut, dplan::kTopShift, NB, s.bounds.u32(),
+                                          s.d->st, kPartCount);
       } else {
-        e1 = partition_lut_pairs_u64_u32(ws, in[r], (*vin)[r], nullptr, nullptr, n[r], lut, dplan::kTopShift, NB,
-                                         s.bounds.u32(), s.d->st, kPartCount);
+        e1 = pd.range ? partition_range_pairs_u64_u32(ws, in[r], (*vin)[r], nullptr, nullptr, n[r], pd.bias, pd.shift,
+                                                      s.bounds.u32(), s.d->st, kPartCount)
+                      : partition_lut_pairs_u64_u32(ws, in[r], (*vin)[r], nullptr, nullptr, n[r], lut,
+                                                    dplan::kTopShift, NB, s.bounds.u32(), s.d->st, kPartCount);
       }
       if (!ok_hip(e1, "partition counts") ||
           !ok_hip(hipMemcpyAsync(c.h_bounds + (size_t)r * NB, s.bounds.p, NB * 4, hipMemcpyDeviceToHost, s.d->st),
@@ -496,11 +517,17 @@ bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<co
           !ok_hip(hipEventRecord(s.ev_bounds, s.d->st), "hipEventRecord"))
         return false;
       if constexpr (sizeof(K) == 4) {
-        e2 = partition_lut_u32(ws, in[r], s.part.u32(), n[r], lut, dplan::kTopShift, NB, nullptr, s.d->st,
-                               kPartScatter);
+        e2 = pd.range ? partition_range_u32(ws, in[r], s.part.u32(), n[r], (uint32_t)pd.bias, pd.shift, nullptr,
+                                            s.d->st, kPartScatter)
+                      : partition_lut_u32(ws, in[r], s.part.u32(), n[r], lut, dplan::kTopShift, NB, nullptr, s.d->st,
+                                          kPartScatter);
       } else {
-        e2 = partition_lut_pairs_u64_u32(ws, in[r], (*vin)[r], static_cast<uint64_t*>(s.part.p), s.pv.u32(), n[r],
-                                         lut, dplan::kTopShift, NB, nullptr, s.d->st, kPartScatter);
+        e2 = pd.range ? partition_range_pairs_u64_u32(ws, in[r], (*vin)[r], static_cast<uint64_t*>(s.part.p),
+                                                      s.pv.u32(), n[r], pd.bias, pd.shift, nullptr, s.d->st,
+                                                      kPartScatter)
+                      : partition_lut_pairs_u64_u32(ws, in[r], (*vin)[r], static_cast<uint64_t*>(s.part.p),
+                                                    s.pv.u32(), n[r], lut, dplan::kTopShift, NB, nullptr, s.d->st,
+                                                    kPartScatter);
       }
       if (!ok_hip(e2, "partition scatter")) return false;
     }
@@ -516,6 +543,42 @@ bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<co
   return true;
 }
 
+// The range digit over the keys of every rank: bias = the smallest key,
+// shift = (bits of largest - smallest) - 8 (at least 0).  False on a HIP
+// error; *useful = false when it would not split finer than the top digit
+// (or all keys are equal).
+template <typename K>
+bool range_digit(Ctx& c, const std::vector<const K*>& in, const std::vector<uint64_t>& n, PartDigit& pd,
+                 bool* useful) {
+  const int R = (int)c.ranks.size();
+  for (int r = 0; r < R; ++r) {
+    RankState& s = c.ranks[r];
+    if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice")) return false;
+    hipError_t e;
+    if constexpr (sizeof(K) == 4)
+      e = minmax_u32(*s.d->ws, in[r], n[r], s.mm.u32(), s.d->st);
+    else
+      e = minmax_u64(*s.d->ws, in[r], n[r], static_cast<uint64_t*>(s.mm.p), s.d->st);
+    if (!ok_hip(e, "min/max") ||
+        !ok_hip(hipMemcpyAsync(c.h_mm + 2 * (size_t)r, s.mm.p, 2 * sizeof(K), hipMemcpyDeviceToHost, s.d->st),
+                "D2H min/max") ||
+        !ok_hip(hipEventRecord(s.ev_bounds, s.d->st), "hipEventRecord"))
+      return false;
+  }
+  uint64_t lo = ~0ull, hi = 0;
+  for (int r = 0; r < R; ++r) {
+    if (!ok_hip(hipEventSynchronize(c.ranks[r].ev_bounds), "hipEventSynchronize")) return false;
+    if (!n[r]) continue;
+    K mm[2];
+    memcpy(mm, c.h_mm + 2 * (size_t)r, sizeof(mm));
+    lo = std::min<uint64_t>(lo, mm[0]);
+    hi = std::max<uint64_t>(hi, mm[1]);
+  }
+  pd.range = true;
+  *useful = dplan::range_digit(lo, hi, 8 * (int)sizeof(K), &pd.bias, &pd.shift);
+  return true;
+}
+
 // The rounds after the partition: every round's exchange issued up front on
 // the communication streams, each round sorted into its slice of the rank's
 // output as soon as it has arrived (keys: straight from the (source, digit)
@@ -523,7 +586,8 @@ bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<co
 // then the equal re-cut into out (vout).
 template <typename K>
 bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& out,
-                      const std::vector<uint32_t*>* vout, bool use_rccl, bool self_rccl, int bits) {
+                      const std::vector<uint32_t*>* vout, bool use_rccl, bool self_rccl, int bits,
+                      const PartDigit& pd) {
   const int R = (int)c.ranks.size(), K_ = p.K;
   const bool pairs = vout != nullptr;
   std::map<DevState*, uint64_t> round_max;
@@ -567,8 +631,8 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
       if constexpr (sizeof(K) == 4) {
         e = sort_pieces_u32(*d.ws, s.recv.u32() + a, kdst, d.tmp.u32(), z - a, p.p_off[q].data(), p.p_len[q].data(),
                             p.p_seg[q].data(), p.p_off[q].size(),
-                            (uint32_t)(p.hi[(size_t)i * R + r] - p.lo[(size_t)i * R + r]), dplan::kTopShift, bits,
-                            d.st);
+                            (uint32_t)(p.hi[(size_t)i * R + r] - p.lo[(size_t)i * R + r]), pd.shift, bits, d.st,
+                            (uint32_t)pd.bias);
       } else {
         e = sort_pairs_u64_u32(*d.ws, static_cast<uint64_t*>(s.recv.p) + a, s.rv.u32() + a, kdst, vdst,
                                static_cast<uint64_t*>(d.tmp.p), d.tmpv.u32(), z - a, 0, 64, bits, d.st);
@@ -708,14 +772,26 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
   if (flags & kDistribLsd) return hold.finish(run_lsd(c, in, n, out, S, bits, !copy, self_rccl));
   const int K = std::max(1, std::min(kMaxRounds, 256 / R));
   std::vector<std::vector<uint64_t>> C;
-  if (!partition_top<uint32_t>(c, in, nullptr, n, C)) return hold.finish(false);
+  PartDigit pd;
+  if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd)) return hold.finish(false);
   std::vector<uint8_t> lut(dplan::kTopDigits);
   std::vector<int64_t> est(R);
   dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
-  // one digit range would overload a rank: the LSD rounds from the untouched input
-  if (dplan::msd_too_skewed(est.data(), R, N)) return hold.finish(run_lsd(c, in, n, out, S, bits, !copy, self_rccl));
+  if (dplan::msd_too_skewed(est.data(), R, N)) {
+    // the top digit leaves the keys in too few digits: the 8-bit digit over
+    // the populated key range, if that is finer; else (or still skewed) the
+    // LSD rounds from the untouched input
+    bool useful = false;
+    if (!range_digit<uint32_t>(c, in, n, pd, &useful)) return hold.finish(false);
+    if (useful) {
+      if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd)) return hold.finish(false);
+      dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
+    }
+    if (!useful || dplan::msd_too_skewed(est.data(), R, N))
+      return hold.finish(run_lsd(c, in, n, out, S, bits, !copy, self_rccl));
+  }
   return hold.finish(run_digit_rounds<uint32_t>(c, dplan::digit_plan(C, lut.data(), K), out, nullptr, !copy, self_rccl,
-                                                bits));
+                                                bits, pd));
 }
 
 bool sort_device_pairs(Ctx& c, const uint64_t* const* d_kin, const uint32_t* const* d_vin, const size_t* n_in,
@@ -740,14 +816,25 @@ bool sort_device_pairs(Ctx& c, const uint64_t* const* d_kin, const uint32_t* con
   std::vector<uint32_t*> vout(d_vout, d_vout + R);
   const int K = std::max(1, std::min(kMaxRounds, 256 / R));
   std::vector<std::vector<uint64_t>> C;
-  if (!partition_top<uint64_t>(c, kin, &vin, n, C)) return hold.finish(false);
+  PartDigit pd;
+  if (!partition_top<uint64_t>(c, kin, &vin, n, C, pd)) return hold.finish(false);
   std::vector<uint8_t> lut(dplan::kTopDigits);
   std::vector<int64_t> est(R);
   dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
-  // no skew fallback (as pylibsort.distrib): a heavy digit range concentrates
-  // work on one rank, the result stays exact
+  if (dplan::msd_too_skewed(est.data(), R, N)) {
+    // keys below 2^56, or sharing their top byte (IDs, timestamps): the 8-bit
+    // digit over the populated key range.  Still skewed (few
+    // distinct keys): no LSD fallback for pairs -- a heavy digit range
+    // concentrates work on one rank, the result stays exact.
+    bool useful = false;
+    if (!range_digit<uint64_t>(c, kin, n, pd, &useful)) return hold.finish(false);
+    if (useful) {
+      if (!partition_top<uint64_t>(c, kin, &vin, n, C, pd)) return hold.finish(false);
+      dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
+    }
+  }
   return hold.finish(run_digit_rounds<uint64_t>(c, dplan::digit_plan(C, lut.data(), K), kout, &vout, !copy,
-                                                self_rccl, bits));
+                                                self_rccl, bits, pd));
 }
 
 }  // namespace

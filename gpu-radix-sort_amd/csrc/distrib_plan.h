@@ -133,6 +133,20 @@ inline void plan_digit_rounds(const std::vector<std::vector<uint64_t>>& C, int K
   plan_rounds(H.data(), R, kTopDigits, K, growth, lut, est, kTopDigits);
 }
 
+// The range digit of the rounds when the top digit is too skewed: the 8-bit
+// digit (key - lo) >> shift over the populated keys [lo, hi] of every rank,
+// shift = bits(hi - lo) - 8 (at least 0), so every key's digit is < 256.
+// Returns whether it splits finer than the top digit of a `key_bits`-bit key
+// (false when every key is equal).
+inline bool range_digit(uint64_t lo, uint64_t hi, int key_bits, uint64_t* bias, int* shift) {
+  const uint64_t span = hi >= lo ? hi - lo : 0;
+  int L = 0;
+  while (L < 64 && (span >> L)) ++L;
+  *bias = lo;
+  *shift = std::max(0, L - kTopBits);
+  return span > 0 && *shift < key_bits - kTopBits;
+}
+
 // Digit range [a, b) of group `code` (a == b: empty).  The table is monotone
 // in rank * K + round over the digits, so each group's digits are contiguous.
 inline void digit_range(const uint8_t* lut, int code, int* a, int* b) {

@@ -98,16 +98,17 @@ struct Workspace {
     const void* in;
     const void* vin;
     size_t n;
-    const uint8_t* lut;
+    const uint8_t* lut;  // null: the range digit (key - bias) >> shift
     int shift, nb;
+    uint64_t bias;
     hipStream_t st;
     bool valid;
     bool operator==(const PartToken& o) const {
       return valid && o.valid && in == o.in && vin == o.vin && n == o.n && lut == o.lut && shift == o.shift &&
-             nb == o.nb && st == o.st;
+             nb == o.nb && bias == o.bias && st == o.st;
     }
   };
-  PartToken part_pending{nullptr, nullptr, 0, nullptr, 0, 0, nullptr, false};
+  PartToken part_pending{nullptr, nullptr, 0, nullptr, 0, 0, 0, nullptr, false};
   hipError_t ensure_tiles(size_t count_words, size_t chunk_words);
 
   // MSD hybrid (sort_hybrid_u32): tile tables, per-segment run bases and
@@ -163,14 +164,15 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
 // Sort of pre-partitioned keys (a multi-GPU round's receive buffer, whose
 // pieces arrive partitioned by the senders): piece p = in[off[p], off[p] +
 // len[p]) of segment seg[p] (host arrays; np pieces in non-decreasing segment
-// order, seg < nseg); the keys of segment s share their bits [bits, 32) and
-// those increase with s.  out (distinct from in and tmp) receives the n =
-// sum(len) keys sorted; tmp: scratch of n keys.  The MSD hybrid starts from
-// the pieces' own tiles (no gather, no pass over the top bits); small or
-// skewed inputs are gathered and LSD-sorted.
+// order, seg < nseg); the keys of segment s share the bits [bits, 32) of key -
+// bias and those increase with s.  out (distinct from in and tmp) receives
+// the n = sum(len) keys sorted; tmp: scratch of n keys.  The MSD hybrid
+// starts from the pieces' own tiles (no gather, no pass over the top bits);
+// small or skewed inputs are gathered and LSD-sorted; bits == 0 (every
+// segment one value): the gather alone.
 hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n,
                            const uint64_t* off, const uint64_t* len, const uint32_t* seg, size_t np, uint32_t nseg,
-                           int bits, int digit_bits, hipStream_t stream);
+                           int bits, int digit_bits, hipStream_t stream, uint32_t bias = 0);
 hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t* vin,
                               uint32_t* kout, uint32_t* vout, uint32_t* ktmp, uint32_t* vtmp,
                               size_t n, int lo, int hi, int digit_bits, hipStream_t stream);
@@ -220,6 +222,17 @@ hipError_t partition_lut_u32(Workspace& ws, const uint32_t* in, uint32_t* out, s
 hipError_t partition_lut_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
                                        uint32_t* vout, size_t n, const uint8_t* d_lut, int lut_shift, int nbuckets,
                                        uint32_t* d_bounds, hipStream_t stream, int phase = kPartBoth);
+// The same partitions by the 8-bit range digit (key - bias) >> shift (256
+// buckets; keys in [bias, bias + 2^(shift + 8)), 0 <= shift <= 24 (u32) / 56
+// (u64)): the multi-GPU rounds over a key range narrower than the top digit.
+hipError_t partition_range_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, uint32_t bias, int shift,
+                               uint32_t* d_bounds, hipStream_t stream, int phase = kPartBoth);
+hipError_t partition_range_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
+                                         uint32_t* vout, size_t n, uint64_t bias, int shift, uint32_t* d_bounds,
+                                         hipStream_t stream, int phase = kPartBoth);
+// Smallest and largest key into d_mm[0], d_mm[1] (device; n == 0: ~0, 0).
+hipError_t minmax_u32(Workspace& ws, const uint32_t* keys, size_t n, uint32_t* d_mm, hipStream_t stream);
+hipError_t minmax_u64(Workspace& ws, const uint64_t* keys, size_t n, uint64_t* d_mm, hipStream_t stream);
 // Segment copy with the table already on the device: d_tab = [src_off[nseg] |
 // dst_off[nseg] | len[nseg]] (uint64), nseg <= 65535; maxlen = the longest
 // segment (sizes the grid), total = sum of len (timing only).

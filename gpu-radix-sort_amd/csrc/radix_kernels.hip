@@ -65,6 +65,19 @@ struct BiasedDigit {
   __device__ __forceinline__ uint32_t operator()(uint64_t k) const { return (uint32_t)((k - bias) >> shift) & mask; }
 };
 
+// Digit of (key - bias) for 64-bit keys with a 64-bit bias: the multi-GPU
+// pair partition over the populated key range (keys in [bias, bias +
+// 2^(shift + 8)), distrib.cpp range_partition).
+struct BiasedDigit64 {
+  uint64_t bias;
+  uint32_t shift;
+  uint32_t mask;
+  __device__ __forceinline__ uint32_t operator()(uint64_t k) const { return (uint32_t)((k - bias) >> shift) & mask; }
+  __device__ __forceinline__ uint32_t operator()(uint32_t k) const {
+    return (uint32_t)(((uint64_t)k - bias) >> shift) & mask;
+  }
+};
+
 template <typename Op> __host__ __device__ Op make_digit(uint32_t shift, uint32_t mask, uint32_t bias);
 template <> __host__ __device__ inline RadixDigit make_digit<RadixDigit>(uint32_t shift, uint32_t mask, uint32_t) {
   return RadixDigit{shift, mask};
@@ -1137,9 +1150,12 @@ struct HybridGeo {
   // GEO & 4 (reserved placement, keys-only depth 0 without a count pass;
   // sort_hybrid "Reserved depth 0"): slice e = digit * 8 + range, range
   // = blockIdx.x & 7 (the tile range xcd_tile_of_block gives those blocks)
-  uint32_t* rcur;            // [RADIX * 8] keys reserved in each slice so far
-  const uint32_t* rslice;    // [3][RADIX * 8] slice start | capacity | first next-depth tile
+  // (GEO & 5, a piece sort's depth 0 over its table: slice e = (segment *
+  // RADIX + digit) * 8 + range)
+  uint32_t* rcur;            // [NS] keys reserved in each slice so far
+  const uint32_t* rslice;    // [3][NS] slice start | capacity | first next-depth tile
   uint32_t* rflag;           // set to 1 when a tile's reservation passed its slice's capacity
+  uint32_t rns;              // NS: the slices (RADIX * 8 per segment)
 };
 
 // The pass kernel of the tile-offset path: the onesweep tile body with the
@@ -1207,7 +1223,7 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   // per digit on its range's slice cursor) instead of where a count pass and
   // a column scan put them; keys only (any order within a run).
   constexpr bool RSV = (GEO & 4) != 0;
-  static_assert(!RSV || (ANY_ORDER && !HAS_V && (GEO & 3) == 0), "reserved placement: keys-only depth 0");
+  static_assert(!RSV || (ANY_ORDER && !HAS_V && (GEO & 2) == 0), "reserved placement: keys-only depth 0");
   __shared__ uint32_t s_over;
 
   const int tid = threadIdx.x;
@@ -1246,10 +1262,10 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   if constexpr (RSV) {
     if (tid == 0) s_over = 0u;
     if (tid < RADIX) {
-      const uint32_t e = (uint32_t)tid * 8u + rx;
+      const uint32_t e = (seg * RADIX + (uint32_t)tid) * 8u + rx;
       ncs = geo.rslice[e];
-      rcap = geo.rslice[RADIX * 8 + e];
-      nct = geo.rslice[2 * RADIX * 8 + e];
+      rcap = geo.rslice[geo.rns + e];
+      nct = geo.rslice[2 * geo.rns + e];
     }
   } else if (tid < RADIX) {
     gofs = C[(size_t)row * RADIX + tid] + B[(size_t)(row / CH) * RADIX + tid] + D[(size_t)seg * RADIX + tid];
@@ -1318,10 +1334,11 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
         const uint32_t odd = __shfl_down(cnt_d, 1);
         if ((tid & 1) == 0 && (cnt_d | odd))
           rsv64 = __hip_atomic_fetch_add(
-              reinterpret_cast<unsigned long long*>(&geo.rcur[rsv_cur_index((uint32_t)tid * 8u + rx, RADIX)]),
+              reinterpret_cast<unsigned long long*>(
+                  &geo.rcur[rsv_cur_index((seg * RADIX + (uint32_t)tid) * 8u + rx, RADIX)]),
               (unsigned long long)cnt_d | ((unsigned long long)odd << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else if (cnt_d) {
-        rsv = __hip_atomic_fetch_add(&geo.rcur[rsv_cur_index((uint32_t)tid * 8u + rx, RADIX)], cnt_d,
+        rsv = __hip_atomic_fetch_add(&geo.rcur[rsv_cur_index((seg * RADIX + (uint32_t)tid) * 8u + rx, RADIX)], cnt_d,
                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
@@ -1536,10 +1553,11 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 // replaces them with the cell start, and a key's
 // position is start + the counts of the smaller residuals (three masked
 // popcounts) + its rank.  A 3-bit count that reaches 7 (8+ equal keys) would
-// carry: the bucket then places by u32 cell counters and counts, within its
-// cell, the keys that order before it (the loop below; cells average
-// len / 4096 keys).  lbits <= 12 takes the u32 counters directly (a cell is
-// one value: no loop).  Every key is placed in LDS (over the cell words, once
+// carry: the function then returns false without writing, and the caller
+// sorts the bucket by the LSD steps instead (k_bucket_sort; duplicate-heavy
+// inputs put whole buckets in one cell, so any per-cell search would grow
+// with the square of the cell).  lbits <= 12 places by u32 cell counters (a
+// cell is one value).  Every key is placed in LDS (over the cell words, once
 // the positions are in registers: 32 KB of LDS per block, not 32 KB + the
 // bucket), then the bucket is written out coalesced.  Measured, uniform 2^28 keys in 2^16 buckets (lbits 16):
 // the 4-step LSD kernel ~1.0 ms, this path ~0.5 ms.
@@ -1554,7 +1572,7 @@ constexpr int cnt_lds_words() {  // u64 words: the cell words, or the fallback's
   return (8 * kCntCells > 4 * (kCntCells + 1) + 4 * CAP ? 8 * kCntCells : 4 * (kCntCells + 1) + 4 * CAP + 7) / 8;
 }
 template <int BLOCK, int ITEMS>
-__device__ __forceinline__ void bucket_count_place(const uint32_t (&k)[ITEMS], uint64_t* s_cw, uint32_t* s_wsum,
+__device__ __forceinline__ bool bucket_count_place(const uint32_t (&k)[ITEMS], uint64_t* s_cw, uint32_t* s_wsum,
                                                    uint32_t* s_flag, uint32_t* out, uint32_t start, uint32_t len,
                                                    uint32_t lbits, uint32_t bias) {
   constexpr int PER = kCntCells / BLOCK;
@@ -1619,19 +1637,20 @@ __device__ __forceinline__ void bucket_count_place(const uint32_t (&k)[ITEMS], u
         const uint32_t p = wbase + j * kWave + lane;
         if (p < len) out[(size_t)start + p] = s_keys[p];
       }
-      return;
+      return true;
     }
-    __syncthreads();  // every wave has read the flag before the counters are reused
+    __syncthreads();  // every wave has read the flag before the caller reuses the words
+    return false;
   }
+  // lbits <= 12: one value per cell, u32 counters
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_cw);  // kCntCells + 1 u32 counters, then the keys
   uint32_t* s_keys = s_cnt + kCntCells + 1;
-  auto cj = [&](uint32_t c) -> uint32_t { return c >= (uint32_t)kCntCells ? (uint32_t)kCntCells : ci(c); };
 #pragma unroll
   for (int q = 0; q < PER; ++q) s_cnt[q * BLOCK + tid] = 0u;
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j)
-    if (wbase + j * kWave + lane < len) rk[j] = atomicAdd(&s_cnt[ci(val(k[j]) >> rb)], 1u);
+    if (wbase + j * kWave + lane < len) rk[j] = atomicAdd(&s_cnt[ci(val(k[j]))], 1u);
   __syncthreads();
   uint32_t c[PER], sum = 0;
 #pragma unroll
@@ -1646,31 +1665,17 @@ __device__ __forceinline__ void bucket_count_place(const uint32_t (&k)[ITEMS], u
     s_cnt[q * BLOCK + tid] = run;
     run += c[q];
   }
-  if (tid == 0) s_cnt[kCntCells] = len;
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j)
-    if (wbase + j * kWave + lane < len) s_keys[s_cnt[ci(val(k[j]) >> rb)] + rk[j]] = k[j];
+    if (wbase + j * kWave + lane < len) s_keys[s_cnt[ci(val(k[j]))] + rk[j]] = k[j];
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
     const uint32_t p = wbase + j * kWave + lane;
-    if (p < len) {
-      const uint32_t x = s_keys[p];
-      uint32_t fin = p;
-      if (rb > 0) {
-        const uint32_t vx = val(x), cell = vx >> rb;
-        const uint32_t a = s_cnt[cj(cell)], e = s_cnt[cj(cell + 1)];
-        uint32_t less = 0;
-        for (uint32_t q = a; q < e; ++q) {
-          const uint32_t vy = val(s_keys[q]);
-          less += (vy < vx) || (vy == vx && q < p) ? 1u : 0u;
-        }
-        fin = a + less;
-      }
-      out[(size_t)start + fin] = x;
-    }
+    if (p < len) out[(size_t)start + p] = s_keys[p];
   }
+  return true;
 }
 
 template <int BITS, int BLOCK, int ITEMS, typename Op = RadixDigit, typename K = uint32_t, typename V = NoValue,
@@ -1703,6 +1708,8 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
   static_assert(!CNT || (sizeof(K) == 4 && !HAS_V && FIX == 0), "counting path: 32-bit keys only");
   __shared__ uint64_t s_cw[CNT ? cnt_lds_words<CAP>() : 1];
   __shared__ uint32_t s_flag;
+  // the LSD steps' key buffer (CNT: over the counting words, its fallback)
+  K* const sk = CNT ? reinterpret_cast<K*>(s_cw) : s_keys;
   if (blockIdx.x >= min(*nb, nb_cap)) return;
   const uint32_t b = ilist ? ilist[blockIdx.x] : blockIdx.x;
   const uint32_t start = bstart[b], len = blen[b];
@@ -1778,7 +1785,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
           const uint32_t pos = s_off[w][op(k[j])] + rk[j];
-          s_keys[pos] = k[j];
+          sk[pos] = k[j];
           if constexpr (HAS_V) s_vals[pos] = v[j];
         }
       } else {
@@ -1802,24 +1809,24 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
           const uint32_t pos = s_whist[w][op(k[j])] + rk[j];
-          s_keys[pos] = k[j];
+          sk[pos] = k[j];
           if constexpr (HAS_V) s_vals[pos] = v[j];
         }
       }
       __syncthreads();
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
-        k[j] = s_keys[wbase + j * kWave + lane];
+        k[j] = sk[wbase + j * kWave + lane];
         if constexpr (HAS_V) v[j] = s_vals[wbase + j * kWave + lane];
       }
     }
   };
   load();
   if constexpr (CNT) {
-    bucket_count_place<BLOCK, ITEMS>(k, s_cw, s_wsum, &s_flag, out, start, len, lbits, bias);
-    return;
-  }
-  if constexpr (FIX > 0) {
+    // (a 3-bit count overflowed: the LSD steps below, over the same words)
+    if (bucket_count_place<BLOCK, ITEMS>(k, s_cw, s_wsum, &s_flag, out, start, len, lbits, bias)) return;
+    steps(0, lbits);
+  } else if constexpr (FIX > 0) {
     const uint32_t fs = lbits > (uint32_t)FIX ? lbits - FIX : 0u;  // keys equal above fs form the runs
     steps(fs, lbits);
     if (fs > 0) {
@@ -1845,9 +1852,9 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
 #pragma unroll
       for (int j = 0; j < ITEMS; ++j) {
         const uint32_t p = wbase + j * kWave + lane;
-        const uint32_t before = j > 0 ? readlane(h[j - 1], kWave - 1) : (wbase > 0 ? hi(s_keys[wbase - 1]) : 0u);
+        const uint32_t before = j > 0 ? readlane(h[j - 1], kWave - 1) : (wbase > 0 ? hi(sk[wbase - 1]) : 0u);
         const uint32_t after = j + 1 < ITEMS ? readlane(h[j + 1], 0)
-                                             : (wbase + WSPAN < len ? hi(s_keys[wbase + WSPAN]) : 0u);
+                                             : (wbase + WSPAN < len ? hi(sk[wbase + WSPAN]) : 0u);
         // (the shifts run with every lane active: a DPP source lane that is
         // off in EXEC reads as invalid)
         const uint32_t hp = dpp(h[j], before, WaveShr1{});
@@ -1869,25 +1876,25 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         for (uint32_t r0 = 0; r0 < nruns; r0 += kWave) {
           if (r0 + lane < nruns) {
-            // a stable insertion sort of s_keys[p, p + L) on key - bias
+            // a stable insertion sort of sk[p, p + L) on key - bias
             const uint32_t p = s_runs[w][r0 + lane];
-            const uint32_t h0 = hi(s_keys[p]);
+            const uint32_t h0 = hi(sk[p]);
             uint32_t L = 2;
-            while (L <= kMaxRun && p + L < len && hi(s_keys[p + L]) == h0) ++L;
+            while (L <= kMaxRun && p + L < len && hi(sk[p + L]) == h0) ++L;
             if (L > kMaxRun) {
               long_run = 1;
             } else {
               for (uint32_t a = 1; a < L; ++a) {
-                const K x = s_keys[p + a];
+                const K x = sk[p + a];
                 VS xv;
                 if constexpr (HAS_V) xv = s_vals[p + a];
                 uint32_t c = a;
-                while (c > 0 && (K)(s_keys[p + c - 1] - bias) > (K)(x - bias)) {
-                  s_keys[p + c] = s_keys[p + c - 1];
+                while (c > 0 && (K)(sk[p + c - 1] - bias) > (K)(x - bias)) {
+                  sk[p + c] = sk[p + c - 1];
                   if constexpr (HAS_V) s_vals[p + c] = s_vals[p + c - 1];
                   --c;
                 }
-                s_keys[p + c] = x;
+                sk[p + c] = x;
                 if constexpr (HAS_V) s_vals[p + c] = xv;
               }
             }
@@ -1901,7 +1908,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
       } else {
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
-          k[j] = s_keys[wbase + j * kWave + lane];
+          k[j] = sk[wbase + j * kWave + lane];
           if constexpr (HAS_V) v[j] = s_vals[wbase + j * kWave + lane];
         }
       }
@@ -2184,6 +2191,152 @@ __global__ __launch_bounds__(256) void k_rsv_sample(const uint32_t* __restrict__
   if (tid == 0) *ticket = 0u;
 }
 
+// Reserved depth 0 of a piece sort (sort_pieces_u32: a multi-GPU round's
+// receive buffer, pieces of nseg segments): slice e = (segment * RADIX +
+// digit) * 8 + range, NS = nseg * RADIX * 8 <= kRsvMaxSlices.  Range x = the
+// tiles [t0, t1) that blocks b % 8 == x take (xcd_tile_of over the depth-0
+// table), i.e. the keys of global rank [kb(t0), kb(t1)) in piece order; a
+// sample's rank is mapped to its piece by binary search over the pieces'
+// cumulative key counts pcum[np + 1], and it counts for (its piece's
+// segment, its digit).  131072 samples per range (several children per
+// range); otherwise as k_rsv_sample.  est[0] = the largest child's estimated
+// size (the host's skew check).
+constexpr uint32_t kRsvMaxSlices = 4096;
+constexpr int kRsvPcPer = 16;  // samples per thread (131072 per range)
+template <int RADIX, int TILE, typename Op>
+__global__ __launch_bounds__(256) void k_rsv_sample_pc(const uint32_t* __restrict__ keys, const uint4* __restrict__ pieces,
+                                                       const uint32_t* __restrict__ pcum, uint32_t np, uint32_t nseg,
+                                                       uint32_t T0, uint32_t n, Op op, uint32_t* part,
+                                                       uint32_t* __restrict__ rslice, uint32_t* __restrict__ rcur,
+                                                       uint32_t* __restrict__ est, uint32_t* __restrict__ Czero,
+                                                       uint32_t zero_words, uint32_t* ticket,
+                                                       uint32_t* __restrict__ ctr, uint32_t nb, bool short_caps) {
+  constexpr uint32_t S = kRsvBlocks * 256 * kRsvPcPer;
+  constexpr uint32_t kMaxChildren = kRsvMaxSlices / kRsvRanges;
+  __shared__ uint32_t s_h[kMaxChildren];
+  __shared__ uint32_t s_wsum[2][4];
+  __shared__ uint32_t s_flag, s_max;
+  const uint32_t tid = threadIdx.x, NC = nseg * RADIX, NS = NC * kRsvRanges;
+  const uint32_t x = blockIdx.x / kRsvBlocks, j = blockIdx.x % kRsvBlocks;
+  for (uint32_t i = (blockIdx.x * 256 + tid) * 4; i < zero_words; i += gridDim.x * 256 * 4)
+    *reinterpret_cast<uint4*>(&Czero[i]) = make_uint4(0u, 0u, 0u, 0u);
+  for (uint32_t c = tid; c < NC; c += 256) s_h[c] = 0u;
+  __syncthreads();
+  // keys before depth-0 tile t (the tiles of piece p are full but its last)
+  auto kb = [&](uint32_t t) -> uint64_t {
+    if (t >= T0) return n;
+    uint32_t lo = 0, hi = np;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pieces[mid].w <= t) lo = mid; else hi = mid;
+    }
+    return (uint64_t)pcum[lo] + (uint64_t)(t - pieces[lo].w) * TILE;
+  };
+  const uint32_t q8 = T0 >> 3, r8 = T0 & 7u;
+  auto range_keys = [&](uint32_t xr, uint64_t* k0, uint64_t* k1) {
+    const uint32_t t0 = xr * q8 + min(xr, r8), t1 = t0 + q8 + (xr < r8 ? 1u : 0u);
+    *k0 = kb(t0);
+    *k1 = kb(t1);
+  };
+  uint64_t k0, k1;
+  range_keys(x, &k0, &k1);
+  const uint64_t N = k1 - k0;
+  uint32_t kv[kRsvPcPer], sg[kRsvPcPer];
+  bool ok[kRsvPcPer];
+#pragma unroll
+  for (int q = 0; q < kRsvPcPer; ++q) {
+    const uint32_t i = (j * 256 + tid) * kRsvPcPer + q;
+    uint64_t rank;
+    if (N <= S) {
+      rank = k0 + i;
+      ok[q] = i < N;
+    } else {
+      uint32_t h = (i + 1u) * 0x9E3779B1u ^ (x + 1u) * 0x85EBCA77u;
+      h ^= h >> 15;
+      h *= 0x2C1B3C6Du;
+      h ^= h >> 12;
+      rank = k0 + ((uint64_t)i * N + (((uint64_t)h * N) >> 32)) / S;
+      ok[q] = true;
+    }
+    sg[q] = 0u;
+    kv[q] = 0u;
+    if (ok[q]) {
+      uint32_t lo = 0, hi = np;  // the piece holding global rank `rank`
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pcum[mid] <= rank) lo = mid; else hi = mid;
+      }
+      const uint4 pc = pieces[lo];
+      sg[q] = pc.z;
+      kv[q] = keys[pc.x + (uint32_t)(rank - pcum[lo])];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kRsvPcPer; ++q)
+    if (ok[q]) atomicAdd(&s_h[sg[q] * RADIX + op(kv[q])], 1u);
+  __syncthreads();
+  for (uint32_t c = tid; c < NC; c += 256) st_agent(&part[(size_t)blockIdx.x * NC + c], s_h[c]);
+  if (!last_arriver(ticket, gridDim.x, &s_flag)) return;
+  // thread tid: children [tid * CPT, ...), their 8 range slices each
+  // (contiguous slices e = c * 8 + range)
+  const uint32_t CPT = (NC + 255) / 256;
+  uint32_t scap = 0, stl = 0, mx = 0;
+  if (tid == 0) s_max = 0u;
+  for (uint32_t cc = 0; cc < CPT; ++cc) {
+    const uint32_t c = tid * CPT + cc;
+    if (c >= NC) break;
+    double est_c = 0.0;
+    for (uint32_t xr = 0; xr < (uint32_t)kRsvRanges; ++xr) {
+      uint32_t sc = 0;
+      for (int b = 0; b < kRsvBlocks; ++b) sc += ld_agent(&part[(size_t)(xr * kRsvBlocks + b) * NC + c]);
+      uint64_t a0, a1;
+      range_keys(xr, &a0, &a1);
+      const uint64_t Nx = a1 - a0;
+      uint32_t cap;
+      if (Nx <= S) {
+        cap = sc;
+        est_c += sc;
+      } else {
+        const double w = (double)Nx / S;
+        est_c += sc * w;
+        cap = (uint32_t)min((double)Nx, ceil(((double)sc + 5.0 * sqrt((double)sc) + 24.0) * w));
+      }
+      if (short_caps) cap /= 2;
+      const uint32_t nt = (cap + TILE - 1) / TILE;
+      // (capacity and tile count kept in rslice for the second sweep below)
+      rslice[NS + c * kRsvRanges + xr] = nt * TILE;
+      scap += nt * TILE;
+      stl += nt;
+    }
+    mx = max(mx, (uint32_t)min(4294967295.0, est_c + 0.5));
+  }
+  atomicMax(&s_max, mx);
+  uint32_t tot_c, tot_t;
+  uint32_t start = block_exclusive_scan<256>(scap, s_wsum[0], tot_c);
+  uint32_t row0 = block_exclusive_scan<256>(stl, s_wsum[1], tot_t);
+  __threadfence_block();
+  for (uint32_t cc = 0; cc < CPT; ++cc) {
+    const uint32_t c = tid * CPT + cc;
+    if (c >= NC) break;
+    for (uint32_t xr = 0; xr < (uint32_t)kRsvRanges; ++xr) {
+      const uint32_t e = c * kRsvRanges + xr;
+      const uint32_t cap = rslice[NS + e];
+      rslice[e] = start;
+      rslice[2 * NS + e] = row0;
+      rcur[rsv_cur_index(e, RADIX)] = 0u;
+      start += cap;
+      row0 += cap / TILE;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    rslice[3 * NS] = tot_t;
+    __hip_atomic_store(&est[0], s_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (tid < 16) ctr[tid] = tid == 9 ? nb : 0u;  // (k_hyb_init's words; k_hyb_pieces sets ctr[0] after)
+  if (tid == 0) *ticket = 0u;
+}
+
 // After the reserved depth-0 pass: the next depth's tile table, the
 // children's starts in the next depth's (compact) output, their tile (row)
 // ranges and the tile count.  FUSED (4-bit): the count rows are numbered by
@@ -2200,43 +2353,50 @@ __global__ __launch_bounds__(256) void k_rsv_tiles(const uint32_t* __restrict__ 
                                                    const uint32_t* __restrict__ rcur, const uint32_t* __restrict__ flag,
                                                    uint32_t bound, uint4* __restrict__ tiles,
                                                    uint32_t* __restrict__ cstart, uint32_t* __restrict__ ctile0,
-                                                   uint32_t* __restrict__ ntiles, uint32_t* __restrict__ Czero) {
-  constexpr int NS = RADIX * kRsvRanges;
-  static_assert(RADIX <= 256, "one digit per thread");
-  __shared__ uint32_t s_row0[NS + 1];  // first count row per slice (capacity), [NS] = rows
-  __shared__ uint32_t s_a0[NS + 1];    // first listed tile per slice, [NS] = tiles
-  __shared__ uint32_t s_keys[NS];
+                                                   uint32_t* __restrict__ ntiles, uint32_t* __restrict__ Czero,
+                                                   uint32_t nc) {
+  // nc children (segments x RADIX digits), NS = nc * 8 slices; thread tid
+  // holds slices [tid * SPT, (tid + 1) * SPT)
+  constexpr uint32_t kMaxSpt = kRsvMaxSlices / 256;
+  __shared__ uint32_t s_row0[kRsvMaxSlices + 1];  // first count row per slice (capacity), [NS] = rows
+  __shared__ uint32_t s_a0[kRsvMaxSlices + 1];    // first listed tile per slice, [NS] = tiles
+  __shared__ uint32_t s_keys[kRsvMaxSlices];
+  __shared__ uint32_t s_kb[kRsvMaxSlices];        // keys of the slices before
   __shared__ uint32_t s_wsum[2][4];
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x, NS = nc * kRsvRanges, SPT = (NS + 255) / 256;
   const bool over = *flag != 0u;
-  uint32_t keys[kRsvRanges], nl = 0, dk = 0;
+  uint32_t keys[kMaxSpt], nl = 0, dk = 0;
 #pragma unroll
-  for (int xr = 0; xr < kRsvRanges; ++xr) {
-    const uint32_t e = tid * kRsvRanges + xr;
-    keys[xr] = (tid < (uint32_t)RADIX && !over) ? rcur[rsv_cur_index(e, RADIX)] : 0u;
-    nl += (keys[xr] + TILE - 1) / TILE;
-    dk += keys[xr];
+  for (uint32_t q = 0; q < kMaxSpt; ++q) {
+    const uint32_t e = tid * SPT + q;
+    keys[q] = (q < SPT && e < NS && !over) ? rcur[rsv_cur_index(e, RADIX)] : 0u;
+    nl += (keys[q] + TILE - 1) / TILE;
+    dk += keys[q];
   }
   uint32_t listed, total_keys;
   uint32_t a0 = block_exclusive_scan<256>(nl, s_wsum[0], listed);
-  const uint32_t before = block_exclusive_scan<256>(dk, s_wsum[1], total_keys);
-  for (uint32_t e = tid; e <= (uint32_t)NS; e += 256) s_row0[e] = rslice[2 * NS + e];
-  if (tid < (uint32_t)RADIX) {
+  uint32_t before = block_exclusive_scan<256>(dk, s_wsum[1], total_keys);
+  for (uint32_t e = tid; e <= NS; e += 256) s_row0[e] = rslice[2 * NS + e];
 #pragma unroll
-    for (int xr = 0; xr < kRsvRanges; ++xr) {
-      const uint32_t e = tid * kRsvRanges + xr;
+  for (uint32_t q = 0; q < kMaxSpt; ++q) {
+    const uint32_t e = tid * SPT + q;
+    if (q < SPT && e < NS) {
       s_a0[e] = a0;
-      s_keys[e] = keys[xr];
-      a0 += (keys[xr] + TILE - 1) / TILE;
+      s_keys[e] = keys[q];
+      s_kb[e] = before;
+      a0 += (keys[q] + TILE - 1) / TILE;
+      before += keys[q];
     }
   }
   if (tid == 0) s_a0[NS] = listed;
   __syncthreads();
-  if (blockIdx.x == 0 && tid < (uint32_t)RADIX) {
-    cstart[tid] = before;
-    ctile0[tid] = FUSED ? s_row0[tid * kRsvRanges] : s_a0[tid * kRsvRanges];
+  if (blockIdx.x == 0) {
+    for (uint32_t c = tid; c < nc; c += 256) {
+      cstart[c] = s_kb[c * kRsvRanges];
+      ctile0[c] = FUSED ? s_row0[c * kRsvRanges] : s_a0[c * kRsvRanges];
+    }
     if (tid == 0) {
-      ctile0[RADIX] = FUSED ? s_row0[NS] : listed;  // (RADIX may equal the block: not thread RADIX's)
+      ctile0[nc] = FUSED ? s_row0[NS] : listed;
       *ntiles = listed;
     }
   }
@@ -3045,12 +3205,13 @@ hipError_t tiles_colscan(Workspace& ws, uint32_t* C, uint32_t tiles, hipStream_t
 // 10.03 -> 12.29 ms).  LIBSORT_DSTREAM=0 turns it off (A/B).
 // Reserved depth 0 (k_rsv_sample + k_tile_pass GEO & 4): the default for
 // keys-only 32-bit hybrid sorts; LIBSORT_HYB_RESERVE=0 keeps the count pass,
+// =nomem acts as if the slices could not be allocated (the same count pass),
 // =short halves every sampled capacity (tests: the overflow fallback).  Read
 // per call (the tests switch it in process).
 inline int rsv_mode() {
   const char* s = getenv("LIBSORT_HYB_RESERVE");
   if (!s) return 1;
-  return s[0] == '0' ? 0 : s[0] == 's' ? 2 : 1;
+  return s[0] == '0' ? 0 : s[0] == 's' ? 2 : s[0] == 'n' ? 3 : 1;
 }
 
 inline bool dstream_on() {
@@ -3376,7 +3537,17 @@ struct HybPieces {
   uint32_t tiles;       // T0 = sum over pieces of ceil(len / TILE)
   int depths;           // digit passes (the bucket sort covers W - BITS * depths bits)
   double fill;          // populated segments / nseg (sizes the bucket blocks)
+  const uint32_t* cum;  // [np + 1] keys before each piece (the reserved depth 0's sampler)
 };
+
+// Words of the reserved depth 0's slices: n keys plus each slice's sampled
+// slack (k_rsv_sample: (s + 5 sqrt(s) + 24) N / S per slice, rounded up to
+// whole tiles), over NS = nc * 8 slices, S samples per range: at most
+// n (1 + 5 sqrt(nc / S) + 25 nc / S) + NS * TILE.
+inline size_t rsv_capacity_bound_nc(size_t n, uint32_t nc, uint32_t S, uint32_t tile) {
+  const double f = 5.0 * std::sqrt((double)nc / S) + 25.0 * nc / S;
+  return n + (size_t)std::ceil((double)n * f) + (size_t)nc * kRsvRanges * tile + 1024;
+}
 
 // Depth 0 of a pre-partitioned input: tile t of piece p (first tile w <= t <
 // next piece's first tile) = (off + k * TILE, min(TILE, len - k * TILE), seg),
@@ -3456,13 +3627,28 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   // reserved depth 0 (32-bit keys only, in != out: the fallback re-reads in):
   // no count pass; depth 0 writes slices of ws.rsv (tile rows of depth 1
   // numbered by slice capacity, at most tb1)
+  // (pieces: slices per (segment, digit, range), at most kRsvMaxSlices)
   constexpr bool kRsvOk = sizeof(K) == 4 && std::is_same<V, NoValue>::value;
-  const int rmode = kRsvOk && !pc && DEPTHS > 1 && (const void*)in != (const void*)out ? rsv_mode() : 0;
-  const bool rsv = rmode != 0;
-  const uint32_t tb1 = (uint32_t)((rsv_capacity_bound(n, BITS) + TILE - 1) / TILE) + RADIX * kRsvRanges;
+  const uint32_t rnc = (pc ? nseg0 : 1u) * (uint32_t)RADIX;  // children of depth 0
+  const uint32_t rns = rnc * kRsvRanges;                      // slices
+  int rmode = kRsvOk && DEPTHS > 1 && (const void*)in != (const void*)out && (!pc || (pc->cum && rns <= kRsvMaxSlices))
+                  ? rsv_mode()
+                  : 0;
+  const size_t rbound = pc ? rsv_capacity_bound_nc(n, rnc, kRsvBlocks * 256 * kRsvPcPer, TILE)
+                           : rsv_capacity_bound(n, BITS);
+  const uint32_t tb1 = (uint32_t)((rbound + TILE - 1) / TILE) + rns;
   // the cursors after the slices, 256-byte aligned (8-bit: 64-bit adds)
-  const size_t rcur_off = (rsv_capacity_bound(n, BITS) + 63) & ~(size_t)63;
-  if (rsv) LS_TRY(ws.ensure_rsv(rcur_off + (size_t)RADIX * kRsvRanges * kRsvCurStride));
+  const size_t rcur_off = (rbound + 63) & ~(size_t)63;
+  // The slices (~1.14 n words at 4-bit digits, ~1.28 n at 8-bit) stay cached
+  // in the workspace like its other buffers (grow-only, freed by
+  // libsortRelease).  If they cannot be allocated, depth 0 takes the count
+  // pass instead: the sort needs no more memory than before.
+  // (LIBSORT_HYB_RESERVE=nomem: as if the allocation failed -- tests)
+  if (rmode == 3 || (rmode && ws.ensure_rsv(rcur_off + (size_t)rns * kRsvCurStride) != hipSuccess)) {
+    (void)hipGetLastError();
+    rmode = 0;
+  }
+  const bool rsv = rmode != 0;
   // segments of depth k (each child has at most one partial tile)
   auto nseg_at = [&](int k) { return nseg0 << (BITS * k); };
   auto tbound = [&](int k) { return k == 0 ? T0 : (k == 1 && rsv) ? tb1 : T0 + nseg_at(k); };
@@ -3471,8 +3657,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   LS_TRY(ws.ensure_tiles((size_t)TB * RADIX, ((size_t)tp_chunks(TB, BITS) + 1) * RADIX));
   // hybrid block: tiles[2] | segbase | cstart[2] | nsize | ctile0[2] | ntl | counters
   const size_t w_tiles = (size_t)TB * 4;
-  constexpr size_t kRsvWords = kRsvRanges * kRsvBlocks * RADIX + 3 * RADIX * kRsvRanges + 16;
-  const size_t words = 2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16 + kListCap + kRsvWords;
+  const size_t rsv_words = (size_t)kRsvRanges * kRsvBlocks * rnc + 3 * (size_t)rns + 16;
+  const size_t words = 2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16 + kListCap + rsv_words;
   LS_TRY(ws.ensure_hybrid(words));
   uint32_t* h = ws.hyb;
   uint4* tiles[2] = {reinterpret_cast<uint4*>(h), reinterpret_cast<uint4*>(h + w_tiles)};
@@ -3490,11 +3676,29 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   h += kListCap;
   // reserved depth 0: sample partials | slices (start | capacity | first tile,
   // + the tile count) | cursors | estimated digit sizes; ctr[14] = overflow
-  uint32_t* rpart = h; h += kRsvRanges * kRsvBlocks * RADIX;
-  uint32_t* rslice = h; h += 3 * RADIX * kRsvRanges + 16;
+  uint32_t* rpart = h; h += (size_t)kRsvRanges * kRsvBlocks * rnc;
+  uint32_t* rslice = h; h += 3 * (size_t)rns + 16;
   uint32_t* rcur = rsv ? ws.rsv + rcur_off : nullptr;  // kRsvCurStride apart
+  uint32_t* Cn0 = ws.tc[1];  // depth 1's count rows (the fused counts of depth 0)
   if (!rsv) {  // (reserved depth 0: k_rsv_sample sets them)
     hipLaunchKernelGGL(k_hyb_init, dim3(1), dim3(64), 0, st, ctr, NB);  // one launch, not two memsets (4 fills)
+    LS_TRY(hipGetLastError());
+  } else {
+    // Reserved depth 0: sample -> slices (the depth-0 pass reserves its runs
+    // in them; the next depth's tiles and child starts from the cursors)
+    const Op op0 = make_digit<Op>((uint32_t)(W - BITS), (uint32_t)RADIX - 1u, bias);
+    ScopedTimer tm("rsvsample", st, n);
+    if (pc) {
+      hipLaunchKernelGGL((k_rsv_sample_pc<RADIX, TILE, Op>), dim3(kRsvRanges * kRsvBlocks), dim3(256), 0, st,
+                         reinterpret_cast<const uint32_t*>(in), reinterpret_cast<const uint4*>(pc->dev), pc->cum,
+                         pc->np, nseg0, T0, (uint32_t)n, op0, rpart, rslice, rcur, ws.hyb_host, Cn0,
+                         BITS == 4 ? tb1 * (uint32_t)RADIX : 0u, ws.tticket + 32, ctr, NB, rmode == 2);
+    } else {
+      hipLaunchKernelGGL((k_rsv_sample<RADIX, TILE, Op>), dim3(kRsvRanges * kRsvBlocks), dim3(256), 0, st,
+                         reinterpret_cast<const uint32_t*>(in), (uint32_t)n, T0, op0, rpart, rslice, rcur,
+                         ws.hyb_host, Cn0, BITS == 4 ? tb1 * (uint32_t)RADIX : 0u, ws.tticket + 32, ctr, NB,
+                         rmode == 2);
+    }
     LS_TRY(hipGetLastError());
   }
   if (pc) {
@@ -3531,39 +3735,40 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     V* vdst = vbuf(k + 1);
     if constexpr (kRsvOk) {
       if (k == 0 && rsv) {
-        // Reserved depth 0: sample -> slices; the pass reserves its runs in
-        // them; the next depth's tiles and child starts from the cursors
-        {
-          ScopedTimer tm("rsvsample", st, n);
-          hipLaunchKernelGGL((k_rsv_sample<RADIX, TILE, Op>), dim3(kRsvRanges * kRsvBlocks), dim3(256), 0, st,
-                             reinterpret_cast<const uint32_t*>(in), (uint32_t)n, T0, op, rpart, rslice, rcur,
-                             ws.hyb_host, Cn, BITS == 4 ? tb1 * (uint32_t)RADIX : 0u, ws.tticket + 32, ctr, NB,
-                             rmode == 2);
-          LS_TRY(hipGetLastError());
-        }
+        // Reserved depth 0 (sampled above): the pass reserves its runs in the
+        // slices; the next depth's tiles and child starts from the cursors
         LS_TRY(hipEventRecord(ws.hyb_evt, st));
-        HybridGeo g0{nullptr, nullptr, nullptr, nullptr, nullptr, rcur, rslice, ctr + 14};
+        HybridGeo g0{tiles[0], ctr, nullptr, nullptr, nullptr, rcur, rslice, ctr + 14, rns};
         {
           ScopedTimer tm("tilepass", st, n);
-          hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 4, true>), dim3(T0), dim3(B), 0, st,
-                             src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase, Cn, g0);
+          if (pc)
+            hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 5, true>), dim3(T0), dim3(B), 0,
+                               st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase, Cn, g0);
+          else
+            hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 4, true>), dim3(T0), dim3(B), 0,
+                               st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase, Cn, g0);
           LS_TRY(hipGetLastError());
         }
         {
           ScopedTimer tm("hybplan", st, m);
           hipLaunchKernelGGL((k_rsv_tiles<RADIX, TILE, BITS == 4>), dim3((tb1 + 255) / 256), dim3(256), 0, st, rslice,
-                             rcur, ctr + 14, tb1, tiles[1], cstart[1], ctile0[1], ctr + 1, Cn);
+                             rcur, ctr + 14, tb1, tiles[1], cstart[1], ctile0[1], ctr + 1, Cn, rnc);
           LS_TRY(hipGetLastError());
         }
-        // skew check on the sampled digit sizes (the pass keeps the GPU busy;
-        // it wrote only ws.rsv, so abandoning leaves in intact)
+        // skew check on the sampled digit (pieces: child) sizes (the pass
+        // keeps the GPU busy; it wrote only ws.rsv, so abandoning leaves in
+        // intact)
         LS_TRY(hipEventSynchronize(ws.hyb_evt));
-        uint32_t mx = 0;
-        for (int d = 0; d < RADIX; ++d) mx = std::max(mx, ws.hyb_host[d]);
-        const double share = (double)n / (RADIX * fill);
-        if ((double)mx > 1.25 * share + 4.0 * std::sqrt(share) + 32.0 ||
-            (double)mx / (double)(NB / RADIX) > 0.9 * cap)
-          return hipSuccess;
+        if (pc) {
+          if ((double)ws.hyb_host[0] / (double)(1ull << (BITS * (DEPTHS - 1))) > 0.9 * cap) return hipSuccess;
+        } else {
+          uint32_t mx = 0;
+          for (int d = 0; d < RADIX; ++d) mx = std::max(mx, ws.hyb_host[d]);
+          const double share = (double)n / (RADIX * fill);
+          if ((double)mx > 1.25 * share + 4.0 * std::sqrt(share) + 32.0 ||
+              (double)mx / (double)(NB / RADIX) > 0.9 * cap)
+            return hipSuccess;
+        }
         continue;
       }
     }
@@ -3616,7 +3821,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
         LS_TRY(hipGetLastError());
       }
     }
-    HybridGeo geo{tiles[k & 1], ctr + k, cstart[(k + 1) & 1], ctile0[(k + 1) & 1], nullptr, nullptr, nullptr, nullptr};
+    HybridGeo geo{tiles[k & 1], ctr + k, cstart[(k + 1) & 1], ctile0[(k + 1) & 1], nullptr, nullptr, nullptr, nullptr, 0u};
     if (BITS == 8 && dstream && !last) geo.dout = ws.dstream;  // the next depth's digits
     {
       ScopedTimer tm("tilepass", st, n);
@@ -3807,9 +4012,9 @@ constexpr size_t kPiecesMinKeys = 1ull << 20;
 
 hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n,
                            const uint64_t* off, const uint64_t* len, const uint32_t* seg, size_t np, uint32_t nseg,
-                           int bits, int digit_bits, hipStream_t st) {
+                           int bits, int digit_bits, hipStream_t st, uint32_t bias) {
   if (n == 0) return hipSuccess;
-  if (n > 0xffffffffull || in == out || tmp == out || tmp == in || nseg == 0 || nseg > (1u << 20) || bits < 1 ||
+  if (n > 0xffffffffull || in == out || tmp == out || tmp == in || nseg == 0 || nseg > (1u << 20) || bits < 0 ||
       bits > 32 || (digit_bits != 4 && digit_bits != 8))
     return hipErrorInvalidValue;
   // the non-empty pieces, checked: segments non-decreasing and < nseg, offsets
@@ -3854,7 +4059,7 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   // (the 512 x 17-key block holds that + 3.5 sigma), within `bits`
   const int hyb = hybrid_mode_for(st);
   int depths = 0;
-  if (hyb == 2 ? n >= 1024 : (hyb == 1 && n >= kPiecesMinKeys)) {
+  if (bits > 0 && (hyb == 2 ? n >= 1024 : (hyb == 1 && n >= kPiecesMinKeys))) {
     for (int d = 1; d * digit_bits <= bits; ++d) {
       depths = d;
       if ((double)maxseg / std::ldexp(1.0, d * digit_bits) <= 8320.0) break;
@@ -3862,10 +4067,11 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
     if (((uint64_t)nseg << (digit_bits * depths)) > (1ull << 22)) depths = 0;
   }
   // host table (pinned staging, one upload): pieces uint4 (off, len, seg,
-  // first tile) | ctile0[nseg + 1] | cstart[nseg] | (8-byte aligned) the
-  // gather table of the fallback: src_off[K] | dst_off[K] | len[K] (uint64)
+  // first tile) | ctile0[nseg + 1] | cstart[nseg] | cum[K + 1] (keys before
+  // each piece) | (8-byte aligned) the gather table of the fallback:
+  // src_off[K] | dst_off[K] | len[K] (uint64)
   const uint32_t TILE = (uint32_t)(tp_block<uint32_t>(digit_bits) * tp_items<uint32_t>(digit_bits));
-  const size_t w32 = 4 * (size_t)K + 2 * (size_t)nseg + 1;
+  const size_t w32 = 4 * (size_t)K + 2 * (size_t)nseg + 1 + (size_t)K + 1;
   const size_t g64 = (w32 + 1) / 2;  // first uint64 word of the gather table
   LS_TRY(ws.ensure_seg(g64 + 3 * (size_t)K));
   LS_TRY(hipEventSynchronize(ws.seg_evt));  // the staging may still feed the previous upload
@@ -3873,6 +4079,7 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   uint64_t* hg = ws.seg_host + g64;
   uint32_t* ct0 = h32 + 4 * (size_t)K;
   uint32_t* cst = ct0 + nseg + 1;
+  uint32_t* pcum = cst + nseg;
   {
     uint64_t run = 0;
     for (uint32_t s = 0; s < nseg; ++s) {
@@ -3880,13 +4087,15 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
       run += segsize[s];
     }
   }
-  uint32_t tile = 0, i = 0;
+  uint32_t tile = 0, i = 0, run = 0;
   std::vector<uint64_t> dpos(cst, cst + nseg);
   for (uint32_t s = 0; s <= nseg; ++s) {
     ct0[s] = tile;  // segment s's pieces start at this tile
     for (; i < K && (s == nseg || cseg[seg[keep[i]]] == s); ++i) {
       const size_t p = keep[i];
       const uint32_t cs = cseg[seg[p]];
+      pcum[i] = run;
+      run += (uint32_t)len[p];
       h32[4 * (size_t)i + 0] = (uint32_t)off[p];
       h32[4 * (size_t)i + 1] = (uint32_t)len[p];
       h32[4 * (size_t)i + 2] = cs;
@@ -3898,14 +4107,20 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
       dpos[cs] += len[p];
     }
   }
+  pcum[K] = run;
   LS_TRY(hipMemcpyAsync(ws.seg_dev, ws.seg_host, (g64 + 3 * (size_t)K) * sizeof(uint64_t), hipMemcpyHostToDevice,
                         st));
   LS_TRY(hipEventRecord(ws.seg_evt, st));
   if (depths > 0) {
-    HybPieces pc{reinterpret_cast<const uint32_t*>(ws.seg_dev), K, nseg, tile, depths, (double)npop / nseg};
+    const uint32_t* dev32 = reinterpret_cast<const uint32_t*>(ws.seg_dev);
+    HybPieces pc{dev32, K, nseg, tile, depths, (double)npop / nseg, dev32 + (pcum - h32)};
     bool handled = false;
     NoValue* nv = nullptr;
-    if (digit_bits == 4)
+    if (bias && digit_bits == 4)
+      LS_TRY((sort_hybrid<4, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, bias, st, &handled, 0, &pc)));
+    else if (bias)
+      LS_TRY((sort_hybrid<8, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, bias, st, &handled, 0, &pc)));
+    else if (digit_bits == 4)
       LS_TRY((sort_hybrid<4, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, 0u, st, &handled, 0, &pc)));
     else
       LS_TRY((sort_hybrid<8, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, 0u, st, &handled, 0, &pc)));
@@ -3915,7 +4130,9 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
     }
   }
   // small or skewed: gather the pieces into segment order, LSD sort in place
+  // (bits == 0: the segments are single values, already in order)
   LS_TRY(segment_copy_dev_u32(in, out, ws.seg_dev + g64, K, maxlen, n, st));
+  if (bits == 0) return hipSuccess;
   return sort_impl<uint32_t, NoValue>(ws, out, out, tmp, nullptr, nullptr, nullptr, n, 0, 32, digit_bits, st);
 }
 
@@ -4037,21 +4254,20 @@ hipError_t partition_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_
 }
 
 namespace {
-// One tile-offset pass whose digit is a table lookup: per-tile counts, column
-// scan, pass kernel; bucket starts = row 0 of the scanned chunk totals.
-// u64 keys: the table indexes the top bits of the key's high word.
-template <int BITS, typename K, typename V>
-hipError_t partition_lut_impl(Workspace& ws, const K* in, K* out, const V* vin, V* vout, size_t n,
-                              const uint8_t* d_lut, int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st,
-                              int phase) {
+// One tile-offset pass whose digit is `op` (a table lookup, or the 8-bit
+// digit of key - bias): per-tile counts, column scan, pass kernel; bucket
+// starts = row 0 of the scanned chunk totals.  u64 keys: the table indexes
+// the top bits of the key's high word.
+template <int BITS, typename K, typename V, typename Op>
+hipError_t partition_op_impl(Workspace& ws, const K* in, K* out, const V* vin, V* vout, size_t n, Op op,
+                             const Workspace::PartToken& tok, int nbuckets, uint32_t* d_bounds, hipStream_t st,
+                             int phase) {
   constexpr int RADIX = 1 << BITS;
   constexpr int B = tp_block<K>(BITS);
   const uint32_t tiles = tp_tiles<K>(n, BITS);
-  const LutDigit op{d_lut, (uint32_t)lut_shift, (uint32_t)RADIX - 1u, nullptr};
-  Workspace::PartToken tok{in, vin, n, d_lut, lut_shift, nbuckets, st, true};
   if (phase != kPartScatter) {
     LS_TRY(ws.ensure_tiles((size_t)tiles * RADIX, ((size_t)tp_chunks(tiles, BITS) + 1) * RADIX));
-    LS_TRY((tiles_counts<BITS, K, LutDigit>(ws, in, n, op, tiles, ws.tc[0], nullptr, 0, st)));
+    LS_TRY((tiles_counts<BITS, K, Op>(ws, in, n, op, tiles, ws.tc[0], nullptr, 0, st)));
     LS_TRY(tiles_colscan<BITS>(ws, ws.tc[0], tiles, st));
     if (d_bounds)
       LS_TRY(hipMemcpyAsync(d_bounds, tiles_digit_starts(ws, tiles, BITS), (size_t)nbuckets * sizeof(uint32_t),
@@ -4066,12 +4282,22 @@ hipError_t partition_lut_impl(Workspace& ws, const K* in, K* out, const V* vin, 
   ws.part_pending.valid = false;
   {
     ScopedTimer tm("partition", st, n);
-    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(BITS), K, V, false, LutDigit>), dim3(tiles), dim3(B), 0, st, in,
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(BITS), K, V, false, Op>), dim3(tiles), dim3(B), 0, st, in,
                        out, vin, vout, (uint32_t)n, op, RadixDigit{0u, 1u}, ws.tc[0], (const uint32_t*)ws.tb,
                        (const uint32_t*)tiles_digit_starts(ws, tiles, BITS), ws.tc[1], HybridGeo{});
     LS_TRY(hipGetLastError());
   }
   return hipSuccess;
+}
+
+template <typename K, typename V>
+bool partition_args_ok(const K* in, K* out, const V* vin, V* vout, size_t n, int phase) {
+  const bool need_out = phase != kPartCount;
+  if (!in || (need_out && (!out || (const void*)in == (const void*)out))) return false;
+  if constexpr (!std::is_same<V, NoValue>::value) {
+    if (!vin || (need_out && (!vout || (const void*)vin == (const void*)vout))) return false;
+  }
+  return n <= 0xffffffffull;
 }
 
 template <typename K, typename V>
@@ -4085,19 +4311,75 @@ hipError_t partition_lut_any(Workspace& ws, const K* in, K* out, const V* vin, V
       LS_TRY(hipMemsetAsync(d_bounds, 0, (size_t)nbuckets * sizeof(uint32_t), st));
     return hipSuccess;
   }
-  const bool need_out = phase != kPartCount;
-  if (!in || !d_lut || (need_out && (!out || (const void*)in == (const void*)out)) ||
-      (reinterpret_cast<uintptr_t>(d_lut) & 3u))
+  if (!partition_args_ok(in, out, vin, vout, n, phase) || !d_lut || (reinterpret_cast<uintptr_t>(d_lut) & 3u))
     return hipErrorInvalidValue;
-  if constexpr (!std::is_same<V, NoValue>::value) {
-    if (!vin || (need_out && (!vout || (const void*)vin == (const void*)vout))) return hipErrorInvalidValue;
-  }
+  const Workspace::PartToken tok{in, vin, n, d_lut, lut_shift, nbuckets, 0, st, true};
   // digit width by bucket count: 16 -> 4-bit tiles, 32 -> 5-bit (the 8-rank x 4-round exchange), else 8-bit
   if (nbuckets <= 16)
-    return partition_lut_impl<4, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st, phase);
+    return partition_op_impl<4, K, V>(ws, in, out, vin, vout, n, LutDigit{d_lut, (uint32_t)lut_shift, 15u, nullptr},
+                                      tok, nbuckets, d_bounds, st, phase);
   if (nbuckets <= 32)
-    return partition_lut_impl<5, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st, phase);
-  return partition_lut_impl<8, K, V>(ws, in, out, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st, phase);
+    return partition_op_impl<5, K, V>(ws, in, out, vin, vout, n, LutDigit{d_lut, (uint32_t)lut_shift, 31u, nullptr},
+                                      tok, nbuckets, d_bounds, st, phase);
+  return partition_op_impl<8, K, V>(ws, in, out, vin, vout, n, LutDigit{d_lut, (uint32_t)lut_shift, 255u, nullptr},
+                                    tok, nbuckets, d_bounds, st, phase);
+}
+
+// 256 buckets by the 8-bit digit (key - bias) >> shift (keys in [bias, bias +
+// 2^(shift + 8)): the digit is masked, so a key outside only lands in a wrong
+// bucket, never outside the counters).
+template <typename K, typename V>
+hipError_t partition_range_any(Workspace& ws, const K* in, K* out, const V* vin, V* vout, size_t n, uint64_t bias,
+                               int shift, uint32_t* d_bounds, hipStream_t st, int phase) {
+  if (n > 0xffffffffull || shift < 0 || shift + 8 > 8 * (int)sizeof(K)) return hipErrorInvalidValue;
+  if (n == 0) {
+    if (d_bounds && phase != kPartScatter) LS_TRY(hipMemsetAsync(d_bounds, 0, 256 * sizeof(uint32_t), st));
+    return hipSuccess;
+  }
+  if (!partition_args_ok(in, out, vin, vout, n, phase)) return hipErrorInvalidValue;
+  const Workspace::PartToken tok{in, vin, n, nullptr, shift, 256, bias, st, true};
+  if constexpr (sizeof(K) == 4)
+    return partition_op_impl<8, K, V>(ws, in, out, vin, vout, n, BiasedDigit{(uint32_t)shift, 255u, (uint32_t)bias},
+                                      tok, 256, d_bounds, st, phase);
+  else
+    return partition_op_impl<8, K, V>(ws, in, out, vin, vout, n, BiasedDigit64{bias, (uint32_t)shift, 255u}, tok,
+                                      256, d_bounds, st, phase);
+}
+
+// min and max of the keys into d_mm[0], d_mm[1] (d_mm[0] starts at ~0, d_mm[1]
+// at 0: k_minmax_init)
+template <typename K>
+__global__ void k_minmax_init(K* mm) {
+  mm[0] = ~(K)0;
+  mm[1] = 0;
+}
+template <typename K>
+__global__ __launch_bounds__(256) void k_minmax(const K* __restrict__ keys, uint64_t n, K* __restrict__ mm) {
+  K lo = ~(K)0, hi = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    const K x = load_stream(&keys[i]);
+    lo = x < lo ? x : lo;
+    hi = x > hi ? x : hi;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const K a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if ((threadIdx.x & (kWave - 1)) == 0) {
+    atomicMin(&mm[0], lo);
+    atomicMax(&mm[1], hi);
+  }
+}
+template <typename K>
+hipError_t minmax_any(Workspace& ws, const K* keys, size_t n, K* d_mm, hipStream_t st) {
+  hipLaunchKernelGGL(k_minmax_init<K>, dim3(1), dim3(1), 0, st, d_mm);
+  LS_TRY(hipGetLastError());
+  if (n == 0) return hipSuccess;
+  ScopedTimer tm("minmax", st, n);
+  const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, (uint64_t)std::max(1, ws.num_cus) * 8);
+  hipLaunchKernelGGL(k_minmax<K>, dim3((uint32_t)blocks), dim3(256), 0, st, keys, (uint64_t)n, d_mm);
+  return hipGetLastError();
 }
 }  // namespace
 
@@ -4112,6 +4394,25 @@ hipError_t partition_lut_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const
                                        uint32_t* d_bounds, hipStream_t st, int phase) {
   return partition_lut_any<uint64_t, uint32_t>(ws, kin, kout, vin, vout, n, d_lut, lut_shift, nbuckets, d_bounds, st,
                                                phase);
+}
+
+hipError_t partition_range_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, uint32_t bias, int shift,
+                               uint32_t* d_bounds, hipStream_t st, int phase) {
+  return partition_range_any<uint32_t, NoValue>(ws, in, out, nullptr, nullptr, n, bias, shift, d_bounds, st, phase);
+}
+
+hipError_t partition_range_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
+                                         uint32_t* vout, size_t n, uint64_t bias, int shift, uint32_t* d_bounds,
+                                         hipStream_t st, int phase) {
+  return partition_range_any<uint64_t, uint32_t>(ws, kin, kout, vin, vout, n, bias, shift, d_bounds, st, phase);
+}
+
+hipError_t minmax_u32(Workspace& ws, const uint32_t* keys, size_t n, uint32_t* d_mm, hipStream_t st) {
+  return minmax_any<uint32_t>(ws, keys, n, d_mm, st);
+}
+
+hipError_t minmax_u64(Workspace& ws, const uint64_t* keys, size_t n, uint64_t* d_mm, hipStream_t st) {
+  return minmax_any<uint64_t>(ws, keys, n, d_mm, st);
 }
 
 hipError_t segment_copy_dev_u32(const uint32_t* src, uint32_t* dst, const uint64_t* d_tab, size_t nseg,

@@ -153,10 +153,12 @@ def stable_sort_kv64v64(k, v):
     return kk, vv
 
 
-def sorted_pcg_sha256(n, first=0, chunk_values=1 << 24):
+def sorted_pcg_sha256(n, first=0, chunk_values=1 << 24, shift=0):
     """sha256 (hex) of std::sort of elements [first, first+n) of the
     populateInput stream, little-endian uint32, without sorting: a one-byte
-    count per value (4 GiB), expanded in value order chunk by chunk."""
+    count per value (4 GiB), expanded in value order chunk by chunk.
+    shift > 0: of the keys x >> shift instead (a monotone map, so the sorted
+    stream is the sorted one shifted)."""
     import hashlib
     counts = np.zeros(1 << 32, dtype=np.uint8)
     mx = lib().oracle_pcg_value_counts(counts.ctypes.data, n, first)
@@ -168,7 +170,7 @@ def sorted_pcg_sha256(n, first=0, chunk_values=1 << 24):
         c = counts[a:a + chunk_values]
         nz = np.nonzero(c)[0]
         if nz.size:
-            vals = np.repeat((nz + a).astype(np.uint32), c[nz])
+            vals = np.repeat(((nz + a) >> shift).astype(np.uint32), c[nz])
             total += vals.size
             h.update(vals.astype("<u4").tobytes())
     assert total == n

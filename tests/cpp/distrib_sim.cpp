@@ -49,23 +49,39 @@ static void apply(const std::vector<Piece>& ps, const std::vector<Vec>& src, std
   for (const Piece& p : ps) memcpy(dst[p.dst].data() + p.dst_off, src[p.src].data() + p.src_off, p.count * 4);
 }
 
-// top-digit rounds: exact digit counts, stable partition by key >> 24, the
-// plan, the rounds (the receiver's piece table checked piece by piece: inside
-// the round, the right digit, covering the round exactly), re-cut
-static bool run_msd(const Vec& x, int R, int K, double growth) {
+// top-digit rounds: exact digit counts, stable partition by key >> 24 (or,
+// range = true, as the engine does when that plan is too skewed: by the
+// range digit (key - min) >> shift, distrib_plan.h range_digit), the plan,
+// the rounds (the receiver's piece table checked piece by piece: inside the
+// round, the right digit, covering the round exactly), re-cut.  balanced:
+// the plan must not be too skewed (msd_too_skewed false).
+static bool run_msd(const Vec& x, int R, int K, double growth, bool range = false, bool balanced = false) {
   std::vector<Vec> in = split(x, R);
+  uint64_t bias = 0;
+  int shift = kTopShift;
+  if (range) {
+    uint64_t lo = ~0ull, hi = 0;
+    for (uint32_t k : x) {
+      lo = std::min<uint64_t>(lo, k);
+      hi = std::max<uint64_t>(hi, k);
+    }
+    CHECK(range_digit(lo, hi, 32, &bias, &shift), "range digit not useful");
+  }
+  auto dig = [&](uint32_t k) -> uint32_t { return ((k - (uint32_t)bias) >> shift) & (kTopDigits - 1); };
   std::vector<std::vector<uint64_t>> C(R, std::vector<uint64_t>(kTopDigits, 0));
   std::vector<Vec> part(R);
   for (int r = 0; r < R; ++r) {
-    for (uint32_t k : in[r]) C[r][k >> kTopShift]++;
+    for (uint32_t k : in[r]) C[r][dig(k)]++;
     std::vector<uint64_t> at(kTopDigits + 1, 0);
     for (int g = 0; g < kTopDigits; ++g) at[g + 1] = at[g] + C[r][g];
     part[r].resize(in[r].size());
-    for (uint32_t k : in[r]) part[r][at[k >> kTopShift]++] = k;  // stable
+    for (uint32_t k : in[r]) part[r][at[dig(k)]++] = k;  // stable
   }
   std::vector<uint8_t> lut(kTopDigits);
   std::vector<int64_t> est(R);
   plan_digit_rounds(C, K, growth, lut.data(), est.data());
+  CHECK(!balanced || !msd_too_skewed(est.data(), R, x.size()), "plan too skewed (R=%d n=%zu range=%d)", R, x.size(),
+        (int)range);
   uint64_t tot = 0;
   for (int r = 0; r < R; ++r) tot += (uint64_t)est[r];
   CHECK(tot == x.size(), "est sum %llu != %zu", (unsigned long long)tot, x.size());
@@ -103,8 +119,8 @@ static bool run_msd(const Vec& x, int R, int K, double growth) {
         for (uint64_t t = 0; t < m; ++t) {
           CHECK(!seen[o + t], "pieces overlap");
           seen[o + t] = 1;
-          CHECK((int)(recv[r][a + o + t] >> kTopShift) == lo + (int)sg, "key of digit %u in segment %u",
-                recv[r][a + o + t] >> kTopShift, sg);
+          CHECK((int)dig(recv[r][a + o + t]) == lo + (int)sg, "key of digit %u in segment %u",
+                dig(recv[r][a + o + t]), sg);
         }
         covered += m;
       }
@@ -181,6 +197,10 @@ static Vec make(const std::string& kind, size_t n, uint64_t seed) {
     std::fill(x.begin(), x.end(), 12345u);
   } else if (kind == "skewtop") {
     for (auto& v : x) v = (uint32_t)(g() % (1u << 20));
+  } else if (kind == "below26") {  // keys below 2^26: 4 top digits
+    for (auto& v : x) v = (uint32_t)(g() % (1u << 26));
+  } else if (kind == "offset") {  // a 2^25-wide range at 2^31
+    for (auto& v : x) v = (1u << 31) + (uint32_t)(g() % (1u << 25));
   } else if (kind == "sorted" || kind == "reverse") {
     for (auto& v : x) v = (uint32_t)g();
     std::sort(x.begin(), x.end());
@@ -208,6 +228,13 @@ int main() {
           ++cases;
         }
       }
+  // the range digit (the engine's re-partition when the top digit is too
+  // skewed): narrow key ranges spread over every rank, balanced
+  for (const char* k : {"below26", "offset", "skewtop"})
+    for (int R : {2, 3, 5, 8}) {
+      run_msd(make(k, 300007, R), R, 4, 1.2, true, true);
+      ++cases;
+    }
   // R * K = 256 groups (the table limit): most digits a group of their own
   run_msd(make("wide", 100003, 5), 2, 128, 1.2);
   run_msd(make("pcg", 300007, 6), 64, 4, 1.2);

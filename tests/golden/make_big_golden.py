@@ -12,7 +12,13 @@ test_maximum_size, test_config5_pairs_size), computed with the oracle here
                 2i+1, the first n/64 keys masked to 11 bits (many ties),
                 payload_i = i.
 
-Run: python tests/golden/make_big_golden.py
+  2^29 class:   the sorted hashes of the 2^29-class local sorts
+                (test_gpu_hybrid.test_hybrid_auto_2pow29_class: n keys from
+                element n of the stream) and of the 8-GPU per-rank shape
+                (2^29 keys >> 3, test_gpu_distrib_abi.test_shape8_2pow29).
+
+Run: python tests/golden/make_big_golden.py          (everything)
+     python tests/golden/make_big_golden.py 2pow29   (adds the 2^29 class)
 """
 import hashlib
 import json
@@ -57,5 +63,27 @@ def main():
     (ROOT / "tests" / "golden" / "big_golden.json").write_text(json.dumps(out, indent=1) + "\n")
 
 
+def add_2pow29():
+    path = ROOT / "tests" / "golden" / "big_golden.json"
+    out = json.loads(path.read_text())
+    gold = json.loads((ROOT / "tests" / "golden" / "pcg_golden.json").read_text())["sha256_prefix"]
+    h = oracle.sorted_pcg_sha256(1 << 20)  # the pin first
+    assert h[:16] == gold[str(1 << 20)]["sorted"], h
+    at = out.setdefault("sorted_u32_first", {})
+    for n in ((1 << 29) + 12345, 400000007):
+        t = time.time()
+        at["%d@%d" % (n, n)] = oracle.sorted_pcg_sha256(n, first=n)
+        print(n, at["%d@%d" % (n, n)], "%.0f s" % (time.time() - t), flush=True)
+    sh = out.setdefault("sorted_u32_shift", {})
+    n = 1 << 29
+    t = time.time()
+    sh["%d>>3" % n] = oracle.sorted_pcg_sha256(n, shift=3)
+    print(n, ">> 3", sh["%d>>3" % n], "%.0f s" % (time.time() - t), flush=True)
+    path.write_text(json.dumps(out, indent=1) + "\n")
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["2pow29"]:
+        add_2pow29()
+    else:
+        main()

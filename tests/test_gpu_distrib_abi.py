@@ -99,6 +99,50 @@ def test_ranks_sharing_the_gpu(D, oracle_mod, R, lsd, case):
     _check(oracle_mod, x, outs, R, lsd)
 
 
+def _timed_names(D, fn, *names):
+    """Runs fn with the per-kernel timing registry on; returns fn's result and
+    the launch count of each named timer."""
+    D.timing_enable(True)
+    D.timing_reset()
+    try:
+        out = fn()
+        torch.cuda.synchronize()
+        return out, [D.timing_query(nm)[0] for nm in names]
+    finally:
+        D.timing_enable(False)
+
+
+@pytest.mark.parametrize("R", [3, 8])
+@pytest.mark.parametrize("case", ["below2pow26", "offset_narrow", "one_digit_dups"])
+def test_range_digit_rounds(D, oracle_mod, R, case):
+    """Keys whose top 8 bits take fewer values than there are ranks (below
+    2^26 at 8 ranks; a 2^25-wide range at 2^31; 40 values inside one top
+    digit): the top-digit plan is too skewed, so the rounds re-partition by
+    the 8-bit digit of key - min over the populated range instead of falling
+    back to the 4-exchange LSD rounds (ADVICE r03).  Exact against the oracle;
+    the LSD rounds did not run (no "lsdround" launches) and the min/max
+    kernel ran once per rank."""
+    rng = np.random.default_rng(R)
+    n = (1 << 21) + 77
+    if case == "below2pow26":
+        x = rng.integers(0, 1 << 26, n, dtype=np.uint64).astype(np.uint32)
+    elif case == "offset_narrow":
+        x = (rng.integers(0, 1 << 25, n, dtype=np.uint64) + (1 << 31)).astype(np.uint32)
+    else:  # 40 distinct values a few apart: shift 0, one value per digit
+        x = (rng.integers(0, 40, n, dtype=np.uint64) * 3 + 0x7F000000).astype(np.uint32)
+    outs, (nlsd, nmm) = _timed_names(D, lambda: _run(D, x, R, COPY), "lsdround", "minmax")
+    _check(oracle_mod, x, outs, R, False)
+    assert nlsd == 0 and nmm == R, (nlsd, nmm)
+
+
+def test_range_digit_all_equal_takes_lsd(D, oracle_mod):
+    """One distinct key: no digit splits it, so the LSD rounds run (exact)."""
+    x = np.full(300001, 0xDEADBEEF, dtype=np.uint32)
+    outs, (nlsd,) = _timed_names(D, lambda: _run(D, x, 4, COPY), "lsdround")
+    _check(oracle_mod, x, outs, 4, False)
+    assert nlsd > 0
+
+
 def test_repeated_calls_reuse_the_context(D, oracle_mod):
     """Same ranks, different sizes and inputs back to back (grow-only
     buffers, cached communicator, stream ordering of the workspaces)."""
@@ -139,6 +183,30 @@ def test_reference_size_over_rccl(D, golden):
     assert pylibsort.lib().libsortDeviceErrors() == 0
 
 
+@pytest.mark.slow
+def test_shape8_2pow29(D):
+    """configs[3]'s per-rank size in the 8-GPU shape (2^29 keys of the stream
+    >> 3: the keys of 32 top digits, as one of 8 ranks receives them; round
+    sorts of 8 segments of ~2^24 keys, the reserved depth 0 of the piece sort)
+    through one RCCL rank with every piece through RCCL: the oracle's sha256
+    (big_golden.json "sorted_u32_shift", monotone map of the pinned sorted
+    stream).  Reference: localTest/tests.cpp:137-143 (GPU == CPU)."""
+    import json
+    import pathlib
+    big = json.loads((pathlib.Path(__file__).with_name("golden") / "big_golden.json").read_text())
+    n = 1 << 29
+    x = D.populate_u32(n)
+    x >>= 3
+    out = D.distrib_sort_u32([x], SELF_RCCL)[0]
+    del x
+    h = hashlib.sha256()
+    for i in range(0, n, 1 << 26):
+        h.update(out[i:i + (1 << 26)].cpu().numpy().view("<u4").tobytes())
+    assert h.hexdigest() == big["sorted_u32_shift"]["%d>>3" % n]
+    del out
+    torch.cuda.empty_cache()
+
+
 def _pair_case(oracle, case):
     rng = np.random.default_rng(len(case))
     if case == "c5":            # configs[4]'s pairs: key = draw 2i << 32 | draw 2i+1
@@ -148,11 +216,15 @@ def _pair_case(oracle, case):
         return rng.integers(0, 1 << 12, 300007, dtype=np.uint64) * np.uint64(0x0010000100000001)
     if case == "onekey":
         return np.full(100003, 0x123456789ABCDEF0, dtype=np.uint64)
+    if case == "below2pow40":   # IDs: every key in top digit 0 (range partition)
+        return rng.integers(0, 1 << 40, 400009, dtype=np.uint64)
+    if case == "stamps":        # ns timestamps of one day: one shared top byte, ties included
+        return np.uint64(0x17A0000000000000) + rng.integers(0, 86400 * 10**9, 400009, dtype=np.uint64) // np.uint64(1000)
     return rng.integers(0, 1 << 63, 5, dtype=np.uint64)  # tiny: empty shards at 8 ranks
 
 
 @pytest.mark.parametrize("R", [1, 2, 3, 5, 8])
-@pytest.mark.parametrize("case", ["c5", "ties", "onekey", "tiny"])
+@pytest.mark.parametrize("case", ["c5", "ties", "onekey", "tiny", "below2pow40", "stamps"])
 def test_pairs_engine(D, oracle_mod, bits, R, case):
     """configs[4] behind the C ABI (libsortDistribSortPairsU64U32): one RCCL
     rank with every piece through RCCL, or R ranks sharing the GPU; the
@@ -170,6 +242,27 @@ def test_pairs_engine(D, oracle_mod, bits, R, case):
     assert [t.numel() for t in ko] == [max(0, min(n, (r + 1) * S) - r * S) for r in range(R)]
     np.testing.assert_array_equal(np.concatenate([t.cpu().numpy().view(np.uint64) for t in ko]), rk)
     np.testing.assert_array_equal(np.concatenate([t.cpu().numpy().view(np.uint32) for t in vo]), rv)
+
+
+@pytest.mark.parametrize("case", ["below2pow40", "stamps"])
+def test_pairs_range_digit(D, oracle_mod, case):
+    """Pair keys below 2^56 or sharing their top byte: the top-digit plan
+    would send every pair to one rank, so the engine re-partitions by the
+    8-bit digit over the populated key range (the min/max kernel runs once
+    per rank); exact and stable against the oracle.  (The balance itself is
+    host arithmetic, checked in tests/cpp/distrib_sim.cpp.)"""
+    R = 4
+    k = _pair_case(oracle_mod, case)
+    n = k.size
+    v = np.arange(n, dtype=np.uint32)
+    S = -(-n // R)
+    ks = [torch.from_numpy(k[r * S:(r + 1) * S].view(np.int64).copy()).cuda() for r in range(R)]
+    vs = [torch.from_numpy(v[r * S:(r + 1) * S].view(np.int32).copy()).cuda() for r in range(R)]
+    (ko, vo), (nmm,) = _timed_names(D, lambda: D.distrib_sort_pairs_u64_u32(ks, vs, COPY), "minmax")
+    rk, rv = oracle_mod.stable_sort_kv64(k, v)
+    np.testing.assert_array_equal(np.concatenate([t.cpu().numpy().view(np.uint64) for t in ko]), rk)
+    np.testing.assert_array_equal(np.concatenate([t.cpu().numpy().view(np.uint32) for t in vo]), rv)
+    assert nmm == R
 
 
 def test_pairs_engine_rejects_lsd(D):

@@ -104,3 +104,36 @@ def test_worker_device_path_when_pylibsort_is_imported_first(tmp_path):
             "print('OK')" % (str(root), str(root / "gpu-radix-sort_amd"), str(tmp_path)))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+@pytest.mark.parametrize("handler", ["f", "fDevice"])
+def test_distrib_worker_two_partrefs(mount, oracle_mod, handler):
+    """The reference's DistribWorkerTest (benchmark/pkg/sort/testHelpers.go:
+    324-388, run by distrib_test.go:14-24 as TestLocalDistribWorker /
+    ...File): 1021 keys of a fresh generator stream written to one
+    partition of array "initial"; the worker reads it as TWO PartRefs (bytes
+    [0, 510*4) and [510*4, 1021*4) of partition 0) and partial-sorts their
+    concatenation at offset 0, width 4.  The output array must have 16
+    partitions holding all 4084 bytes, and reading them back in order gives
+    the stable partition by the low 4 bits (checkPartial,
+    testHelpers.go:411-448) -- here compared bit for bit with the oracle."""
+    from pylibsort import data as D
+    from pylibsort import faas
+    n, width = 1021, 4
+    x = oracle_mod.pcg(n)
+    arr = D.fileDistribArray.Create(mount / "initial", D.ArrayShape.fromUniform(n * 4, 1))
+    arr.WriteAll(x.tobytes())
+    arr.Close()
+    half = (n // 2) * 4
+    refs = [{"arrayName": "initial", "partID": 0, "start": 0, "nbyte": half},
+            {"arrayName": "initial", "partID": 0, "start": half, "nbyte": n * 4 - half}]
+    req = {"offset": 0, "width": width, "arrType": "file", "input": refs, "output": "testDistribWorker"}
+    assert getattr(faas, handler)(req) == {"success": True, "err": ""}
+    out = D.fileDistribArray.Open(mount / "testDistribWorker")
+    assert len(out.shape.lens) == 1 << width
+    assert sum(out.shape.lens) == n * 4
+    got = np.frombuffer(out.ReadAll(), dtype=np.uint32)
+    d, b = oracle_mod.partial_u32(x, 0, width)
+    np.testing.assert_array_equal(got, d)
+    assert out.shape.lens == np.diff(b.astype(np.int64) * 4, append=4 * n).tolist()
+    out.Close()

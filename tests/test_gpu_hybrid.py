@@ -504,24 +504,24 @@ def test_graph_capture_skips_the_host_waits(dev, oracle_mod):
 def test_hybrid_auto_2pow29_class(dev, bits, n):
     """Full sorts of 2^28 + 2^24 .. 2^29 + 2^23 keys take the hybrid with
     the 512-thread bucket blocks (buckets of ~6-8K keys; configs[3]'s 2^29
-    keys per GPU): equal to the LSD sort of the same keys (libsortSetHybrid
-    off), which the parity suite pins bit-exact, and one bucket-sort launch
-    pair ran."""
-    import pylibsort
+    keys per GPU): the sha256 of the sorted keys equals the oracle's
+    (tests/golden/big_golden.json "sorted_u32_first", made by
+    make_big_golden.py from the counting-sort restatement pinned on the
+    reference's own hashes), and one bucket-sort launch pair ran."""
+    import hashlib
+    import json
+    import pathlib
+    big = json.loads((pathlib.Path(__file__).with_name("golden") / "big_golden.json").read_text())
     x = dev.populate_u32(n, first=n)
     out = torch.empty_like(x)
     tmp = torch.empty_like(x)
     got, nbs, npass = _sort_counting(dev, x, out=out, tmp=tmp)
     assert nbs == 1 and npass == 16 // bits, (nbs, npass)  # 16 / bits digit passes + the bucket sort, no fallback
-    ref = torch.empty_like(x)
-    prev = pylibsort.setHybrid("off")
-    try:
-        dev.sort_keys_u32(x, out=ref, tmp=tmp)
-    finally:
-        pylibsort.setHybrid(prev)
-    torch.cuda.synchronize()
-    assert torch.equal(got, ref)
-    del x, out, tmp, ref
+    h = hashlib.sha256()
+    for i in range(0, n, 1 << 26):
+        h.update(got[i:i + (1 << 26)].cpu().numpy().view("<u4").tobytes())
+    assert h.hexdigest() == big["sorted_u32_first"]["%d@%d" % (n, n)]
+    del x, out, tmp
     torch.cuda.empty_cache()
 
 
@@ -607,3 +607,56 @@ def test_reserved_depth0_range_sort(dev, oracle_mod, digit4, force, monkeypatch)
     out = dev.sort_keys_range_u32(_tensor(x), lo, lo + 0x5000000)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+
+
+def test_reserved_depth0_nomem_falls_back(dev, oracle_mod, digit4, force, monkeypatch):
+    """The slices cannot be allocated (LIBSORT_HYB_RESERVE=nomem acts as a
+    failed allocation): depth 0 takes the count pass and the hybrid still
+    runs to its bucket sort (the sort must not fail)."""
+    monkeypatch.setenv("LIBSORT_HYB_RESERVE", "nomem")
+    n = (1 << 22) + 5
+    x = oracle_mod.pcg(n, first=n + 3)
+    out, nbs = _sort_counting_buckets(dev, _tensor(x))
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
+    assert nbs == 1
+
+
+@pytest.mark.parametrize("mask", [0xFFFF0000, 0xFFFF0003], ids=["low16_const", "low16_four"])
+def test_counting_bucket_duplicates_full_size(dev, oracle_mod, bits, mask):
+    """Duplicate-heavy keys at the bench size (2^28, auto mode): every 16-bit
+    bucket holds ~4096 keys of one (or four) values, so the counting
+    placement's 3-bit counts overflow in every bucket and the block sorts it
+    by the LSD steps instead (no per-cell search, whose cost grew
+    with the square of the cell).  Exact: masking the low bits is monotone, so
+    sort(x & m) == sort(x) & m, and sort(x) is pinned by the oracle's hash.
+    Timed against the uniform sort: within 3x (the quadratic search was ~100x)."""
+    import hashlib
+    import time
+    n = 1 << 28
+    x = dev.populate_u32(n, first=0)
+    ref = dev.sort_keys_u32(x)
+    torch.cuda.synchronize()
+    h = hashlib.sha256()
+    for i in range(0, n, 1 << 26):
+        h.update(ref[i:i + (1 << 26)].cpu().numpy().view("<u4").tobytes())
+    assert h.hexdigest() == oracle_mod.sorted_pcg_sha256(n, first=0)
+    m = torch.tensor(np.uint32(mask).view(np.int32).item(), dtype=torch.int32, device=x.device)
+    xm = x & m
+    out = torch.empty_like(x)
+    tmp = torch.empty_like(x)
+
+    def timed(t):
+        dev.sort_keys_u32(t, out=out, tmp=tmp)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            dev.sort_keys_u32(t, out=out, tmp=tmp)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / 3
+
+    t_dup = timed(xm)
+    assert torch.equal(out, ref & m)
+    t_uni = timed(x)
+    assert t_dup < 3.0 * t_uni, (t_dup, t_uni)
+    del x, xm, ref, out, tmp
+    torch.cuda.empty_cache()

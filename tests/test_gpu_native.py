@@ -8,10 +8,14 @@ on the image's HIP 7.2 runtime, as C / C++ / cgo callers load it):
   plus gpuDistribSort callers mixed with single-device ones;
 - tests/cpp/test_parallel_asan: the same against build_asan/libsort.so,
   whose host code is compiled with AddressSanitizer (-Xarch_host; device
-  code untouched).  Listed in .gpurunignore since round 3 (with build_asan/),
-  so it does not travel to the GPU box and its case skips there; the host
-  arithmetic of the distributed engine still runs under ASan on the CPU
-  (tests/cpp/distrib_sim.cpp)."""
+  code untouched): the device pool's concurrent host code under ASan
+  against a real GPU (the reference's libsort_test.go:35-87 callers);
+- tests/cpp/test_rccl_native: the C engine over RCCL in a torch-free
+  process (the image's /opt/rocm RCCL, as C and Go callers load it), every
+  piece through RCCL, 2^27 + 12345 and 2^28 keys.
+
+A missing binary fails: __graft_entry__.build() makes all three and they
+travel to the GPU box (not in .gpurunignore)."""
 import os
 import pathlib
 import subprocess
@@ -22,11 +26,9 @@ pytestmark = pytest.mark.gpu
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 
 
-@pytest.mark.parametrize("exe", ["test_parallel", "test_parallel_asan"])
+@pytest.mark.parametrize("exe", ["test_parallel", "test_parallel_asan", "test_rccl_native"])
 def test_native_parallel_callers(exe):
     path = ROOT / "tests" / "cpp" / exe
-    if exe.endswith("_asan") and not path.exists():
-        pytest.skip("ASan build not shipped to this box (.gpurunignore)")
     assert path.exists(), "built by __graft_entry__.build() (make -C tests/cpp)"
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:verify_asan_link_order=0")
     r = subprocess.run([str(path)], capture_output=True, text=True, timeout=120, env=env)

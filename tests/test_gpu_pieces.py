@@ -141,3 +141,76 @@ def test_bad_tables_fail_loudly(D):
     assert "libsortSortPiecesU32" in pylibsort.last_error()
     out = D.sort_pieces_u32(t, [], [], [], 1, 24)  # nothing to sort
     assert out.numel() == 0
+
+
+def _digits_round(oracle_mod, n, R, a, b, seed):
+    """A round whose every key lies in the top digits [a, b), uniform below:
+    segments large enough for two or more digit passes."""
+    rng = np.random.default_rng(seed)
+    x = (oracle_mod.pcg(n, first=seed) & np.uint32(0x00FFFFFF)) | \
+        (rng.integers(a, b, n, dtype=np.uint64).astype(np.uint32) << np.uint32(24))
+    return _round(x, R, a, b, seed=seed)
+
+
+def _sort_timed(D, buf, off, ln, sg, nseg, b):
+    D.timing_enable(True)
+    D.timing_reset()
+    try:
+        got = _sort(D, buf, off, ln, sg, nseg, b)
+        return got, D.timing_query("rsvsample")[0], D.timing_query("bucketsort")[0]
+    finally:
+        D.timing_enable(False)
+
+
+@pytest.mark.parametrize("reserve", ["0", "1"])
+@pytest.mark.parametrize("nseg,n", [(1, (1 << 21) + 5), (5, (1 << 22) + 3), (8, (1 << 23) + 1), (31, (1 << 23) + 7),
+                                    (40, (1 << 23) + 9)])
+def test_reserved_depth0_pieces(D, oracle_mod, monkeypatch, reserve, nseg, n):
+    """The piece sort's reserved depth 0 (4-bit digits; the round sorts of the
+    multi-GPU schedule): no count pass, the depth-0 pass reserves each run in
+    a slice per (segment, digit, range) sized by 131072 samples per range,
+    taken by global key rank through the piece table.  Up to 4096 slices
+    (31 segments); 40 segments keep the count pass.  Exact; which depth 0
+    ran is read from the timing registry."""
+    import pylibsort
+    monkeypatch.setenv("LIBSORT_HYB_RESERVE", reserve)
+    prev = pylibsort.setDigitBits(4)
+    try:
+        buf, off, ln, sg = _digits_round(oracle_mod, n, 8, 100, 100 + nseg, seed=nseg)
+        got, nsample, nbs = _sort_timed(D, buf, off, ln, sg, nseg, 24)
+        np.testing.assert_array_equal(got, oracle_mod.sort_u32(buf))
+        assert nbs == 1
+        assert nsample == (1 if reserve == "1" and nseg * 16 * 8 <= 4096 else 0), nsample
+    finally:
+        pylibsort.setDigitBits(prev)
+
+
+def test_reserved_depth0_pieces_digit8(D, oracle_mod, monkeypatch):
+    """8-bit digits: 2 segments x 256 digits x 8 ranges = 4096 slices."""
+    import pylibsort
+    monkeypatch.setenv("LIBSORT_HYB_RESERVE", "1")
+    prev = pylibsort.setDigitBits(8)
+    try:
+        buf, off, ln, sg = _digits_round(oracle_mod, (1 << 23) + 3, 4, 7, 9, seed=2)
+        got, nsample, nbs = _sort_timed(D, buf, off, ln, sg, 2, 24)
+        np.testing.assert_array_equal(got, oracle_mod.sort_u32(buf))
+        assert nsample == 1 and nbs == 1
+    finally:
+        pylibsort.setDigitBits(prev)
+
+
+@pytest.mark.parametrize("reserve", ["short", "nomem"])
+def test_reserved_depth0_pieces_fallbacks(D, oracle_mod, monkeypatch, reserve):
+    """Slices at half their sampled capacity (a depth-0 tile finds its slice
+    full: the piece sort gathers and LSD-sorts from the untouched pieces), and
+    an allocation that fails (the count pass instead)."""
+    import pylibsort
+    monkeypatch.setenv("LIBSORT_HYB_RESERVE", reserve)
+    prev = pylibsort.setDigitBits(4)
+    try:
+        buf, off, ln, sg = _digits_round(oracle_mod, (1 << 23) + 1, 8, 40, 48, seed=9)
+        got, nsample, nbs = _sort_timed(D, buf, off, ln, sg, 8, 24)
+        np.testing.assert_array_equal(got, oracle_mod.sort_u32(buf))
+        assert (nsample, nbs) == ((1, 0) if reserve == "short" else (0, 1)), (nsample, nbs)
+    finally:
+        pylibsort.setDigitBits(prev)
