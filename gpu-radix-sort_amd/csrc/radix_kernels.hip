@@ -1567,108 +1567,181 @@ __device__ __forceinline__ uint32_t field3_sum(uint64_t w) {
   return (uint32_t)__popcll(w & B0) + 2u * (uint32_t)__popcll(w & (B0 << 1)) +
          4u * (uint32_t)__popcll(w & (B0 << 2));
 }
-template <int CAP>
-constexpr int cnt_lds_words() {  // u64 words: the cell words, or the fallback's u32 counters + keys
-  return (8 * kCntCells > 4 * (kCntCells + 1) + 4 * CAP ? 8 * kCntCells : 4 * (kCntCells + 1) + 4 * CAP + 7) / 8;
+// Counting modes (the host picks one per launch from lbits and the block):
+//   kCntSmall  lbits <= 12: one value per cell, u32 counters;
+//   kCnt3      13..16 bits: u64 cells of 16 3-bit residual counts + the key
+//              count (overflow at 8 equal keys);
+//   kCnt3F     the same, lbits == 16 known at compile time;
+//   kCnt2F     lbits == 16, buckets of <= ~5K keys (256-thread blocks): u32
+//              cells of 16 2-bit counts, the cell's key count their sum (two
+//              popcounts), the cell starts as u16 (24 KB instead of 32 KB of
+//              LDS, ~60 instead of ~93 VGPRs: six blocks per CU instead of
+//              five).  A 2-bit count overflows at 4 equal keys -- ~4% of the
+//              uniform 4096-key buckets of a 2^28 sort (~1/16 key per value)
+//              -- and such a bucket goes to the LSD steps (the list launch).
+constexpr int kCntSmall = 0, kCnt3 = 1, kCnt3F = 2, kCnt2F = 3;
+template <int CAP, int MODE>
+constexpr int cnt_lds_words() {  // u64 words: the cell words (and starts), or the keys placed over them
+  constexpr int cells = MODE == kCnt2F ? 4 * kCntCells + 2 * kCntCells : 8 * kCntCells;
+  return (cells > 4 * CAP ? cells : 4 * CAP + 7) / 8;
 }
-template <int BLOCK, int ITEMS>
-__device__ __forceinline__ bool bucket_count_place(const uint32_t (&k)[ITEMS], uint64_t* s_cw, uint32_t* s_wsum,
-                                                   uint32_t* s_flag, uint32_t* out, uint32_t start, uint32_t len,
-                                                   uint32_t lbits, uint32_t bias) {
+// Exclusive block scan whose wave sums live in `s` (any LDS words the
+// block's other waves are done with: the caller's barrier before, and the
+// barrier after, keep them from being overwritten while read).
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_exclusive_scan_in(uint32_t v, uint32_t* s) {
+  uint32_t total;
+  const uint32_t ex = block_exclusive_scan<BLOCK>(v, s, total);
+  __syncthreads();
+  return ex;
+}
+__device__ __forceinline__ uint32_t field2_sum(uint32_t w) {
+  return (uint32_t)__builtin_popcount(w & 0x55555555u) + 2u * (uint32_t)__builtin_popcount(w & 0xAAAAAAAAu);
+}
+// The counting placement works in exactly the cell words (32 KB: five blocks
+// of 256 threads per CU): the overflow flag is a spare bit of a cell word,
+// the block scan's wave sums borrow cell words once every wave holds its
+// cells in registers, and the keys are placed over the words.  Returns false
+// (nothing written) on a count overflow.
+template <int BLOCK, int ITEMS, int MODE, typename Op>
+__device__ __forceinline__ bool bucket_count_place(const uint32_t (&k)[ITEMS], uint64_t* s_cw, uint32_t* out,
+                                                   uint32_t start, uint32_t len, uint32_t lbits_in, uint32_t bias) {
   constexpr int PER = kCntCells / BLOCK;
   static_assert(PER >= 1 && kCntCells % BLOCK == 0, "cells per thread");
+  constexpr bool FIXED = MODE == kCnt3F || MODE == kCnt2F;
+  constexpr bool BIAS = !std::is_same<Op, RadixDigit>::value;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
   const uint32_t wbase = w * ITEMS * kWave;
-  const uint32_t rb = lbits > 12 ? lbits - 12 : 0u;
+  const uint32_t lbits = FIXED ? 16u : lbits_in;
+  const uint32_t rb = FIXED ? 4u : lbits > 12 ? lbits - 12 : 0u;
   const uint32_t lmask = (1u << lbits) - 1u, rmask = (1u << rb) - 1u;
   // cell c's counter at (c % PER) * BLOCK + c / PER: the PER cells a thread
   // scans are one LDS column, read and written without bank conflicts
   auto ci = [&](uint32_t c) -> uint32_t { return (c % PER) * BLOCK + c / PER; };
-  auto val = [&](uint32_t x) -> uint32_t { return (x - bias) & lmask; };
+  auto val = [&](uint32_t x) -> uint32_t { return (BIAS ? x - bias : x) & lmask; };
+  uint32_t* const s_keys = reinterpret_cast<uint32_t*>(s_cw);
+  auto valid = [&](int j) { return wbase + j * kWave + lane < len; };
+
   uint32_t rk[ITEMS];
-  if (rb > 0) {
+  if constexpr (MODE == kCnt2F) {
+    uint32_t* const s_w = s_keys;                                              // 4096 u32 cells
+    uint16_t* const s_st = reinterpret_cast<uint16_t*>(s_keys + kCntCells);  // 4096 u16 starts
 #pragma unroll
-    for (int q = 0; q < PER; ++q) s_cw[q * BLOCK + tid] = 0ull;
-    if (tid == 0) *s_flag = 0u;
+    for (int q = 0; q < PER; ++q) s_w[q * BLOCK + tid] = 0u;
+    if (tid == 0) s_st[0] = 0;  // (the overflow flag until the starts are written)
     __syncthreads();
     bool ovf = false;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j)
-      if (wbase + j * kWave + lane < len) {
+      if (valid(j)) {
+        const uint32_t v = val(k[j]), sh = 2u * (v & 15u);
+        rk[j] = (atomicAdd(&s_w[ci(v >> 4)], 1u << sh) >> sh) & 3u;
+        ovf |= rk[j] == 3u;
+      }
+    if (__any(ovf) && lane == 0) s_st[0] = 1;
+    __syncthreads();
+    if (s_st[0]) return false;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) sum += field2_sum(s_w[q * BLOCK + tid]);
+    __syncthreads();  // (every wave has read the flag before the starts overwrite it)
+    uint32_t run = block_exclusive_scan_in<BLOCK>(sum, reinterpret_cast<uint32_t*>(s_st));
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      s_st[q * BLOCK + tid] = (uint16_t)run;
+      run += field2_sum(s_w[q * BLOCK + tid]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (valid(j)) {
+        const uint32_t v = val(k[j]), c = ci(v >> 4);
+        rk[j] += (uint32_t)s_st[c] + field2_sum(s_w[c] & ((1u << (2u * (v & 15u))) - 1u));
+      }
+  } else if constexpr (MODE != kCntSmall) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) s_cw[q * BLOCK + tid] = 0ull;
+    __syncthreads();
+    bool ovf = false;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (valid(j)) {
         const uint32_t v = val(k[j]), sh = 3u * (v & rmask);
         const uint64_t old = atomicAdd((unsigned long long*)&s_cw[ci(v >> rb)], (1ull << sh) + (1ull << 48));
         rk[j] = (uint32_t)(old >> sh) & 7u;
         ovf |= rk[j] == 7u;
       }
-    if (__any(ovf) && lane == 0) *s_flag = 1u;
+    // the overflow flag is bit 63 of cell 0 (a count uses 13 of its 16 bits):
+    // no LDS beyond the cells (__syncthreads_or would take 256 bytes)
+    if (__any(ovf) && lane == 0) atomicOr((unsigned long long*)&s_cw[0], 1ull << 63);
     __syncthreads();
-    if (!*s_flag) {
-      uint64_t cw[PER];
-      uint32_t sum = 0;
+    if (s_cw[0] >> 63) return false;
+    uint64_t cw[PER];
+    uint32_t sum = 0;
 #pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        cw[q] = s_cw[q * BLOCK + tid];
-        sum += (uint32_t)(cw[q] >> 48);
-      }
-      uint32_t total;
-      uint32_t run = block_exclusive_scan<BLOCK>(sum, s_wsum, total);
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const uint32_t n = (uint32_t)(cw[q] >> 48);
-        s_cw[q * BLOCK + tid] = (cw[q] & 0xFFFFFFFFFFFFull) | ((uint64_t)run << 48);
-        run += n;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j)
-        if (wbase + j * kWave + lane < len) {
-          const uint32_t v = val(k[j]);
-          const uint64_t c = s_cw[ci(v >> rb)];
-          rk[j] += (uint32_t)(c >> 48) + field3_sum(c & ((1ull << (3u * (v & rmask))) - 1ull));
-        }
-      __syncthreads();  // the keys take the words' place
-      uint32_t* s_keys = reinterpret_cast<uint32_t*>(s_cw);
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j)
-        if (wbase + j * kWave + lane < len) s_keys[rk[j]] = k[j];
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < ITEMS; ++j) {
-        const uint32_t p = wbase + j * kWave + lane;
-        if (p < len) out[(size_t)start + p] = s_keys[p];
-      }
-      return true;
+    for (int q = 0; q < PER; ++q) {
+      cw[q] = s_cw[q * BLOCK + tid];
+      sum += (uint32_t)(cw[q] >> 48);
     }
-    __syncthreads();  // every wave has read the flag before the caller reuses the words
-    return false;
-  }
-  // lbits <= 12: one value per cell, u32 counters
-  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_cw);  // kCntCells + 1 u32 counters, then the keys
-  uint32_t* s_keys = s_cnt + kCntCells + 1;
+    // (256-thread blocks: the wave sums borrow cell words, so the block needs
+    // exactly 32 KB -- five per CU; larger blocks keep 64 B of their own: the
+    // aliasing made the 64-VGPR 1024-thread class spill to scratch)
+    uint32_t run;
+    if constexpr (BLOCK == 256) {
+      __syncthreads();
+      run = block_exclusive_scan_in<BLOCK>(sum, s_keys);
+    } else {
+      __shared__ uint32_t s_ws[BLOCK / kWave];
+      uint32_t total;
+      run = block_exclusive_scan<BLOCK>(sum, s_ws, total);
+    }
 #pragma unroll
-  for (int q = 0; q < PER; ++q) s_cnt[q * BLOCK + tid] = 0u;
-  __syncthreads();
+    for (int q = 0; q < PER; ++q) {
+      const uint32_t n = (uint32_t)(cw[q] >> 48);
+      s_cw[q * BLOCK + tid] = (cw[q] & 0xFFFFFFFFFFFFull) | ((uint64_t)run << 48);
+      run += n;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (valid(j)) {
+        const uint32_t v = val(k[j]);
+        const uint64_t c = s_cw[ci(v >> rb)];
+        rk[j] += (uint32_t)(c >> 48) + field3_sum(c & ((1ull << (3u * (v & rmask))) - 1ull));
+      }
+  } else {
+    // lbits <= 12: one value per cell, u32 counters (an atomic's return is
+    // the key's rank among its equals: no overflow)
+    uint32_t* const s_cnt = s_keys;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) s_cnt[q * BLOCK + tid] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (valid(j)) rk[j] = atomicAdd(&s_cnt[ci(val(k[j]))], 1u);
+    __syncthreads();
+    uint32_t c[PER], sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      c[q] = s_cnt[q * BLOCK + tid];
+      sum += c[q];
+    }
+    __syncthreads();
+    uint32_t run = block_exclusive_scan_in<BLOCK>(sum, s_cnt);
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      s_cnt[q * BLOCK + tid] = run;
+      run += c[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (valid(j)) rk[j] += s_cnt[ci(val(k[j]))];
+  }
+  __syncthreads();  // the keys take the words' place
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j)
-    if (wbase + j * kWave + lane < len) rk[j] = atomicAdd(&s_cnt[ci(val(k[j]))], 1u);
-  __syncthreads();
-  uint32_t c[PER], sum = 0;
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    c[q] = s_cnt[q * BLOCK + tid];
-    sum += c[q];
-  }
-  uint32_t total;
-  uint32_t run = block_exclusive_scan<BLOCK>(sum, s_wsum, total);
-#pragma unroll
-  for (int q = 0; q < PER; ++q) {
-    s_cnt[q * BLOCK + tid] = run;
-    run += c[q];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < ITEMS; ++j)
-    if (wbase + j * kWave + lane < len) s_keys[s_cnt[ci(val(k[j]))] + rk[j]] = k[j];
+    if (valid(j)) s_keys[rk[j]] = k[j];
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
@@ -1678,8 +1751,52 @@ __device__ __forceinline__ bool bucket_count_place(const uint32_t (&k)[ITEMS], u
   return true;
 }
 
+// The counting placement's own kernel (32-bit keys without values, lbits <=
+// 16; the host picks it): block b places bucket b with bucket_count_place in
+// exactly the cell words' LDS (32 KB: five 256-thread blocks per CU; the
+// 16K-key buckets of configs[2]: 68 KB and a 64-VGPR budget, two 1024-thread
+// blocks per CU).  A bucket larger than the block is listed for the next
+// size (as k_bucket_sort); one whose 3-bit counts overflowed (8+ equal keys)
+// is written nothing and listed in ovf_list (*ovf_n entries) for the LSD
+// steps of k_bucket_sort LIST, so this kernel holds no LSD-step code.
+template <int BLOCK, int ITEMS, typename Op, int MODE>
+__global__ __launch_bounds__(BLOCK)
+__attribute__((amdgpu_waves_per_eu(BLOCK >= 1024 && ITEMS <= 17 && MODE != kCntSmall ? 8 : 1, 8)))
+void k_bucket_count(const uint32_t* in, uint32_t* out, const uint32_t* __restrict__ bstart,
+                    const uint32_t* __restrict__ blen, const uint32_t* __restrict__ nb, uint32_t nb_cap,
+                    const uint32_t* __restrict__ ilist, uint32_t lbits, uint32_t bias,
+                    uint32_t* __restrict__ oversized, uint32_t* __restrict__ olist, uint32_t olist_cap,
+                    uint32_t* __restrict__ ovf_n, uint32_t* __restrict__ ovf_list) {
+  constexpr int CAP = BLOCK * ITEMS;
+  static_assert(CAP < 65536, "16-bit cell starts");
+  __shared__ uint64_t s_cw[cnt_lds_words<CAP, MODE>()];
+  if (blockIdx.x >= min(*nb, nb_cap)) return;
+  const uint32_t b = ilist ? ilist[blockIdx.x] : blockIdx.x;
+  const uint32_t start = bstart[b], len = blen[b];
+  if (len > (uint32_t)CAP) {
+    if (threadIdx.x == 0) {
+      const uint32_t slot = atomicAdd(oversized, 1u);
+      if (olist && slot < olist_cap) olist[slot] = b;
+    }
+    return;
+  }
+  if (len == 0) return;
+  const uint32_t wbase = (threadIdx.x / kWave) * ITEMS * kWave, lane = threadIdx.x & (kWave - 1);
+  uint32_t k[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t i = wbase + j * kWave + lane;
+    k[j] = i < len ? load_stream(&in[(size_t)start + i]) : 0u;
+  }
+  if (!bucket_count_place<BLOCK, ITEMS, MODE, Op>(k, s_cw, out, start, len, lbits, bias) && threadIdx.x == 0)
+    ovf_list[atomicAdd(ovf_n, 1u)] = b;  // (in == out keeps the bucket for the LSD steps)
+}
+
+// LIST: a persistent grid walks a list of buckets (ilist[0, min(*nb,
+// nb_cap))) -- the launch after the counting placement, over its overflow
+// list.
 template <int BITS, int BLOCK, int ITEMS, typename Op = RadixDigit, typename K = uint32_t, typename V = NoValue,
-          int FIX = 0, bool CNT = false>
+          int FIX = 0, bool LIST = false>
 __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, const V* vin, V* vout,
                                                        const uint32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ blen,
@@ -1697,7 +1814,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
   constexpr uint32_t kRunList = FIX > 0 ? 2 * kWave : 1;  // run starts listed per wave (FIX)
   static_assert(RADIX <= BLOCK && CAP < 65536, "one digit per thread; 16-bit wave counters");
   static_assert(FIX == 0 || (sizeof(K) == 8 && FIX % BITS == 0 && FIX <= 32), "tie fix-up: 64-bit keys");
-  __shared__ K s_keys[CNT ? 1 : CAP];
+  __shared__ K s_keys[CAP];
   __shared__ VS s_vals[HAS_V ? CAP : 1];
   __shared__ WaveCount s_whist[WAVES][RADIX];
   __shared__ WaveCount s_off[RADIX <= kWave ? WAVES : 1][RADIX];
@@ -1705,13 +1822,8 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
   __shared__ uint16_t s_runs[FIX > 0 ? WAVES : 1][kRunList];
   constexpr bool ATOMIC0 = LIBSORT_BUCKET_ATOMIC0 && !HAS_V && FIX == 0;
   __shared__ uint32_t s_acnt[ATOMIC0 ? WAVES : 1][ATOMIC0 ? RADIX : 1];
-  static_assert(!CNT || (sizeof(K) == 4 && !HAS_V && FIX == 0), "counting path: 32-bit keys only");
-  __shared__ uint64_t s_cw[CNT ? cnt_lds_words<CAP>() : 1];
-  __shared__ uint32_t s_flag;
-  // the LSD steps' key buffer (CNT: over the counting words, its fallback)
-  K* const sk = CNT ? reinterpret_cast<K*>(s_cw) : s_keys;
-  if (blockIdx.x >= min(*nb, nb_cap)) return;
-  const uint32_t b = ilist ? ilist[blockIdx.x] : blockIdx.x;
+  K* const sk = s_keys;
+  auto one = [&](const uint32_t b) {
   const uint32_t start = bstart[b], len = blen[b];
   if (len > (uint32_t)CAP) {
     if (threadIdx.x == 0) {
@@ -1822,11 +1934,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
     }
   };
   load();
-  if constexpr (CNT) {
-    // (a 3-bit count overflowed: the LSD steps below, over the same words)
-    if (bucket_count_place<BLOCK, ITEMS>(k, s_cw, s_wsum, &s_flag, out, start, len, lbits, bias)) return;
-    steps(0, lbits);
-  } else if constexpr (FIX > 0) {
+  if constexpr (FIX > 0) {
     const uint32_t fs = lbits > (uint32_t)FIX ? lbits - FIX : 0u;  // keys equal above fs form the runs
     steps(fs, lbits);
     if (fs > 0) {
@@ -1923,6 +2031,17 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
       out[(size_t)start + i] = k[j];
       if constexpr (HAS_V) vout[(size_t)start + i] = v[j];
     }
+  }
+  };  // one(b)
+  if constexpr (LIST) {
+    const uint32_t cnt = min(*nb, nb_cap);
+    for (uint32_t bi = blockIdx.x; bi < cnt; bi += gridDim.x) {
+      one(ilist[bi]);
+      __syncthreads();  // the LDS of one bucket before the next one's
+    }
+  } else {
+    if (blockIdx.x >= min(*nb, nb_cap)) return;
+    one(ilist ? ilist[blockIdx.x] : blockIdx.x);
   }
 }
 
@@ -3214,6 +3333,16 @@ inline int rsv_mode() {
   return s[0] == '0' ? 0 : s[0] == 's' ? 2 : s[0] == 'n' ? 3 : 1;
 }
 
+// The 2-bit counting cells for 256-thread bucket blocks (kCnt2F);
+// LIBSORT_BUCKET2=0 keeps the 3-bit cells (A/B).
+inline bool bucket2_on() {
+  static const bool on = [] {
+    const char* s = getenv("LIBSORT_BUCKET2");
+    return !(s && s[0] == '0');
+  }();
+  return on;
+}
+
 inline bool dstream_on() {
   static const bool on = [] {
     const char* s = getenv("LIBSORT_DSTREAM");
@@ -3658,7 +3787,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   // hybrid block: tiles[2] | segbase | cstart[2] | nsize | ctile0[2] | ntl | counters
   const size_t w_tiles = (size_t)TB * 4;
   const size_t rsv_words = (size_t)kRsvRanges * kRsvBlocks * rnc + 3 * (size_t)rns + 16;
-  const size_t words = 2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16 + kListCap + rsv_words;
+  const size_t words = 2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16 + kListCap + NB + rsv_words;
   LS_TRY(ws.ensure_hybrid(words));
   uint32_t* h = ws.hyb;
   uint4* tiles[2] = {reinterpret_cast<uint4*>(h), reinterpret_cast<uint4*>(h + w_tiles)};
@@ -3670,10 +3799,13 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   uint32_t* ntl = h; h += NB;
   uint32_t* ctr = h;  // [k] tiles of depth k, [8] buckets over the first block, [9] bucket count, [10] over the
                       // second, [11] largest bucket, [12] buckets over the first block (planning),
-                      // [13] largest child of depth 0 (pieces), [14] scratch
+                      // [13] largest child of depth 0 (pieces), [14] reserved depth 0 overflow,
+                      // [15] buckets whose counting placement overflowed
   h += 16;
   uint32_t* olist = h;  // the buckets over the first block (kListCap)
   h += kListCap;
+  uint32_t* flist = h;  // the buckets whose counting placement overflowed (ctr[15] of NB)
+  h += NB;
   // reserved depth 0: sample partials | slices (start | capacity | first tile,
   // + the tile count) | cursors | estimated digit sizes; ctr[14] = overflow
   uint32_t* rpart = h; h += (size_t)kRsvRanges * kRsvBlocks * rnc;
@@ -3894,29 +4026,55 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     // (k_bucket_sort CNT, `cnt` above)
     auto launch = [&](auto cnt_c) -> hipError_t {
       constexpr bool C = decltype(cnt_c)::value;
-#define LS_BS(I, G, NBP, CAPN, IL, OV, OL)                                                                     \
-  hipLaunchKernelGGL((k_bucket_sort<BITS, BB, ((I) * 256 + BB - 1) / BB, Op, K, V, FIXB, C>), dim3(G), dim3(BB), 0, st, \
-                     out, out, vout, vout, bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
+#define LS_BSX(B, I, G, NBP, CAPN, IL, OV, OL)                                                                   \
+  if constexpr (C) {                                                                                             \
+    const uint32_t* ci_ = reinterpret_cast<const uint32_t*>(out);                                                \
+    uint32_t* co_ = reinterpret_cast<uint32_t*>(out);                                                            \
+    if (lbits <= 12)                                                                                             \
+      hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCntSmall>), dim3(G), dim3(B), 0, st, ci_, co_, bstart,     \
+                         nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, ctr + 15, flist);                  \
+    else if (lbits != 16)                                                                                        \
+      hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt3>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize,  \
+                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, ctr + 15, flist);                         \
+    else if (B == 256 && bucket2_on())                                                                           \
+      hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt2F>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize, \
+                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, ctr + 15, flist);                         \
+    else                                                                                                         \
+      hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt3F>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize, \
+                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, ctr + 15, flist);                         \
+  } else {                                                                                                       \
+    hipLaunchKernelGGL((k_bucket_sort<BITS, B, (I), Op, K, V, FIXB>), dim3(G), dim3(B), 0, st, out, out, vout, vout, \
+                       bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap);                             \
+  }
+#define LS_BS(I, G, NBP, CAPN, IL, OV, OL) LS_BSX(BB, ((I) * 256 + BB - 1) / BB, G, NBP, CAPN, IL, OV, OL)
 #define LS_BS2(I)                                          \
   LS_BS(I, NB, ctr + 9, NB, nullptr, ctr + 8, olist);      \
   LS_TRY(hipGetLastError());                               \
   LS_BS(I + 6, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr)
-#define LS_BS512(I, G, NBP, CAPN, IL, OV, OL)                                                                    \
-  hipLaunchKernelGGL((k_bucket_sort<BITS, 512, (I), Op, K, V, FIXB, C>), dim3(G), dim3(512), 0, st, out, out, vout, \
-                     vout, bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
-#define LS_BS1024(I, G, NBP, CAPN, IL, OV, OL)                                                                  \
-  hipLaunchKernelGGL((k_bucket_sort<BITS, 1024, (I), Op, K, V, FIXB, C>), dim3(G), dim3(1024), 0, st, out, out, vout, \
-                     vout, bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap)
+#define LS_BS512(I, G, NBP, CAPN, IL, OV, OL) LS_BSX(512, I, G, NBP, CAPN, IL, OV, OL)
+#define LS_BS1024(I, G, NBP, CAPN, IL, OV, OL) LS_BSX(1024, I, G, NBP, CAPN, IL, OV, OL)
+      // the buckets the counting placement listed (3-bit overflow: 8+ equal
+      // keys), by the LSD steps in blocks of the second size: a persistent
+      // grid over the list (none listed: the blocks read the count and exit)
+#define LS_BSL(B, I)                                                                                               \
+  if constexpr (C) {                                                                                               \
+    hipLaunchKernelGGL((k_bucket_sort<BITS, B, (I), Op, K, V, 0, true>),                                           \
+                       dim3(std::min<uint32_t>(NB, (uint32_t)std::max(1, ws.num_cus) * 2)), dim3(B), 0, st, out,   \
+                       out, vout, vout, bstart, nsize, ctr + 15, NB, flist, lbits, bias, ctr + 14, nullptr, 0u);    \
+    LS_TRY(hipGetLastError());                                                                                     \
+  }
       switch (cls) {
-        case 0: LS_BS2(9); break;
-        case 1: LS_BS2(13); break;
-        case 2: LS_BS2(17); break;
-        case 3: LS_BS2(19); break;
+        case 0: LS_BS2(9); LS_TRY(hipGetLastError()); LS_BSL(BB, (15 * 256 + BB - 1) / BB); break;
+        case 1: LS_BS2(13); LS_TRY(hipGetLastError()); LS_BSL(BB, (19 * 256 + BB - 1) / BB); break;
+        case 2: LS_BS2(17); LS_TRY(hipGetLastError()); LS_BSL(BB, (23 * 256 + BB - 1) / BB); break;
+        case 3: LS_BS2(19); LS_TRY(hipGetLastError()); LS_BSL(BB, (25 * 256 + BB - 1) / BB); break;
         case 4:
           if constexpr (sizeof(K) == 4) {
             LS_BS512(17, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
             LS_TRY(hipGetLastError());
             LS_BS512(23, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+            LS_TRY(hipGetLastError());
+            LS_BSL(512, 23);
           }
           break;
         default:
@@ -3924,6 +4082,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
             LS_BS1024(17, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
             LS_TRY(hipGetLastError());
             LS_BS1024(23, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+            LS_TRY(hipGetLastError());
+            LS_BSL(1024, 23);
           }
           break;
       }
@@ -3937,6 +4097,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     } else {
       LS_TRY(launch(std::false_type{}));
     }
+#undef LS_BSL
+#undef LS_BSX
 #undef LS_BS1024
 #undef LS_BS512
 #undef LS_BS2

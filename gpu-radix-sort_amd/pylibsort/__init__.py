@@ -146,8 +146,15 @@ def _setup():
                            "or put libsort.so on LD_LIBRARY_PATH / $LIBSORT_PATH")
     s.path = path
     s.sortLib = ctypes.cdll.LoadLibrary(path)
+    # (LIBSORT_AB_MISSING_OK=1: an older build in an A/B run may lack newer
+    # entry points; they then stay unbound)
+    missing_ok = os.environ.get("LIBSORT_AB_MISSING_OK") == "1"
     for name, res, args in _SIGS:
-        fn = getattr(s.sortLib, name)
+        fn = getattr(s.sortLib, name, None)
+        if fn is None:
+            if missing_ok:
+                continue
+            raise AttributeError("%s lacks %s" % (path, name))
         fn.restype = res
         fn.argtypes = args
     # Must be called exactly once per process (reference __init__.py:19-20).

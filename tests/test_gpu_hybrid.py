@@ -621,15 +621,16 @@ def test_reserved_depth0_nomem_falls_back(dev, oracle_mod, digit4, force, monkey
     assert nbs == 1
 
 
-@pytest.mark.parametrize("mask", [0xFFFF0000, 0xFFFF0003], ids=["low16_const", "low16_four"])
-def test_counting_bucket_duplicates_full_size(dev, oracle_mod, bits, mask):
+@pytest.mark.parametrize("four", [False, True], ids=["low16_const", "low16_four"])
+def test_counting_bucket_duplicates_full_size(dev, oracle_mod, bits, four):
     """Duplicate-heavy keys at the bench size (2^28, auto mode): every 16-bit
     bucket holds ~4096 keys of one (or four) values, so the counting
-    placement's 3-bit counts overflow in every bucket and the block sorts it
-    by the LSD steps instead (no per-cell search, whose cost grew
-    with the square of the cell).  Exact: masking the low bits is monotone, so
-    sort(x & m) == sort(x) & m, and sort(x) is pinned by the oracle's hash.
-    Timed against the uniform sort: within 3x (the quadratic search was ~100x)."""
+    placement's counts overflow in every bucket and the bucket is sorted by
+    the LSD steps instead (no per-cell search, whose cost grew
+    with the square of the cell).  Exact: f(x) = high 16 bits of x, plus (four)
+    its bits 14-15 as the low bits, is monotone, so sort(f(x)) == f(sort(x)),
+    and sort(x) is pinned by the oracle's hash.  Timed against the uniform
+    sort: within 3x (the quadratic search was ~100x)."""
     import hashlib
     import time
     n = 1 << 28
@@ -640,8 +641,10 @@ def test_counting_bucket_duplicates_full_size(dev, oracle_mod, bits, mask):
     for i in range(0, n, 1 << 26):
         h.update(ref[i:i + (1 << 26)].cpu().numpy().view("<u4").tobytes())
     assert h.hexdigest() == oracle_mod.sorted_pcg_sha256(n, first=0)
-    m = torch.tensor(np.uint32(mask).view(np.int32).item(), dtype=torch.int32, device=x.device)
-    xm = x & m
+    def f(t):
+        y = t & -65536  # the high 16 bits
+        return (y | ((t & 0xC000) >> 14)) if four else y
+    xm = f(x)
     out = torch.empty_like(x)
     tmp = torch.empty_like(x)
 
@@ -655,7 +658,7 @@ def test_counting_bucket_duplicates_full_size(dev, oracle_mod, bits, mask):
         return (time.perf_counter() - t0) / 3
 
     t_dup = timed(xm)
-    assert torch.equal(out, ref & m)
+    assert torch.equal(out, f(ref))
     t_uni = timed(x)
     assert t_dup < 3.0 * t_uni, (t_dup, t_uni)
     del x, xm, ref, out, tmp

@@ -658,7 +658,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
     const uint32_t i = wbase + j * kWave + lane;
     k[j] = i < len ? load_stream(&in[(size_t)start + i]) : 0xffffffffu;
   }
-  bucket_count_place<BLOCK, ITEMS>(k, s_cw, s_wsum, &s_flag, out, start, len, lbits, 0u);
+  bucket_count_place<BLOCK, ITEMS>(k, s_cw, out, start, len, lbits, 0u);
 }
 
 // ---- abl: cntF's phases cut at STAGE (0 copy with the same LDS, 1 + atomics,

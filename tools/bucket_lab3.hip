@@ -207,9 +207,10 @@ int main(int argc, char** argv) {
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const size_t NMAX = (size_t)1 << 30;
-  uint32_t *in, *out, *bs, *bl, *nb, *ov;
+  uint32_t *in, *out, *bs, *bl, *nb, *ov, *ovn, *ovl;
   CK(hipMalloc(&in, NMAX * 4)); CK(hipMalloc(&out, NMAX * 4));
   CK(hipMalloc(&bs, (NMAX / 1024 + 1) * 4)); CK(hipMalloc(&bl, (NMAX / 1024 + 1) * 4)); CK(hipMalloc(&nb, 4)); CK(hipMalloc(&ov, 4));
+  CK(hipMalloc(&ovn, 4)); CK(hipMalloc(&ovl, (NMAX / 1024 + 1) * 4));
   hipStream_t st; CK(hipStreamCreate(&st));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   struct V { std::string name; int lg; uint32_t S; std::function<void(uint32_t)> launch; };
@@ -218,8 +219,9 @@ int main(int argc, char** argv) {
   vs.push_back({"c3 copy 1024x17", 30, 16384, [&](uint32_t m) {
     hipLaunchKernelGGL((k_copy<1024, 17>), dim3(m), dim3(1024), 0, st, in, out, bs, bl, nb); }});
   vs.push_back({"c3 prod 1024x17", 30, 16384, [&](uint32_t m) {
-    hipLaunchKernelGGL((k_bucket_sort<8, 1024, 17, RadixDigit, uint32_t, NoValue, 0, true>), dim3(m), dim3(1024), 0, st, in,
-                       out, (const NoValue*)nullptr, (NoValue*)nullptr, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u); }});
+    CK(hipMemsetAsync(ovn, 0, 4, st));
+    hipLaunchKernelGGL((k_bucket_count<1024, 17, RadixDigit, kCnt3F>), dim3(m), dim3(1024), 0, st, in, out, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u, ovn, ovl);
+    hipLaunchKernelGGL((k_bucket_sort<8, 1024, 17, RadixDigit, uint32_t, NoValue, 0, true>), dim3(512), dim3(1024), 0, st, in, out, (const NoValue*)nullptr, (NoValue*)nullptr, bs, bl, ovn, m, ovl, 16u, 0u, ov, nullptr, 0u); }});
   vs.push_back({"c3 one 1024x17", 30, 16384, [&](uint32_t m) {
     hipLaunchKernelGGL((k_one<1024, 17>), dim3(m), dim3(1024), 0, st, in, out, bs, bl, nb); }});
   vs.push_back({"c3 one 512x34", 30, 16384, [&](uint32_t m) {
@@ -234,8 +236,9 @@ int main(int argc, char** argv) {
   vs.push_back({"c2 copy 256x17", 28, 4096, [&](uint32_t m) {
     hipLaunchKernelGGL((k_copy<256, 17>), dim3(m), dim3(256), 0, st, in, out, bs, bl, nb); }});
   vs.push_back({"c2 prod 256x17", 28, 4096, [&](uint32_t m) {
-    hipLaunchKernelGGL((k_bucket_sort<4, 256, 17, RadixDigit, uint32_t, NoValue, 0, true>), dim3(m), dim3(256), 0, st, in,
-                       out, (const NoValue*)nullptr, (NoValue*)nullptr, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u); }});
+    CK(hipMemsetAsync(ovn, 0, 4, st));
+    hipLaunchKernelGGL((k_bucket_count<256, 17, RadixDigit, kCnt2F>), dim3(m), dim3(256), 0, st, in, out, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u, ovn, ovl);
+    hipLaunchKernelGGL((k_bucket_sort<4, 256, 17, RadixDigit, uint32_t, NoValue, 0, true>), dim3(512), dim3(256), 0, st, in, out, (const NoValue*)nullptr, (NoValue*)nullptr, bs, bl, ovn, m, ovl, 16u, 0u, ov, nullptr, 0u); }});
   vs.push_back({"c2 one 256x17", 28, 4096, [&](uint32_t m) {
     hipLaunchKernelGGL((k_one<256, 17>), dim3(m), dim3(256), 0, st, in, out, bs, bl, nb); }});
   for (int g : {2, 3, 4}) {
