@@ -1624,11 +1624,14 @@ __device__ __forceinline__ bool bucket_count_place(const uint32_t (&k)[ITEMS], u
 
   uint32_t rk[ITEMS];
   if constexpr (MODE == kCnt2F) {
+    // (24 KB of cells and starts: six blocks per CU with room for the flag
+    // and the wave sums of their own)
     uint32_t* const s_w = s_keys;                                              // 4096 u32 cells
     uint16_t* const s_st = reinterpret_cast<uint16_t*>(s_keys + kCntCells);  // 4096 u16 starts
+    __shared__ uint32_t s_ws2[BLOCK / kWave + 1];                            // wave sums | overflow flag
 #pragma unroll
     for (int q = 0; q < PER; ++q) s_w[q * BLOCK + tid] = 0u;
-    if (tid == 0) s_st[0] = 0;  // (the overflow flag until the starts are written)
+    if (tid == 0) s_ws2[BLOCK / kWave] = 0u;
     __syncthreads();
     bool ovf = false;
 #pragma unroll
@@ -1638,18 +1641,21 @@ __device__ __forceinline__ bool bucket_count_place(const uint32_t (&k)[ITEMS], u
         rk[j] = (atomicAdd(&s_w[ci(v >> 4)], 1u << sh) >> sh) & 3u;
         ovf |= rk[j] == 3u;
       }
-    if (__any(ovf) && lane == 0) s_st[0] = 1;
+    if (__any(ovf) && lane == 0) s_ws2[BLOCK / kWave] = 1u;
     __syncthreads();
-    if (s_st[0]) return false;
-    uint32_t sum = 0;
+    if (s_ws2[BLOCK / kWave]) return false;
+    uint32_t cnt[PER], sum = 0;
 #pragma unroll
-    for (int q = 0; q < PER; ++q) sum += field2_sum(s_w[q * BLOCK + tid]);
-    __syncthreads();  // (every wave has read the flag before the starts overwrite it)
-    uint32_t run = block_exclusive_scan_in<BLOCK>(sum, reinterpret_cast<uint32_t*>(s_st));
+    for (int q = 0; q < PER; ++q) {
+      cnt[q] = field2_sum(s_w[q * BLOCK + tid]);
+      sum += cnt[q];
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan<BLOCK>(sum, s_ws2, total);
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       s_st[q * BLOCK + tid] = (uint16_t)run;
-      run += field2_sum(s_w[q * BLOCK + tid]);
+      run += cnt[q];
     }
     __syncthreads();
 #pragma unroll

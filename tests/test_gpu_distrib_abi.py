@@ -120,8 +120,9 @@ def test_range_digit_rounds(D, oracle_mod, R, case):
     digit): the top-digit plan is too skewed, so the rounds re-partition by
     the 8-bit digit of key - min over the populated range instead of falling
     back to the 4-exchange LSD rounds (ADVICE r03).  Exact against the oracle;
-    the LSD rounds did not run (no "lsdround" launches) and the min/max
-    kernel ran once per rank."""
+    the LSD rounds did not run (no "lsdround" launches); at 8 ranks (and for
+    the one-digit input at any R) the min/max kernel ran once per rank (at 3
+    ranks, 2-4 populated top digits can still give a balanced plan)."""
     rng = np.random.default_rng(R)
     n = (1 << 21) + 77
     if case == "below2pow26":
@@ -132,7 +133,9 @@ def test_range_digit_rounds(D, oracle_mod, R, case):
         x = (rng.integers(0, 40, n, dtype=np.uint64) * 3 + 0x7F000000).astype(np.uint32)
     outs, (nlsd, nmm) = _timed_names(D, lambda: _run(D, x, R, COPY), "lsdround", "minmax")
     _check(oracle_mod, x, outs, R, False)
-    assert nlsd == 0 and nmm == R, (nlsd, nmm)
+    assert nlsd == 0 and nmm in (0, R), (nlsd, nmm)
+    if R == 8 or case == "one_digit_dups":
+        assert nmm == R, nmm
 
 
 def test_range_digit_all_equal_takes_lsd(D, oracle_mod):
@@ -197,6 +200,7 @@ def test_shape8_2pow29(D):
     n = 1 << 29
     x = D.populate_u32(n)
     x >>= 3
+    x &= 0x1FFFFFFF  # (a logical shift: the tensor is int32)
     out = D.distrib_sort_u32([x], SELF_RCCL)[0]
     del x
     h = hashlib.sha256()

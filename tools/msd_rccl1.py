@@ -26,14 +26,20 @@ def main():
     ops = distrib.HipOps()
     n = 1 << int(os.environ.get("MSD_LG", "28"))  # keys per rank (29: configs[3]'s share)
     keys = D.populate_u32(n)
-    if os.environ.get("MSD_SHAPE8") == "1":
+    if os.environ.get("MSD_SHAPE8") == "arith":  # rounds 1-3's variant (see below), for comparison
+        keys >>= 3
+    elif os.environ.get("MSD_SHAPE8") == "1":
         # the per-rank shape of an 8-GPU run on one rank: keep the top 5 bits
         # at 0, so the 2^29 keys fall in 32 top digits -- the 1/8 of the key
         # space one of 8 ranks receives; the rounds then hold ~8 digits of
         # ~2^24 keys each, as on every rank of configs[3] (the local
         # partition, which sees all 256 digits at 8 GPUs, is measured on the
         # uniform keys)
+        # (a LOGICAL shift: the tensor is int32, and an arithmetic one put
+        # the keys >= 2^31 in 16 top digits 0xF0-0xFF -- rounds 1-3's
+        # "shape8" was that 48-digit variant)
         keys >>= 3
+        keys &= 0x1FFFFFFF
     out = torch.empty_like(keys)
     tmp = torch.empty_like(keys)
 
