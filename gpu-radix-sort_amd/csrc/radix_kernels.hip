@@ -2323,12 +2323,17 @@ __global__ __launch_bounds__(256) void k_rsv_sample(const uint32_t* __restrict__
 // table), i.e. the keys of global rank [kb(t0), kb(t1)) in piece order; a
 // sample's rank is mapped to its piece by binary search over the pieces'
 // cumulative key counts pcum[np + 1], and it counts for (its piece's
-// segment, its digit).  131072 samples per range (several children per
-// range); otherwise as k_rsv_sample.  est[0] = the largest child's estimated
+// segment, its digit).  PER samples per thread (rsv_pc_per: several
+// children per range); otherwise as k_rsv_sample.  est[0] = the largest child's estimated
 // size (the host's skew check).
 constexpr uint32_t kRsvMaxSlices = 4096;
-constexpr int kRsvPcPer = 16;  // samples per thread (131072 per range)
-template <int RADIX, int TILE, typename Op>
+// samples per thread: 4, 8 or 16 (32768, 65536 or 131072 per range), the
+// fewest giving >= 256 per slice.  The samples are random gathers (~70 us per
+// 2^20 of them on MI355X), so they are sized to the slices, not fixed: the
+// capacity slack at 256 per slice is ~41% of the keys (memory, not passes).
+inline int rsv_pc_per(uint32_t nc) { return nc <= 128 ? 4 : nc <= 256 ? 8 : 16; }
+constexpr uint32_t kRsvLdsCum = 2048;
+template <int RADIX, int TILE, int PER, typename Op>
 __global__ __launch_bounds__(256) void k_rsv_sample_pc(const uint32_t* __restrict__ keys, const uint4* __restrict__ pieces,
                                                        const uint32_t* __restrict__ pcum, uint32_t np, uint32_t nseg,
                                                        uint32_t T0, uint32_t n, Op op, uint32_t* part,
@@ -2336,72 +2341,117 @@ __global__ __launch_bounds__(256) void k_rsv_sample_pc(const uint32_t* __restric
                                                        uint32_t* __restrict__ est, uint32_t* __restrict__ Czero,
                                                        uint32_t zero_words, uint32_t* ticket,
                                                        uint32_t* __restrict__ ctr, uint32_t nb, bool short_caps) {
-  constexpr uint32_t S = kRsvBlocks * 256 * kRsvPcPer;
+  constexpr uint32_t S = kRsvBlocks * 256 * PER;
   constexpr uint32_t kMaxChildren = kRsvMaxSlices / kRsvRanges;
   __shared__ uint32_t s_h[kMaxChildren];
   __shared__ uint32_t s_wsum[2][4];
   __shared__ uint32_t s_flag, s_max;
+  __shared__ uint64_t s_kb[kRsvRanges + 1];
+  __shared__ uint32_t s_cum[kRsvLdsCum], s_off[kRsvLdsCum], s_w[kRsvLdsCum];
+  __shared__ uint16_t s_seg[kRsvLdsCum];
   const uint32_t tid = threadIdx.x, NC = nseg * RADIX, NS = NC * kRsvRanges;
   const uint32_t x = blockIdx.x / kRsvBlocks, j = blockIdx.x % kRsvBlocks;
   for (uint32_t i = (blockIdx.x * 256 + tid) * 4; i < zero_words; i += gridDim.x * 256 * 4)
     *reinterpret_cast<uint4*>(&Czero[i]) = make_uint4(0u, 0u, 0u, 0u);
   for (uint32_t c = tid; c < NC; c += 256) s_h[c] = 0u;
+  // the cumulative counts, and the pieces' first tiles, key offsets and
+  // segments, are read from LDS when they fit (a round's np = sources *
+  // segments, 512 at 8 GPUs): the searches below are chains of dependent
+  // loads, ~1 us each from HBM
+  const bool lds = np < kRsvLdsCum;
+  if (lds)
+    for (uint32_t i = tid; i <= np; i += 256) {
+      const uint32_t c = pcum[i];
+      s_cum[i] = c;
+      if (i < np) {
+        const uint4 pc = pieces[i];
+        s_w[i] = pc.w;
+        s_off[i] = pc.x - c;  // (mod 2^32: key index = rank + s_off)
+        s_seg[i] = pc.z;
+      }
+    }
+  const uint32_t* cum = lds ? s_cum : pcum;
   __syncthreads();
   // keys before depth-0 tile t (the tiles of piece p are full but its last)
   auto kb = [&](uint32_t t) -> uint64_t {
     if (t >= T0) return n;
+    auto w = [&](uint32_t p) { return lds ? s_w[p] : pieces[p].w; };
     uint32_t lo = 0, hi = np;
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (pieces[mid].w <= t) lo = mid; else hi = mid;
+      if (w(mid) <= t) lo = mid; else hi = mid;
     }
-    return (uint64_t)pcum[lo] + (uint64_t)(t - pieces[lo].w) * TILE;
+    return (uint64_t)cum[lo] + (uint64_t)(t - w(lo)) * TILE;
   };
+  // range xr = the keys [s_kb[xr], s_kb[xr + 1]): the 9 bounds are searched
+  // once, by 9 threads, not per use
   const uint32_t q8 = T0 >> 3, r8 = T0 & 7u;
-  auto range_keys = [&](uint32_t xr, uint64_t* k0, uint64_t* k1) {
-    const uint32_t t0 = xr * q8 + min(xr, r8), t1 = t0 + q8 + (xr < r8 ? 1u : 0u);
-    *k0 = kb(t0);
-    *k1 = kb(t1);
-  };
-  uint64_t k0, k1;
-  range_keys(x, &k0, &k1);
-  const uint64_t N = k1 - k0;
-  uint32_t kv[kRsvPcPer], sg[kRsvPcPer];
-  bool ok[kRsvPcPer];
+  if (tid <= (uint32_t)kRsvRanges) s_kb[tid] = kb(tid * q8 + min(tid, r8));
+  __syncthreads();
+  const uint64_t k0 = s_kb[x], N = s_kb[x + 1] - k0;
+  // three phases over the thread's samples so that each phase's loads are
+  // all in flight together: ranks + piece searches (LDS, lock-step levels),
+  // the pieces (LDS, or global past kRsvLdsCum), then the keys
+  uint64_t rank[PER];
+  uint32_t lo[PER], kv[PER], sg[PER];
+  bool ok[PER];
 #pragma unroll
-  for (int q = 0; q < kRsvPcPer; ++q) {
-    const uint32_t i = (j * 256 + tid) * kRsvPcPer + q;
-    uint64_t rank;
+  for (int q = 0; q < PER; ++q) {
+    const uint32_t i = (j * 256 + tid) * PER + q;
     if (N <= S) {
-      rank = k0 + i;
+      rank[q] = k0 + i;
       ok[q] = i < N;
     } else {
       uint32_t h = (i + 1u) * 0x9E3779B1u ^ (x + 1u) * 0x85EBCA77u;
       h ^= h >> 15;
       h *= 0x2C1B3C6Du;
       h ^= h >> 12;
-      rank = k0 + ((uint64_t)i * N + (((uint64_t)h * N) >> 32)) / S;
+      rank[q] = k0 + ((uint64_t)i * N + (((uint64_t)h * N) >> 32)) / S;
       ok[q] = true;
     }
-    sg[q] = 0u;
-    kv[q] = 0u;
-    if (ok[q]) {
-      uint32_t lo = 0, hi = np;  // the piece holding global rank `rank`
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pcum[mid] <= rank) lo = mid; else hi = mid;
-      }
-      const uint4 pc = pieces[lo];
+    lo[q] = 0u;
+  }
+  // lo = the last piece with cum[lo] <= rank (the piece holding that rank)
+  for (uint32_t step = np > 1 ? 1u << (31 - __builtin_clz(np - 1)) : 0u; step; step >>= 1) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const uint32_t m = lo[q] + step;
+      if (m < np && cum[m] <= rank[q]) lo[q] = m;
+    }
+  }
+  uint32_t off[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (lds) {
+      off[q] = s_off[lo[q]];
+      sg[q] = s_seg[lo[q]];
+    } else {
+      const uint4 pc = pieces[lo[q]];
+      off[q] = pc.x - cum[lo[q]];
       sg[q] = pc.z;
-      kv[q] = keys[pc.x + (uint32_t)(rank - pcum[lo])];
     }
   }
 #pragma unroll
-  for (int q = 0; q < kRsvPcPer; ++q)
+  for (int q = 0; q < PER; ++q) kv[q] = ok[q] ? keys[(uint32_t)rank[q] + off[q]] : 0u;
+#pragma unroll
+  for (int q = 0; q < PER; ++q)
     if (ok[q]) atomicAdd(&s_h[sg[q] * RADIX + op(kv[q])], 1u);
   __syncthreads();
   for (uint32_t c = tid; c < NC; c += 256) st_agent(&part[(size_t)blockIdx.x * NC + c], s_h[c]);
-  if (!last_arriver(ticket, gridDim.x, &s_flag)) return;
+  // two levels: range x's last block sums its range's kRsvBlocks rows into
+  // the range's first row (ticket[1 + x]), the last of those finishes
+  // (ticket[0]); a thread per child, all its loads in flight together
+  if (!last_arriver(ticket + 1 + x, kRsvBlocks, &s_flag)) return;
+  for (uint32_t c = tid; c < NC; c += 256) {
+    uint32_t v[kRsvBlocks], sc = 0;
+#pragma unroll
+    for (int b = 0; b < kRsvBlocks; ++b) v[b] = ld_agent(&part[(size_t)(x * kRsvBlocks + b) * NC + c]);
+#pragma unroll
+    for (int b = 0; b < kRsvBlocks; ++b) sc += v[b];
+    st_agent(&part[(size_t)x * kRsvBlocks * NC + c], sc);
+  }
+  if (tid == 0) ticket[1 + x] = 0u;
+  if (!last_arriver(ticket, kRsvRanges, &s_flag)) return;
   // thread tid: children [tid * CPT, ...), their 8 range slices each
   // (contiguous slices e = c * 8 + range)
   const uint32_t CPT = (NC + 255) / 256;
@@ -2411,12 +2461,13 @@ __global__ __launch_bounds__(256) void k_rsv_sample_pc(const uint32_t* __restric
     const uint32_t c = tid * CPT + cc;
     if (c >= NC) break;
     double est_c = 0.0;
+    uint32_t scx[kRsvRanges];
+#pragma unroll
+    for (int xr = 0; xr < kRsvRanges; ++xr) scx[xr] = ld_agent(&part[(size_t)xr * kRsvBlocks * NC + c]);
+#pragma unroll
     for (uint32_t xr = 0; xr < (uint32_t)kRsvRanges; ++xr) {
-      uint32_t sc = 0;
-      for (int b = 0; b < kRsvBlocks; ++b) sc += ld_agent(&part[(size_t)(xr * kRsvBlocks + b) * NC + c]);
-      uint64_t a0, a1;
-      range_keys(xr, &a0, &a1);
-      const uint64_t Nx = a1 - a0;
+      const uint32_t sc = scx[xr];
+      const uint64_t Nx = s_kb[xr + 1] - s_kb[xr];
       uint32_t cap;
       if (Nx <= S) {
         cap = sc;
@@ -3769,7 +3820,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   int rmode = kRsvOk && DEPTHS > 1 && (const void*)in != (const void*)out && (!pc || (pc->cum && rns <= kRsvMaxSlices))
                   ? rsv_mode()
                   : 0;
-  const size_t rbound = pc ? rsv_capacity_bound_nc(n, rnc, kRsvBlocks * 256 * kRsvPcPer, TILE)
+  const int rper = rsv_pc_per(rnc);
+  const size_t rbound = pc ? rsv_capacity_bound_nc(n, rnc, kRsvBlocks * 256 * rper, TILE)
                            : rsv_capacity_bound(n, BITS);
   const uint32_t tb1 = (uint32_t)((rbound + TILE - 1) / TILE) + rns;
   // the cursors after the slices, 256-byte aligned (8-bit: 64-bit adds)
@@ -3827,7 +3879,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     const Op op0 = make_digit<Op>((uint32_t)(W - BITS), (uint32_t)RADIX - 1u, bias);
     ScopedTimer tm("rsvsample", st, n);
     if (pc) {
-      hipLaunchKernelGGL((k_rsv_sample_pc<RADIX, TILE, Op>), dim3(kRsvRanges * kRsvBlocks), dim3(256), 0, st,
+      auto smp = rper == 4 ? k_rsv_sample_pc<RADIX, TILE, 4, Op>
+                 : rper == 8 ? k_rsv_sample_pc<RADIX, TILE, 8, Op> : k_rsv_sample_pc<RADIX, TILE, 16, Op>;
+      hipLaunchKernelGGL(smp, dim3(kRsvRanges * kRsvBlocks), dim3(256), 0, st,
                          reinterpret_cast<const uint32_t*>(in), reinterpret_cast<const uint4*>(pc->dev), pc->cum,
                          pc->np, nseg0, T0, (uint32_t)n, op0, rpart, rslice, rcur, ws.hyb_host, Cn0,
                          BITS == 4 ? tb1 * (uint32_t)RADIX : 0u, ws.tticket + 32, ctr, NB, rmode == 2);

@@ -163,14 +163,16 @@ def _sort_timed(D, buf, off, ln, sg, nseg, b):
 
 
 @pytest.mark.parametrize("reserve", ["0", "1"])
-@pytest.mark.parametrize("nseg,n", [(1, (1 << 21) + 5), (5, (1 << 22) + 3), (8, (1 << 23) + 1), (31, (1 << 23) + 7),
+@pytest.mark.parametrize("nseg,n", [(1, (1 << 21) + 5), (5, (1 << 22) + 3), (8, (1 << 23) + 1), (16, (1 << 23) + 5),
+                                    (31, (1 << 23) + 7),
                                     (40, (1 << 23) + 9)])
 def test_reserved_depth0_pieces(D, oracle_mod, monkeypatch, reserve, nseg, n):
     """The piece sort's reserved depth 0 (4-bit digits; the round sorts of the
     multi-GPU schedule): no count pass, the depth-0 pass reserves each run in
-    a slice per (segment, digit, range) sized by 131072 samples per range,
-    taken by global key rank through the piece table.  Up to 4096 slices
-    (31 segments); 40 segments keep the count pass.  Exact; which depth 0
+    a slice per (segment, digit, range) sized by 32768 (<= 8 segments),
+    65536 (16) or 131072 (31) samples per range, taken by global key rank
+    through the piece table.  Up to 4096 slices (31 segments); 40 segments
+    keep the count pass.  Exact; which depth 0
     ran is read from the timing registry."""
     import pylibsort
     monkeypatch.setenv("LIBSORT_HYB_RESERVE", reserve)
