@@ -115,7 +115,8 @@ struct Workspace {
   // child tables of two depths, counters; a pinned mirror for the host checks
   uint32_t* hyb = nullptr;
   size_t hyb_cap = 0;  // words
-  uint32_t* hyb_host = nullptr;  // pinned, 256 words
+  uint32_t* hyb_host = nullptr;  // pinned, 512 words
+  uint32_t hyb_seq = 0;          // the last sampler sequence number (hyb_host[511])
   hipEvent_t hyb_evt = nullptr;
   hipError_t ensure_hybrid(size_t words);
 

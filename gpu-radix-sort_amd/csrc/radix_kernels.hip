@@ -27,7 +27,10 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
+#include <cstring>
 #include <type_traits>
 
 namespace lsort {
@@ -2063,6 +2066,10 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const K* in, K* out, cons
 //             of its segment),
 // and the child's start, size and tile count for the next depth.  Depth 0
 // (fixed tiles) has one segment, tiles [0, fixed_tiles), starting at 0.
+// The last block to finish (ticket) then, when asked, scans the children's
+// tile counts into ctile0_next[0..m] (*ntiles = the next depth's tile count)
+// and copies the counter words ctr[11..14] (stats = ctr + 11) to the host's
+// pinned mirror: no separate prefix launch, no copy.
 template <int RADIX, int TILE>
 __global__ __launch_bounds__(256) void k_hyb_children(const uint32_t* __restrict__ C, const uint32_t* __restrict__ B,
                                                       const uint32_t* __restrict__ D, uint32_t rows, uint32_t nkeys,
@@ -2070,10 +2077,13 @@ __global__ __launch_bounds__(256) void k_hyb_children(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ cstart, uint32_t fixed_tiles,
                                                       uint32_t* __restrict__ segbase, uint32_t* __restrict__ ncstart,
                                                       uint32_t* __restrict__ nsize, uint32_t* __restrict__ ntl,
-                                                      uint32_t* __restrict__ stats, uint32_t cap1) {
+                                                      uint32_t* __restrict__ stats, uint32_t cap1, uint32_t* ticket,
+                                                      uint32_t* __restrict__ ctile0_next, uint32_t* __restrict__ ntiles,
+                                                      const uint32_t* ctr_words, uint32_t* __restrict__ host_words) {
   static_assert(RADIX == 16 || RADIX == 256, "4- or 8-bit digits");
   constexpr int CH = col_chunk_rows(RADIX);
   __shared__ uint32_t s_wsum[4];
+  __shared__ uint32_t s_flag;
   const uint32_t g = blockIdx.x * 256 + threadIdx.x;
   const uint32_t seg = g / RADIX, d = g % RADIX;
   const bool live = seg < nseg;
@@ -2112,39 +2122,53 @@ __global__ __launch_bounds__(256) void k_hyb_children(const uint32_t* __restrict
     if ((threadIdx.x & (kWave - 1)) == 0 && mx) atomicMax(&stats[0], mx);
     if (size > cap1) atomicAdd(&stats[1], 1u);
   }
-  if (!live) return;
-  const uint32_t start = cs + excl;
-  segbase[g] = start - p0;
-  ncstart[g] = start;
-  nsize[g] = size;
-  if (ntl) ntl[g] = (size + TILE - 1) / TILE;
+  if (live) {
+    const uint32_t start = cs + excl;
+    segbase[g] = start - p0;
+    ncstart[g] = start;
+    nsize[g] = size;
+    if (ntl) st_agent(&ntl[g], (size + TILE - 1) / TILE);
+  }
+  if (!ctile0_next && !host_words) return;
+  if (!last_arriver(ticket, gridDim.x, &s_flag)) return;
+  if (ctile0_next) {
+    const uint32_t m = nseg * RADIX, per = (m + 255) / 256;
+    const uint32_t a = min(m, threadIdx.x * per), b = min(m, a + per);
+    // (batches of 16 loads in flight: a loop of single loads waits on each)
+    uint32_t sum = 0;
+    for (uint32_t i = a; i < b; i += 16) {
+      uint32_t v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = i + q < b ? ld_agent(&ntl[i + q]) : 0u;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sum += v[q];
+    }
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan<256>(sum, s_wsum, tot);
+    for (uint32_t i = a; i < b; i += 16) {
+      uint32_t v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = i + q < b ? ld_agent(&ntl[i + q]) : 0u;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        if (i + q < b) ctile0_next[i + q] = run;
+        run += v[q];
+      }
+    }
+    if (threadIdx.x == 0) {
+      ctile0_next[m] = tot;
+      *ntiles = tot;
+    }
+  }
+  if (host_words && threadIdx.x < 4)
+    __hip_atomic_store(&host_words[threadIdx.x], ld_agent(&ctr_words[threadIdx.x]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) *ticket = 0u;
 }
 
 // The hybrid's counter words: zero, and [9] = the bucket count.
 __global__ void k_hyb_init(uint32_t* __restrict__ ctr, uint32_t nb) {
   if (threadIdx.x < 16) ctr[threadIdx.x] = threadIdx.x == 9 ? nb : 0u;
-}
-
-// Exclusive scan of the children's tile counts (one block): ctile0[0..m],
-// ctile0[m] = *total = the next depth's tile count.
-__global__ __launch_bounds__(1024) void k_hyb_tile_prefix(const uint32_t* __restrict__ ntl, uint32_t m,
-                                                          uint32_t* __restrict__ ctile0, uint32_t* __restrict__ total) {
-  __shared__ uint32_t s_wsum[16];
-  const uint32_t per = (m + 1023) / 1024;
-  const uint32_t a = threadIdx.x * per, b = min(m, a + per);
-  uint32_t sum = 0;
-  for (uint32_t i = a; i < b; ++i) sum += ntl[i];
-  uint32_t tot;
-  uint32_t run = block_exclusive_scan<1024>(sum, s_wsum, tot);
-  for (uint32_t i = a; i < b; ++i) {
-    const uint32_t v = ntl[i];
-    ctile0[i] = run;
-    run += v;
-  }
-  if (threadIdx.x == 0) {
-    ctile0[m] = tot;
-    *total = tot;
-  }
 }
 
 // The next depth's tile table: tile t belongs to the child c with
@@ -2182,6 +2206,27 @@ __global__ __launch_bounds__(256) void k_hyb_expand(const uint32_t* __restrict__
 // its slice full writes nothing and raises a flag, and the host then runs the
 // LSD sort from the untouched input (sort_hybrid).
 constexpr int kRsvRanges = 8;
+// hyb_host word the samplers raise to the sort's sequence number after their
+// size estimates (the host polls it instead of recording an event)
+constexpr uint32_t kHybSeqWord = 511;
+
+// Waits until the pinned word *w == v (a kernel's system-scope store).  After
+// ~1 s of polling (a stream with much queued ahead) it synchronises the
+// stream instead, after which the word must hold v.
+inline hipError_t wait_host_word(const uint32_t* w, uint32_t v, hipStream_t st) {
+  const volatile uint32_t* p = w;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1; *p != v; ++i) {
+    if ((i & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+      const hipError_t e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return e;
+      return *p == v ? hipSuccess : hipErrorUnknown;
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  return hipSuccess;
+}
 constexpr int kRsvBlocks = 32;  // sampling blocks per range
 // samples per thread: 4 for 4-bit digits (32768 per range, ~2048 per slice),
 // 16 for 8-bit (131072 per range, ~512 per slice)
@@ -2222,7 +2267,7 @@ __global__ __launch_bounds__(256) void k_rsv_sample(const uint32_t* __restrict__
                                                     uint32_t* __restrict__ rcur, uint32_t* __restrict__ est,
                                                     uint32_t* __restrict__ Czero, uint32_t zero_words,
                                                     uint32_t* ticket, uint32_t* __restrict__ ctr, uint32_t nb,
-                                                    bool short_caps) {
+                                                    bool short_caps, uint32_t seq) {
   static_assert(RADIX <= 256, "one digit per thread");
   constexpr int NS = RADIX * kRsvRanges;
   constexpr int PT = rsv_per_thread<RADIX>();
@@ -2310,7 +2355,10 @@ __global__ __launch_bounds__(256) void k_rsv_sample(const uint32_t* __restrict__
     // follows this kernel; no copy kernel in between)
     __hip_atomic_store(&est[tid], (uint32_t)min(4294967295.0, est_d + 0.5), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
   }
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(&est[kHybSeqWord], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (tid == 0) rslice[3 * NS] = tot_t;
   if (tid < 16) ctr[tid] = tid == 9 ? nb : 0u;  // (k_hyb_init's words)
   if (tid == 0) *ticket = 0u;
@@ -2340,7 +2388,8 @@ __global__ __launch_bounds__(256) void k_rsv_sample_pc(const uint32_t* __restric
                                                        uint32_t* __restrict__ rslice, uint32_t* __restrict__ rcur,
                                                        uint32_t* __restrict__ est, uint32_t* __restrict__ Czero,
                                                        uint32_t zero_words, uint32_t* ticket,
-                                                       uint32_t* __restrict__ ctr, uint32_t nb, bool short_caps) {
+                                                       uint32_t* __restrict__ ctr, uint32_t nb, bool short_caps,
+                                                       uint32_t seq) {
   constexpr uint32_t S = kRsvBlocks * 256 * PER;
   constexpr uint32_t kMaxChildren = kRsvMaxSlices / kRsvRanges;
   __shared__ uint32_t s_h[kMaxChildren];
@@ -2508,6 +2557,8 @@ __global__ __launch_bounds__(256) void k_rsv_sample_pc(const uint32_t* __restric
   if (tid == 0) {
     rslice[3 * NS] = tot_t;
     __hip_atomic_store(&est[0], s_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+    __hip_atomic_store(&est[kHybSeqWord], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (tid < 16) ctr[tid] = tid == 9 ? nb : 0u;  // (k_hyb_init's words; k_hyb_pieces sets ctr[0] after)
   if (tid == 0) *ticket = 0u;
@@ -3139,7 +3190,10 @@ hipError_t Workspace::ensure_tiles(size_t count_words, size_t chunk_words) {
 
 hipError_t Workspace::ensure_hybrid(size_t words) {
   if (!hyb_evt) LS_TRY(hipEventCreateWithFlags(&hyb_evt, hipEventDisableTiming));
-  if (!hyb_host) LS_TRY(hipHostMalloc(&hyb_host, 256 * sizeof(uint32_t), hipHostMallocDefault));
+  if (!hyb_host) {
+    LS_TRY(hipHostMalloc(&hyb_host, 512 * sizeof(uint32_t), hipHostMallocDefault));
+    std::memset(hyb_host, 0, 512 * sizeof(uint32_t));  // (the sequence word starts below every sort's)
+  }
   if (words <= hyb_cap) return hipSuccess;
   if (hyb) { (void)hipFree(hyb); hyb = nullptr; }
   hyb_cap = 0;
@@ -3836,6 +3890,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     rmode = 0;
   }
   const bool rsv = rmode != 0;
+  uint32_t rseq = 0;  // the sampler's sequence word (wait_host_word)
   // segments of depth k (each child has at most one partial tile)
   auto nseg_at = [&](int k) { return nseg0 << (BITS * k); };
   auto tbound = [&](int k) { return k == 0 ? T0 : (k == 1 && rsv) ? tb1 : T0 + nseg_at(k); };
@@ -3878,18 +3933,19 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     // in them; the next depth's tiles and child starts from the cursors)
     const Op op0 = make_digit<Op>((uint32_t)(W - BITS), (uint32_t)RADIX - 1u, bias);
     ScopedTimer tm("rsvsample", st, n);
+    rseq = ++ws.hyb_seq;
     if (pc) {
       auto smp = rper == 4 ? k_rsv_sample_pc<RADIX, TILE, 4, Op>
                  : rper == 8 ? k_rsv_sample_pc<RADIX, TILE, 8, Op> : k_rsv_sample_pc<RADIX, TILE, 16, Op>;
       hipLaunchKernelGGL(smp, dim3(kRsvRanges * kRsvBlocks), dim3(256), 0, st,
                          reinterpret_cast<const uint32_t*>(in), reinterpret_cast<const uint4*>(pc->dev), pc->cum,
                          pc->np, nseg0, T0, (uint32_t)n, op0, rpart, rslice, rcur, ws.hyb_host, Cn0,
-                         BITS == 4 ? tb1 * (uint32_t)RADIX : 0u, ws.tticket + 32, ctr, NB, rmode == 2);
+                         BITS == 4 ? tb1 * (uint32_t)RADIX : 0u, ws.tticket + 32, ctr, NB, rmode == 2, rseq);
     } else {
       hipLaunchKernelGGL((k_rsv_sample<RADIX, TILE, Op>), dim3(kRsvRanges * kRsvBlocks), dim3(256), 0, st,
                          reinterpret_cast<const uint32_t*>(in), (uint32_t)n, T0, op0, rpart, rslice, rcur,
                          ws.hyb_host, Cn0, BITS == 4 ? tb1 * (uint32_t)RADIX : 0u, ws.tticket + 32, ctr, NB,
-                         rmode == 2);
+                         rmode == 2, rseq);
     }
     LS_TRY(hipGetLastError());
   }
@@ -3929,7 +3985,6 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       if (k == 0 && rsv) {
         // Reserved depth 0 (sampled above): the pass reserves its runs in the
         // slices; the next depth's tiles and child starts from the cursors
-        LS_TRY(hipEventRecord(ws.hyb_evt, st));
         HybridGeo g0{tiles[0], ctr, nullptr, nullptr, nullptr, rcur, rslice, ctr + 14, rns};
         {
           ScopedTimer tm("tilepass", st, n);
@@ -3949,8 +4004,10 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
         }
         // skew check on the sampled digit (pieces: child) sizes (the pass
         // keeps the GPU busy; it wrote only ws.rsv, so abandoning leaves in
-        // intact)
-        LS_TRY(hipEventSynchronize(ws.hyb_evt));
+        // intact).  The sampler raised its sequence word in the pinned
+        // mirror after the sizes: polled, not an event (an event record
+        // stalls the stream ~6 us).
+        LS_TRY(wait_host_word(ws.hyb_host + kHybSeqWord, rseq, st));
         if (pc) {
           if ((double)ws.hyb_host[0] / (double)(1ull << (BITS * (DEPTHS - 1))) > 0.9 * cap) return hipSuccess;
         } else {
@@ -3990,22 +4047,23 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       ScopedTimer tm("hybplan", st, m);
       // stats: the last depth's bucket sizes (ctr[11], [12]); pieces, depth 0
       // of several: its largest child (ctr[13]) for the skew check
+      // (the last depth: ctr[11..14] -> hyb_host[256..259], written by the
+      // kernel's last block and read back while the last pass runs; other
+      // depths: the next depth's tile prefix in the last block)
       uint32_t* stats = last ? ctr + 11 : (pc && k == 0) ? ctr + 13 : nullptr;
       hipLaunchKernelGGL((k_hyb_children<RADIX, TILE>), dim3((m + 255) / 256), dim3(256), 0, st, C, ws.tb, D, rows,
                          (uint32_t)n, nseg, tab ? ctile0[k & 1] : nullptr, cstart[k & 1], T0, segbase,
-                         cstart[(k + 1) & 1], nsize, last ? nullptr : ntl, stats, cap1);
+                         cstart[(k + 1) & 1], nsize, last ? nullptr : ntl, stats, cap1, ws.tticket + 48,
+                         last ? nullptr : ctile0[(k + 1) & 1], ctr + k + 1, ctr + 11,
+                         last ? ws.hyb_host + 256 : nullptr);
       LS_TRY(hipGetLastError());
       if (last) {
-        // the bucket sizes, read back while the last pass runs
-        LS_TRY(hipMemcpyAsync(ws.hyb_host + 20, ctr + 11, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         LS_TRY(hipEventRecord(ws.hyb_evt, st));
       } else if (pc && k == 0) {
-        LS_TRY(hipMemcpyAsync(ws.hyb_host + 24, ctr + 13, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        LS_TRY(hipMemcpyAsync(ws.hyb_host + 260, ctr + 13, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         LS_TRY(hipEventRecord(ws.hyb_evt, st));
       }
       if (!last) {
-        hipLaunchKernelGGL(k_hyb_tile_prefix, dim3(1), dim3(1024), 0, st, ntl, m, ctile0[(k + 1) & 1], ctr + k + 1);
-        LS_TRY(hipGetLastError());
         const uint32_t nb_ = tbound(k + 1);
         hipLaunchKernelGGL((k_hyb_expand<RADIX, TILE>), dim3((nb_ + 255) / 256), dim3(256), 0, st,
                            ctile0[(k + 1) & 1], m, cstart[(k + 1) & 1], nsize, ctr + k + 1, nb_,
@@ -4056,7 +4114,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       // pieces: a depth-0 child whose buckets would average > 0.9 of a block
       // (a skewed input): the caller's LSD sort instead (in is untouched)
       LS_TRY(hipEventSynchronize(ws.hyb_evt));
-      if ((double)ws.hyb_host[24] / (double)(1ull << (BITS * (DEPTHS - 1))) > 0.9 * cap) return hipSuccess;
+      if ((double)ws.hyb_host[260] / (double)(1ull << (BITS * (DEPTHS - 1))) > 0.9 * cap) return hipSuccess;
     }
   }
   // the bucket sizes (read back while the last pass runs): a bucket larger
@@ -4065,9 +4123,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   LS_TRY(hipEventSynchronize(ws.hyb_evt));
   // reserved depth 0 overflowed (a slice's sample undercounted it): the
   // later depths did nothing; the caller's LSD sort from the input instead
-  if (rsv && ws.hyb_host[23]) return hipSuccess;
+  if (rsv && ws.hyb_host[259]) return hipSuccess;
   *handled = true;
-  if (ws.hyb_host[21] > kListCap || ws.hyb_host[20] > cap) {
+  if (ws.hyb_host[257] > kListCap || ws.hyb_host[256] > cap) {
     // pieces: every bit (the segments' own bits vary across out)
     if (pc) return sort_impl<K, V>(ws, out, out, tmp, vout, vout, vtmp, n, 0, 8 * (int)sizeof(K), BITS, st);
     return sort_impl<K, V>(ws, out, out, tmp, vout, vout, vtmp, n, 0, W, BITS, st, bias);
@@ -4082,6 +4140,10 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     // 64-bit keys: on-chip steps over the top 16 of the 48 bucket bits, then
     // the tie fix-up (k_bucket_sort FIX)
     constexpr int FIXB = sizeof(K) == 8 ? LIBSORT_BUCKET64_FIX : 0;
+    // the second size's grid: the buckets over the first block, as planned
+    // (k_hyb_children's count, the same cap as the first launch lists by);
+    // none: no launch
+    const uint32_t n2 = std::min<uint32_t>(ws.hyb_host[257], kListCap);
     // 32-bit keys without values, lbits <= 16: the counting placement
     // (k_bucket_sort CNT, `cnt` above)
     auto launch = [&](auto cnt_c) -> hipError_t {
@@ -4110,7 +4172,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
 #define LS_BS2(I)                                          \
   LS_BS(I, NB, ctr + 9, NB, nullptr, ctr + 8, olist);      \
   LS_TRY(hipGetLastError());                               \
-  LS_BS(I + 6, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr)
+  if (n2) {                                                \
+    LS_BS(I + 6, n2, ctr + 8, kListCap, olist, ctr + 10, nullptr); \
+  }
 #define LS_BS512(I, G, NBP, CAPN, IL, OV, OL) LS_BSX(512, I, G, NBP, CAPN, IL, OV, OL)
 #define LS_BS1024(I, G, NBP, CAPN, IL, OV, OL) LS_BSX(1024, I, G, NBP, CAPN, IL, OV, OL)
       // the buckets the counting placement listed (3-bit overflow: 8+ equal
@@ -4132,7 +4196,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
           if constexpr (sizeof(K) == 4) {
             LS_BS512(17, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
             LS_TRY(hipGetLastError());
-            LS_BS512(23, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+            if (n2) {
+              LS_BS512(23, n2, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+            }
             LS_TRY(hipGetLastError());
             LS_BSL(512, 23);
           }
@@ -4141,7 +4207,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
           if constexpr (C) {
             LS_BS1024(17, NB, ctr + 9, NB, nullptr, ctr + 8, olist);
             LS_TRY(hipGetLastError());
-            LS_BS1024(23, kListCap, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+            if (n2) {
+              LS_BS1024(23, n2, ctr + 8, kListCap, olist, ctr + 10, nullptr);
+            }
             LS_TRY(hipGetLastError());
             LS_BSL(1024, 23);
           }
@@ -4332,7 +4400,9 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   pcum[K] = run;
   LS_TRY(hipMemcpyAsync(ws.seg_dev, ws.seg_host, (g64 + 3 * (size_t)K) * sizeof(uint64_t), hipMemcpyHostToDevice,
                         st));
-  LS_TRY(hipEventRecord(ws.seg_evt, st));
+  // seg_evt guards the staging against the next call; a sort the hybrid
+  // handled has already waited on an event behind this copy (its bucket
+  // stats), so only the other paths record it (an event costs the stream ~6 us)
   if (depths > 0) {
     const uint32_t* dev32 = reinterpret_cast<const uint32_t*>(ws.seg_dev);
     HybPieces pc{dev32, K, nseg, tile, depths, (double)npop / nseg, dev32 + (pcum - h32)};
@@ -4351,6 +4421,7 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
       return hipSuccess;
     }
   }
+  LS_TRY(hipEventRecord(ws.seg_evt, st));
   // small or skewed: gather the pieces into segment order, LSD sort in place
   // (bits == 0: the segments are single values, already in order)
   LS_TRY(segment_copy_dev_u32(in, out, ws.seg_dev + g64, K, maxlen, n, st));

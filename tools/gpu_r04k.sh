@@ -1,7 +1,7 @@
 #!/bin/bash
-# the whole GPU suite, then the 8-GPU-shape schedule (both shape variants) with kernel stats
+# fused planning (children + tile prefix + host stats), sized second bucket launch: full GPU suite, then the 8-GPU-shape schedule
 set -o pipefail
-O=gpurun_out/r04h
+O=gpurun_out/r04k
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ > $O/pytest.log 2>&1
