@@ -2079,7 +2079,8 @@ __global__ __launch_bounds__(256) void k_hyb_children(const uint32_t* __restrict
                                                       uint32_t* __restrict__ nsize, uint32_t* __restrict__ ntl,
                                                       uint32_t* __restrict__ stats, uint32_t cap1, uint32_t* ticket,
                                                       uint32_t* __restrict__ ctile0_next, uint32_t* __restrict__ ntiles,
-                                                      const uint32_t* ctr_words, uint32_t* __restrict__ host_words) {
+                                                      const uint32_t* ctr_words, uint32_t* __restrict__ host_words,
+                                                      uint32_t* host_seq, uint32_t seq) {
   static_assert(RADIX == 16 || RADIX == 256, "4- or 8-bit digits");
   constexpr int CH = col_chunk_rows(RADIX);
   __shared__ uint32_t s_wsum[4];
@@ -2160,9 +2161,16 @@ __global__ __launch_bounds__(256) void k_hyb_children(const uint32_t* __restrict
       *ntiles = tot;
     }
   }
-  if (host_words && threadIdx.x < 4)
-    __hip_atomic_store(&host_words[threadIdx.x], ld_agent(&ctr_words[threadIdx.x]), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (host_words) {
+    if (threadIdx.x < 4) {
+      __hip_atomic_store(&host_words[threadIdx.x], ld_agent(&ctr_words[threadIdx.x]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+    }
+    __syncthreads();
+    // then the sequence word the host polls (wait_host_word)
+    if (threadIdx.x == 0) __hip_atomic_store(host_seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (threadIdx.x == 0) *ticket = 0u;
 }
 
@@ -2209,6 +2217,7 @@ constexpr int kRsvRanges = 8;
 // hyb_host word the samplers raise to the sort's sequence number after their
 // size estimates (the host polls it instead of recording an event)
 constexpr uint32_t kHybSeqWord = 511;
+constexpr uint32_t kHybSeqWord2 = 510;  // k_hyb_children's, after the bucket stats
 
 // Waits until the pinned word *w == v (a kernel's system-scope store).  After
 // ~1 s of polling (a stream with much queued ahead) it synchronises the
@@ -3891,6 +3900,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   }
   const bool rsv = rmode != 0;
   uint32_t rseq = 0;  // the sampler's sequence word (wait_host_word)
+  uint32_t sseq = 0;  // the last depth's children (bucket stats)
   // segments of depth k (each child has at most one partial tile)
   auto nseg_at = [&](int k) { return nseg0 << (BITS * k); };
   auto tbound = [&](int k) { return k == 0 ? T0 : (k == 1 && rsv) ? tb1 : T0 + nseg_at(k); };
@@ -4055,10 +4065,10 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
                          (uint32_t)n, nseg, tab ? ctile0[k & 1] : nullptr, cstart[k & 1], T0, segbase,
                          cstart[(k + 1) & 1], nsize, last ? nullptr : ntl, stats, cap1, ws.tticket + 48,
                          last ? nullptr : ctile0[(k + 1) & 1], ctr + k + 1, ctr + 11,
-                         last ? ws.hyb_host + 256 : nullptr);
+                         last ? ws.hyb_host + 256 : nullptr, ws.hyb_host + kHybSeqWord2, last ? ++ws.hyb_seq : 0u);
       LS_TRY(hipGetLastError());
       if (last) {
-        LS_TRY(hipEventRecord(ws.hyb_evt, st));
+        sseq = ws.hyb_seq;
       } else if (pc && k == 0) {
         LS_TRY(hipMemcpyAsync(ws.hyb_host + 260, ctr + 13, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         LS_TRY(hipEventRecord(ws.hyb_evt, st));
@@ -4120,7 +4130,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   // the bucket sizes (read back while the last pass runs): a bucket larger
   // than the second block, or more buckets over the first than its list
   // holds -> the LSD sort of out (any order sorts) instead of the bucket sort
-  LS_TRY(hipEventSynchronize(ws.hyb_evt));
+  // (polled: the children kernel raised the sequence word after them)
+  LS_TRY(wait_host_word(ws.hyb_host + kHybSeqWord2, sseq, st));
   // reserved depth 0 overflowed (a slice's sample undercounted it): the
   // later depths did nothing; the caller's LSD sort from the input instead
   if (rsv && ws.hyb_host[259]) return hipSuccess;
@@ -4401,8 +4412,9 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   LS_TRY(hipMemcpyAsync(ws.seg_dev, ws.seg_host, (g64 + 3 * (size_t)K) * sizeof(uint64_t), hipMemcpyHostToDevice,
                         st));
   // seg_evt guards the staging against the next call; a sort the hybrid
-  // handled has already waited on an event behind this copy (its bucket
-  // stats), so only the other paths record it (an event costs the stream ~6 us)
+  // handled has already waited for a kernel behind this copy (the bucket
+  // stats' sequence word), so only the other paths record it (an event
+  // costs the stream ~6 us)
   if (depths > 0) {
     const uint32_t* dev32 = reinterpret_cast<const uint32_t*>(ws.seg_dev);
     HybPieces pc{dev32, K, nseg, tile, depths, (double)npop / nseg, dev32 + (pcum - h32)};

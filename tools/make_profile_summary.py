@@ -60,10 +60,11 @@ def headline(row):
 
 
 def bucketsort(row):
-    """The headline's bucket sort: the counting placement (CNT, the last
-    template argument), not variants.bucket_lsd_steps' LSD steps."""
+    """The headline's bucket sort: the counting placement's first-size launch
+    over the 65536 buckets (round 4: its own kernel, k_bucket_count), not
+    variants.bucket_lsd_steps' LSD steps (k_bucket_sort)."""
     name = row.get("Kernel_Name", "")
-    return "k_bucket_sort<4," in name and name.split(">(")[0].endswith("true") and _groups(row) == 65536
+    return "k_bucket_count<" in name and _groups(row) == 65536
 
 
 trace = sorted(glob.glob(str(src / "stats" / "**" / "*kernel_trace.csv"), recursive=True))
@@ -117,13 +118,13 @@ if fetch and write:
 # the bucket sort (the MSD hybrid's last step: one HBM read and write per key)
 fetch, write = pmc("FETCH_SIZE", bucketsort), pmc("WRITE_SIZE", bucketsort)
 bs = []
-bs_name = "k_bucket_sort"
+bs_name = "k_bucket_count"
 for f in trace:
     for r in csv.DictReader(open(f)):
         if bucketsort(r):
             bs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
             nm = r["Kernel_Name"]
-            bs_name = "k_bucket_sort" + nm[nm.find("<"):nm.find(">") + 1].replace("lsort::", "")
+            bs_name = "k_bucket_count" + nm[nm.find("<"):nm.find(">") + 1].replace("lsort::", "")
 if fetch and write and bs:
     fr = sum(fetch) / len(fetch) * 1024 * 2
     wr = sum(write) / len(write) * 1024

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Per-rank step model of the 8-GPU top-digit schedule.
+
+    python tools/msd_model.py [--partition-ms 1.22] [--gpu-ms 5.00] [--n1 119.3]
+
+The step is the partition (exposed), round 0's exchange, then each round
+the longer of its sort and the next round's exchange, then the last sort.
+Inputs are the measured one-GPU numbers of the 8-GPU shape (tools/msd_rccl1.py
+MSD_SHAPE8=1: GPU work per rank without the self copy, the partition's part
+of it) and the N = 1 bench line; the per-GPU send rate is the free variable.
+A per-round overhead (the round sort's small kernels) is kept fixed when the
+round profile changes.
+"""
+import argparse
+
+KEYS_PER_RANK = 1 << 29
+SENT_BYTES = 7 / 8 * KEYS_PER_RANK * 4  # bytes a rank sends at 8 GPUs
+
+PROFILES = {
+    "K4 x1.2 (built)": [1, 1.2, 1.44, 1.728],
+    "K4 flat": [1, 1, 1, 1],
+    "K4 x0.8": [1, 0.8, 0.64, 0.512],
+    "K5 hump": [0.6, 1, 1, 0.9, 0.5],
+    "K6 hump": [0.5, 0.9, 1, 1, 0.8, 0.4],
+}
+
+
+def step_ms(weights, rate_gbs, part_ms, sorts_ms, per_round_ms, built_rounds=4):
+    t = sum(weights)
+    f = [w / t for w in weights]
+    e = SENT_BYTES / (rate_gbs * 1e9) * 1e3
+    body = sorts_ms - built_rounds * per_round_ms
+    s = [x * body + per_round_ms for x in f]
+    k = len(f)
+    return part_ms + f[0] * e + sum(max(s[i], f[i + 1] * e) for i in range(k - 1)) + s[-1], e
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--partition-ms", type=float, default=1.22)
+    ap.add_argument("--gpu-ms", type=float, default=5.00, help="GPU work per rank, 8-GPU shape")
+    ap.add_argument("--per-round-ms", type=float, default=0.13)
+    ap.add_argument("--n1", type=float, default=119.3, help="N = 1 line, Gkeys/s")
+    a = ap.parse_args()
+    sorts = a.gpu_ms - a.partition_ms
+    for name, w in PROFILES.items():
+        cells = []
+        for rate in (700, 450, 400, 360, 300):
+            st, e = step_ms(w, rate, a.partition_ms, sorts, a.per_round_ms)
+            agg = 8 * KEYS_PER_RANK / (st * 1e-3) / 1e9
+            cells.append("%d GB/s: E %.2f step %.2f ms %.0f Gk/s %.2fx" % (rate, e, st, agg, agg / a.n1))
+        print("%-16s %s" % (name, " | ".join(cells)))
+
+
+if __name__ == "__main__":
+    main()
