@@ -1605,9 +1605,12 @@ __device__ __forceinline__ uint32_t field2_sum(uint32_t w) {
 // of 256 threads per CU): the overflow flag is a spare bit of a cell word,
 // the block scan's wave sums borrow cell words once every wave holds its
 // cells in registers, and the keys are placed over the words.  Returns false
-// (nothing written) on a count overflow.
+// (nothing written) on a count overflow.  Returns 0 when placed, else the
+// overflow's weight: kCnt2F the threads that saw a count wrap (a uniform
+// bucket's overflow is one value with 4 keys: 1-2; a duplicate-heavy bucket
+// wraps in most threads), the other modes 1.
 template <int BLOCK, int ITEMS, int MODE, typename Op>
-__device__ __forceinline__ bool bucket_count_place(const uint32_t (&k)[ITEMS], uint64_t* s_cw, uint32_t* out,
+__device__ __forceinline__ uint32_t bucket_count_place(const uint32_t (&k)[ITEMS], uint64_t* s_cw, uint32_t* out,
                                                    uint32_t start, uint32_t len, uint32_t lbits_in, uint32_t bias) {
   constexpr int PER = kCntCells / BLOCK;
   static_assert(PER >= 1 && kCntCells % BLOCK == 0, "cells per thread");
@@ -1644,9 +1647,10 @@ __device__ __forceinline__ bool bucket_count_place(const uint32_t (&k)[ITEMS], u
         rk[j] = (atomicAdd(&s_w[ci(v >> 4)], 1u << sh) >> sh) & 3u;
         ovf |= rk[j] == 3u;
       }
-    if (__any(ovf) && lane == 0) s_ws2[BLOCK / kWave] = 1u;
+    const uint64_t bal = __ballot(ovf);
+    if (bal && lane == 0) atomicAdd(&s_ws2[BLOCK / kWave], (uint32_t)__popcll(bal));
     __syncthreads();
-    if (s_ws2[BLOCK / kWave]) return false;
+    if (const uint32_t sev = s_ws2[BLOCK / kWave]) return sev;
     uint32_t cnt[PER], sum = 0;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -1684,7 +1688,7 @@ __device__ __forceinline__ bool bucket_count_place(const uint32_t (&k)[ITEMS], u
     // no LDS beyond the cells (__syncthreads_or would take 256 bytes)
     if (__any(ovf) && lane == 0) atomicOr((unsigned long long*)&s_cw[0], 1ull << 63);
     __syncthreads();
-    if (s_cw[0] >> 63) return false;
+    if (s_cw[0] >> 63) return 1u;
     uint64_t cw[PER];
     uint32_t sum = 0;
 #pragma unroll
@@ -1757,7 +1761,7 @@ __device__ __forceinline__ bool bucket_count_place(const uint32_t (&k)[ITEMS], u
     const uint32_t p = wbase + j * kWave + lane;
     if (p < len) out[(size_t)start + p] = s_keys[p];
   }
-  return true;
+  return 0u;
 }
 
 // The counting placement's own kernel (32-bit keys without values, lbits <=
@@ -1768,37 +1772,59 @@ __device__ __forceinline__ bool bucket_count_place(const uint32_t (&k)[ITEMS], u
 // size (as k_bucket_sort); one whose 3-bit counts overflowed (8+ equal keys)
 // is written nothing and listed in ovf_list (*ovf_n entries) for the LSD
 // steps of k_bucket_sort LIST, so this kernel holds no LSD-step code.
-template <int BLOCK, int ITEMS, typename Op, int MODE>
+// LIST: a persistent grid over ilist[0, min(*nb, nb_cap)) -- the 3-bit retry
+// of the buckets whose 2-bit counts overflowed.  An overflowed bucket is
+// written nothing and listed: in retry_list when given and its overflow
+// weighs <= kRetryMax (a few values with 4+ keys), else in ovf_list (the LSD
+// steps of k_bucket_sort LIST), so this kernel holds no LSD-step code.
+constexpr uint32_t kRetryMax = 16;
+template <int BLOCK, int ITEMS, typename Op, int MODE, bool LIST = false>
 __global__ __launch_bounds__(BLOCK)
 __attribute__((amdgpu_waves_per_eu(BLOCK >= 1024 && ITEMS <= 17 && MODE != kCntSmall ? 8 : 1, 8)))
 void k_bucket_count(const uint32_t* in, uint32_t* out, const uint32_t* __restrict__ bstart,
                     const uint32_t* __restrict__ blen, const uint32_t* __restrict__ nb, uint32_t nb_cap,
                     const uint32_t* __restrict__ ilist, uint32_t lbits, uint32_t bias,
                     uint32_t* __restrict__ oversized, uint32_t* __restrict__ olist, uint32_t olist_cap,
-                    uint32_t* __restrict__ ovf_n, uint32_t* __restrict__ ovf_list) {
+                    uint32_t* __restrict__ ovf_n, uint32_t* __restrict__ ovf_list, uint32_t* __restrict__ retry_n,
+                    uint32_t* __restrict__ retry_list) {
   constexpr int CAP = BLOCK * ITEMS;
   static_assert(CAP < 65536, "16-bit cell starts");
   __shared__ uint64_t s_cw[cnt_lds_words<CAP, MODE>()];
-  if (blockIdx.x >= min(*nb, nb_cap)) return;
-  const uint32_t b = ilist ? ilist[blockIdx.x] : blockIdx.x;
-  const uint32_t start = bstart[b], len = blen[b];
-  if (len > (uint32_t)CAP) {
-    if (threadIdx.x == 0) {
-      const uint32_t slot = atomicAdd(oversized, 1u);
-      if (olist && slot < olist_cap) olist[slot] = b;
-    }
-    return;
-  }
-  if (len == 0) return;
   const uint32_t wbase = (threadIdx.x / kWave) * ITEMS * kWave, lane = threadIdx.x & (kWave - 1);
-  uint32_t k[ITEMS];
+  auto one = [&](const uint32_t b) {
+    const uint32_t start = bstart[b], len = blen[b];
+    if (len > (uint32_t)CAP) {
+      if (threadIdx.x == 0) {
+        const uint32_t slot = atomicAdd(oversized, 1u);
+        if (olist && slot < olist_cap) olist[slot] = b;
+      }
+      return;
+    }
+    if (len == 0) return;
+    uint32_t k[ITEMS];
 #pragma unroll
-  for (int j = 0; j < ITEMS; ++j) {
-    const uint32_t i = wbase + j * kWave + lane;
-    k[j] = i < len ? load_stream(&in[(size_t)start + i]) : 0u;
+    for (int j = 0; j < ITEMS; ++j) {
+      const uint32_t i = wbase + j * kWave + lane;
+      k[j] = i < len ? load_stream(&in[(size_t)start + i]) : 0u;
+    }
+    const uint32_t sev = bucket_count_place<BLOCK, ITEMS, MODE, Op>(k, s_cw, out, start, len, lbits, bias);
+    if (sev && threadIdx.x == 0) {  // (in == out keeps the bucket for the next try)
+      if (retry_list && sev <= kRetryMax)
+        retry_list[atomicAdd(retry_n, 1u)] = b;
+      else
+        ovf_list[atomicAdd(ovf_n, 1u)] = b;
+    }
+  };
+  if constexpr (LIST) {
+    const uint32_t cnt = min(*nb, nb_cap);
+    for (uint32_t bi = blockIdx.x; bi < cnt; bi += gridDim.x) {
+      one(ilist[bi]);
+      __syncthreads();  // (the LDS of one bucket before the next one's)
+    }
+  } else {
+    if (blockIdx.x >= min(*nb, nb_cap)) return;
+    one(ilist ? ilist[blockIdx.x] : blockIdx.x);
   }
-  if (!bucket_count_place<BLOCK, ITEMS, MODE, Op>(k, s_cw, out, start, len, lbits, bias) && threadIdx.x == 0)
-    ovf_list[atomicAdd(ovf_n, 1u)] = b;  // (in == out keeps the bucket for the LSD steps)
 }
 
 // LIST: a persistent grid walks a list of buckets (ilist[0, min(*nb,
@@ -3910,7 +3936,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   // hybrid block: tiles[2] | segbase | cstart[2] | nsize | ctile0[2] | ntl | counters
   const size_t w_tiles = (size_t)TB * 4;
   const size_t rsv_words = (size_t)kRsvRanges * kRsvBlocks * rnc + 3 * (size_t)rns + 16;
-  const size_t words = 2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16 + kListCap + NB + rsv_words;
+  const size_t words =
+      2 * w_tiles + NB + 2 * (size_t)NB + NB + 2 * ((size_t)NB + 1) + NB + 16 + kListCap + NB + NB + rsv_words;
   LS_TRY(ws.ensure_hybrid(words));
   uint32_t* h = ws.hyb;
   uint4* tiles[2] = {reinterpret_cast<uint4*>(h), reinterpret_cast<uint4*>(h + w_tiles)};
@@ -3920,7 +3947,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   uint32_t* nsize = h; h += NB;
   uint32_t* ctile0[2] = {h, h + NB + 1}; h += 2 * ((size_t)NB + 1);
   uint32_t* ntl = h; h += NB;
-  uint32_t* ctr = h;  // [k] tiles of depth k, [8] buckets over the first block, [9] bucket count, [10] over the
+  uint32_t* ctr = h;  // [k] tiles of depth k (k <= 4), [7] the LSD-step list after 2-bit cells (flist2),
+                      // [8] buckets over the first block, [9] bucket count, [10] over the
                       // second, [11] largest bucket, [12] buckets over the first block (planning),
                       // [13] largest child of depth 0 (pieces), [14] reserved depth 0 overflow,
                       // [15] buckets whose counting placement overflowed
@@ -3928,6 +3956,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   uint32_t* olist = h;  // the buckets over the first block (kListCap)
   h += kListCap;
   uint32_t* flist = h;  // the buckets whose counting placement overflowed (ctr[15] of NB)
+  h += NB;
+  uint32_t* flist2 = h;  // kCnt2F: the buckets for the LSD steps (ctr[7] of NB)
   h += NB;
   // reserved depth 0: sample partials | slices (start | capacity | first tile,
   // + the tile count) | cursors | estimated digit sizes; ctr[14] = overflow
@@ -4159,22 +4189,32 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     // (k_bucket_sort CNT, `cnt` above)
     auto launch = [&](auto cnt_c) -> hipError_t {
       constexpr bool C = decltype(cnt_c)::value;
+      // 2-bit cells (256-thread blocks, lbits 16): their lightly overflowed
+      // buckets (a value with 4+ keys; ~4% of uniform 4096-key buckets) get
+      // a 3-bit retry (a persistent LIST launch over flist, count ctr[15]);
+      // heavy overflows, and the retry's, go to the LSD steps (flist2, count
+      // ctr[7]); other modes list straight for the LSD steps (flist)
+      const bool two = C && lbits == 16 && BB == 256 && cls <= 3 && bucket2_on();
+      uint32_t* const lsd_n = two ? ctr + 7 : ctr + 15;  // the LSD steps' list
+      uint32_t* const lsd_l = two ? flist2 : flist;
+      uint32_t* const rty_n = two ? ctr + 15 : nullptr;
+      uint32_t* const rty_l = two ? flist : nullptr;
 #define LS_BSX(B, I, G, NBP, CAPN, IL, OV, OL)                                                                   \
   if constexpr (C) {                                                                                             \
     const uint32_t* ci_ = reinterpret_cast<const uint32_t*>(out);                                                \
     uint32_t* co_ = reinterpret_cast<uint32_t*>(out);                                                            \
     if (lbits <= 12)                                                                                             \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCntSmall>), dim3(G), dim3(B), 0, st, ci_, co_, bstart,     \
-                         nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, ctr + 15, flist);                  \
+                         nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, lsd_n, lsd_l, rty_n, rty_l);             \
     else if (lbits != 16)                                                                                        \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt3>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize,  \
-                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, ctr + 15, flist);                         \
-    else if (B == 256 && bucket2_on())                                                                           \
+                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, lsd_n, lsd_l, rty_n, rty_l);                    \
+    else if (B == 256 && two)                                                                                    \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt2F>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize, \
-                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, ctr + 15, flist);                         \
+                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, lsd_n, lsd_l, rty_n, rty_l);                    \
     else                                                                                                         \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt3F>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize, \
-                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, ctr + 15, flist);                         \
+                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, lsd_n, lsd_l, rty_n, rty_l);                    \
   } else {                                                                                                       \
     hipLaunchKernelGGL((k_bucket_sort<BITS, B, (I), Op, K, V, FIXB>), dim3(G), dim3(B), 0, st, out, out, vout, vout, \
                        bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap);                             \
@@ -4193,9 +4233,17 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       // grid over the list (none listed: the blocks read the count and exit)
 #define LS_BSL(B, I)                                                                                               \
   if constexpr (C) {                                                                                               \
+    if (two) {                                                                                                     \
+      hipLaunchKernelGGL((k_bucket_count<256, (I), Op, kCnt3F, true>),                                             \
+                         dim3(std::min<uint32_t>(NB, (uint32_t)std::max(1, ws.num_cus) * 5)), dim3(256), 0, st,    \
+                         reinterpret_cast<const uint32_t*>(out), reinterpret_cast<uint32_t*>(out), bstart, nsize,  \
+                         ctr + 15, NB, flist, lbits, bias, ctr + 10, nullptr, 0u, ctr + 7, flist2, nullptr,        \
+                         nullptr);                                                                                 \
+      LS_TRY(hipGetLastError());                                                                                   \
+    }                                                                                                              \
     hipLaunchKernelGGL((k_bucket_sort<BITS, B, (I), Op, K, V, 0, true>),                                           \
                        dim3(std::min<uint32_t>(NB, (uint32_t)std::max(1, ws.num_cus) * 2)), dim3(B), 0, st, out,   \
-                       out, vout, vout, bstart, nsize, ctr + 15, NB, flist, lbits, bias, ctr + 14, nullptr, 0u);    \
+                       out, vout, vout, bstart, nsize, lsd_n, NB, lsd_l, lbits, bias, ctr + 14, nullptr, 0u);       \
     LS_TRY(hipGetLastError());                                                                                     \
   }
       switch (cls) {

@@ -249,11 +249,11 @@ int main(int argc, char** argv) {
   std::vector<V> vs;
   vs.push_back({"c2 prod3F 256x17", 28, 4096, [&](uint32_t m) {
     CK(hipMemsetAsync(ovn, 0, 4, st));
-    hipLaunchKernelGGL((k_bucket_count<256, 17, RadixDigit, kCnt3F>), dim3(m), dim3(256), 0, st, in, out, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u, ovn, ovl);
+    hipLaunchKernelGGL((k_bucket_count<256, 17, RadixDigit, kCnt3F>), dim3(m), dim3(256), 0, st, in, out, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u, ovn, ovl, nullptr, nullptr);
     hipLaunchKernelGGL((k_bucket_sort<4, 256, 17, RadixDigit, uint32_t, NoValue, 0, true>), dim3(512), dim3(256), 0, st, in, out, (const NoValue*)nullptr, (NoValue*)nullptr, bs, bl, ovn, m, ovl, 16u, 0u, ov, nullptr, 0u); }});
   vs.push_back({"c2 prod 256x17", 28, 4096, [&](uint32_t m) {
     CK(hipMemsetAsync(ovn, 0, 4, st));
-    hipLaunchKernelGGL((k_bucket_count<256, 17, RadixDigit, kCnt2F>), dim3(m), dim3(256), 0, st, in, out, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u, ovn, ovl);
+    hipLaunchKernelGGL((k_bucket_count<256, 17, RadixDigit, kCnt2F>), dim3(m), dim3(256), 0, st, in, out, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u, ovn, ovl, nullptr, nullptr);
     hipLaunchKernelGGL((k_bucket_sort<4, 256, 17, RadixDigit, uint32_t, NoValue, 0, true>), dim3(512), dim3(256), 0, st, in, out, (const NoValue*)nullptr, (NoValue*)nullptr, bs, bl, ovn, m, ovl, 16u, 0u, ov, nullptr, 0u); }});
   // (the overflowed buckets: the product's LSD-step kernel over the list,
   // grid 1024 over min(*ovn, 1024); the lab's uniform keys overflow ~4% of
@@ -271,7 +271,7 @@ int main(int argc, char** argv) {
   CNT3(256, 17, 4096, 2, 1) CNT3(256, 17, 4096, 2, 5)
   vs.push_back({"c3 prod 1024x17", 30, 16384, [&](uint32_t m) {
     CK(hipMemsetAsync(ovn, 0, 4, st));
-    hipLaunchKernelGGL((k_bucket_count<1024, 17, RadixDigit, kCnt3F>), dim3(m), dim3(1024), 0, st, in, out, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u, ovn, ovl);
+    hipLaunchKernelGGL((k_bucket_count<1024, 17, RadixDigit, kCnt3F>), dim3(m), dim3(1024), 0, st, in, out, bs, bl, nb, 1u << 30, nullptr, 16u, 0u, ov, nullptr, 0u, ovn, ovl, nullptr, nullptr);
     hipLaunchKernelGGL((k_bucket_sort<8, 1024, 17, RadixDigit, uint32_t, NoValue, 0, true>), dim3(512), dim3(1024), 0, st, in, out, (const NoValue*)nullptr, (NoValue*)nullptr, bs, bl, ovn, m, ovl, 16u, 0u, ov, nullptr, 0u); }});
   CNT3(1024, 17, 16384, 30, 1) CNT3(1024, 17, 16384, 30, 8) CNT3(512, 34, 16384, 30, 4)
   const char* filt = argc > 1 ? argv[1] : nullptr;

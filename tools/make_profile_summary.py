@@ -64,7 +64,7 @@ def bucketsort(row):
     over the 65536 buckets (round 4: its own kernel, k_bucket_count), not
     variants.bucket_lsd_steps' LSD steps (k_bucket_sort)."""
     name = row.get("Kernel_Name", "")
-    return "k_bucket_count<" in name and _groups(row) == 65536
+    return "k_bucket_count<256," in name and _groups(row) == 65536  # (configs[2]'s are 1024-thread blocks)
 
 
 trace = sorted(glob.glob(str(src / "stats" / "**" / "*kernel_trace.csv"), recursive=True))
