@@ -4190,10 +4190,12 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     auto launch = [&](auto cnt_c) -> hipError_t {
       constexpr bool C = decltype(cnt_c)::value;
       // 2-bit cells (256-thread blocks, lbits 16): their lightly overflowed
-      // buckets (a value with 4+ keys; ~4% of uniform 4096-key buckets) get
-      // a 3-bit retry (a persistent LIST launch over flist, count ctr[15]);
-      // heavy overflows, and the retry's, go to the LSD steps (flist2, count
-      // ctr[7]); other modes list straight for the LSD steps (flist)
+      // buckets (a value with 4+ keys; ~4% of uniform 4096-key buckets) and
+      // the buckets over the first block get a 3-bit retry in blocks of the
+      // second size (a persistent LIST launch over flist, count ctr[15]: no
+      // separate second-size launch); heavy overflows, and the retry's, go
+      // to the LSD steps (flist2, count ctr[7]); other modes list straight
+      // for the LSD steps (flist)
       const bool two = C && lbits == 16 && BB == 256 && cls <= 3 && bucket2_on();
       uint32_t* const lsd_n = two ? ctr + 7 : ctr + 15;  // the LSD steps' list
       uint32_t* const lsd_l = two ? flist2 : flist;
@@ -4203,28 +4205,34 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   if constexpr (C) {                                                                                             \
     const uint32_t* ci_ = reinterpret_cast<const uint32_t*>(out);                                                \
     uint32_t* co_ = reinterpret_cast<uint32_t*>(out);                                                            \
+    const uint32_t ocap_ = (OL) == flist ? NB : kListCap;                                                        \
     if (lbits <= 12)                                                                                             \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCntSmall>), dim3(G), dim3(B), 0, st, ci_, co_, bstart,     \
-                         nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, lsd_n, lsd_l, rty_n, rty_l);             \
+                         nsize, NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l);             \
     else if (lbits != 16)                                                                                        \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt3>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize,  \
-                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, lsd_n, lsd_l, rty_n, rty_l);                    \
+                         NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l);                    \
     else if (B == 256 && two)                                                                                    \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt2F>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize, \
-                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, lsd_n, lsd_l, rty_n, rty_l);                    \
+                         NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l);                    \
     else                                                                                                         \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt3F>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize, \
-                         NBP, CAPN, IL, lbits, bias, OV, OL, kListCap, lsd_n, lsd_l, rty_n, rty_l);                    \
+                         NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l);                    \
   } else {                                                                                                       \
     hipLaunchKernelGGL((k_bucket_sort<BITS, B, (I), Op, K, V, FIXB>), dim3(G), dim3(B), 0, st, out, out, vout, vout, \
                        bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap);                             \
   }
 #define LS_BS(I, G, NBP, CAPN, IL, OV, OL) LS_BSX(BB, ((I) * 256 + BB - 1) / BB, G, NBP, CAPN, IL, OV, OL)
-#define LS_BS2(I)                                          \
-  LS_BS(I, NB, ctr + 9, NB, nullptr, ctr + 8, olist);      \
-  LS_TRY(hipGetLastError());                               \
-  if (n2) {                                                \
-    LS_BS(I + 6, n2, ctr + 8, kListCap, olist, ctr + 10, nullptr); \
+#define LS_BS2(I)                                                   \
+  if (two) {                                                        \
+    /* the buckets over the first block join the retry list */      \
+    LS_BS(I, NB, ctr + 9, NB, nullptr, ctr + 15, flist);            \
+  } else {                                                          \
+    LS_BS(I, NB, ctr + 9, NB, nullptr, ctr + 8, olist);             \
+    LS_TRY(hipGetLastError());                                      \
+    if (n2) {                                                       \
+      LS_BS(I + 6, n2, ctr + 8, kListCap, olist, ctr + 10, nullptr); \
+    }                                                               \
   }
 #define LS_BS512(I, G, NBP, CAPN, IL, OV, OL) LS_BSX(512, I, G, NBP, CAPN, IL, OV, OL)
 #define LS_BS1024(I, G, NBP, CAPN, IL, OV, OL) LS_BSX(1024, I, G, NBP, CAPN, IL, OV, OL)
