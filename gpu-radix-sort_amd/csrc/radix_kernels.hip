@@ -1585,7 +1585,11 @@ __device__ __forceinline__ uint32_t field3_sum(uint64_t w) {
 constexpr int kCntSmall = 0, kCnt3 = 1, kCnt3F = 2, kCnt2F = 3;
 template <int CAP, int MODE>
 constexpr int cnt_lds_words() {  // u64 words: the cell words (and starts), or the keys placed over them
-  constexpr int cells = MODE == kCnt2F ? 4 * kCntCells + 2 * kCntCells : 8 * kCntCells;
+  // (bytes: 2-bit cells + u16 starts 24 KB; u32 counters (kCntSmall) 16 KB,
+  // so the bucket's keys set the size there: ~17 KB, 8+ blocks per CU; 3-bit
+  // cells 32 KB)
+  constexpr int cells = MODE == kCnt2F ? 4 * kCntCells + 2 * kCntCells : MODE == kCntSmall ? 4 * kCntCells
+                                                                                        : 8 * kCntCells;
   return (cells > 4 * CAP ? cells : 4 * CAP + 7) / 8;
 }
 // Exclusive block scan whose wave sums live in `s` (any LDS words the
@@ -1629,6 +1633,7 @@ __device__ __forceinline__ uint32_t bucket_count_place(const uint32_t (&k)[ITEMS
   auto valid = [&](int j) { return wbase + j * kWave + lane < len; };
 
   uint32_t rk[ITEMS];
+  uint32_t rkp[(ITEMS + 1) / 2];  // kCntSmall: packed 16-bit ranks / positions
   if constexpr (MODE == kCnt2F) {
     // (24 KB of cells and starts: six blocks per CU with room for the flag
     // and the wave sums of their own)
@@ -1725,36 +1730,42 @@ __device__ __forceinline__ uint32_t bucket_count_place(const uint32_t (&k)[ITEMS
   } else {
     // lbits <= 12: one value per cell, u32 counters (an atomic's return is
     // the key's rank among its equals: no overflow)
+    // (ranks and positions < CAP < 2^16: two per register, so the kernel
+    // fits 72 VGPRs and seven blocks per CU)
     uint32_t* const s_cnt = s_keys;
 #pragma unroll
     for (int q = 0; q < PER; ++q) s_cnt[q * BLOCK + tid] = 0u;
+#pragma unroll
+    for (int q = 0; q < (ITEMS + 1) / 2; ++q) rkp[q] = 0u;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j)
-      if (valid(j)) rk[j] = atomicAdd(&s_cnt[ci(val(k[j]))], 1u);
+      if (valid(j)) rkp[j >> 1] |= atomicAdd(&s_cnt[ci(val(k[j]))], 1u) << (16 * (j & 1));
     __syncthreads();
-    uint32_t c[PER], sum = 0;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) sum += s_cnt[q * BLOCK + tid];
+    // (the wave sums in 64 B of their own, so the counters stay in LDS and
+    // are read again below instead of held in registers: fewer VGPRs, more
+    // blocks per CU -- the multi-GPU round sorts' buckets take this path)
+    __shared__ uint32_t s_wsS[BLOCK / kWave];
+    uint32_t total;
+    uint32_t run = block_exclusive_scan<BLOCK>(sum, s_wsS, total);
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-      c[q] = s_cnt[q * BLOCK + tid];
-      sum += c[q];
-    }
-    __syncthreads();
-    uint32_t run = block_exclusive_scan_in<BLOCK>(sum, s_cnt);
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
+      const uint32_t c = s_cnt[q * BLOCK + tid];
       s_cnt[q * BLOCK + tid] = run;
-      run += c[q];
+      run += c;
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j)
-      if (valid(j)) rk[j] += s_cnt[ci(val(k[j]))];
+      if (valid(j)) rkp[j >> 1] += s_cnt[ci(val(k[j]))] << (16 * (j & 1));
   }
   __syncthreads();  // the keys take the words' place
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j)
-    if (valid(j)) s_keys[rk[j]] = k[j];
+    if (valid(j)) s_keys[MODE == kCntSmall ? (rkp[j >> 1] >> (16 * (j & 1))) & 0xFFFFu : rk[j]] = k[j];
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
@@ -1780,7 +1791,9 @@ __device__ __forceinline__ uint32_t bucket_count_place(const uint32_t (&k)[ITEMS
 constexpr uint32_t kRetryMax = 16;
 template <int BLOCK, int ITEMS, typename Op, int MODE, bool LIST = false>
 __global__ __launch_bounds__(BLOCK)
-__attribute__((amdgpu_waves_per_eu(BLOCK >= 1024 && ITEMS <= 17 && MODE != kCntSmall ? 8 : 1, 8)))
+__attribute__((amdgpu_waves_per_eu(
+    BLOCK >= 1024 && ITEMS <= 17 && MODE != kCntSmall ? 8 : (BLOCK == 256 && ITEMS <= 17 && MODE == kCntSmall) ? 7 : 1,
+    8)))
 void k_bucket_count(const uint32_t* in, uint32_t* out, const uint32_t* __restrict__ bstart,
                     const uint32_t* __restrict__ blen, const uint32_t* __restrict__ nb, uint32_t nb_cap,
                     const uint32_t* __restrict__ ilist, uint32_t lbits, uint32_t bias,
