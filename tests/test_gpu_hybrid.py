@@ -663,3 +663,45 @@ def test_counting_bucket_duplicates_full_size(dev, oracle_mod, bits, four):
     assert t_dup < 3.0 * t_uni, (t_dup, t_uni)
     del x, xm, ref, out, tmp
     torch.cuda.empty_cache()
+
+
+def test_counting_bucket_overflow_classes(dev, oracle_mod, bits):
+    """One 2^27-key sort whose buckets take every route of the counting
+    placement at once: uniform buckets (2-bit cells; the ~4% with a value of
+    4+ keys retry with 3-bit cells), buckets given one value of 6 keys (a
+    light overflow: the 3-bit retry), buckets made of 2 values (heavy: straight
+    to the LSD-step list), and buckets over the first block (~3.2K keys where
+    the mean is 2048: they join the retry list at the second size).  Exact
+    against the oracle."""
+    n = (1 << 27) + 77
+    rng = np.random.default_rng(27)
+    import oracle.oracle as o
+    x = o.pcg(n, first=27)
+    nb = 1 << 16
+    pos = rng.permutation(n)
+    cur = 0
+
+    def take(k):
+        nonlocal cur
+        p = pos[cur:cur + k]
+        cur += k
+        return p
+    pref = rng.permutation(nb).astype(np.uint32)
+    # light: 6 keys of one value in each of 1500 buckets
+    for b in pref[:1500]:
+        x[take(6)] = (b << 16) | np.uint32(rng.integers(0, 1 << 16))
+    # heavy: 2000 keys of 2 values in each of 40 buckets (their own keys
+    # spread over random buckets)
+    for b in pref[1500:1540]:
+        own = np.nonzero((x >> 16) == b)[0]
+        x[own] = (x[own] & np.uint32(0xFFFF)) | (rng.integers(0, nb, own.size).astype(np.uint32) << 16)
+        v = (b << 16) | np.uint32(rng.integers(0, 1 << 16))
+        x[take(2000)] = np.where(rng.random(2000) < 0.5, v, v ^ np.uint32(1)).astype(np.uint32)
+    # over the first block (2304 keys at this size; the second holds 3840):
+    # 1200 more keys in each of 3 buckets
+    for b in pref[1540:1543]:
+        x[take(1200)] = (b << 16) | rng.integers(0, 1 << 16, 1200).astype(np.uint32)
+    t = _tensor(x)
+    out, nbs, npass = _sort_counting(dev, t)
+    assert nbs == 1 and npass == 16 // bits
+    np.testing.assert_array_equal(_u32(out), oracle_mod.sort_u32(x))
