@@ -574,8 +574,12 @@ bool range_digit(Ctx& c, const std::vector<const K*>& in, const std::vector<uint
     lo = std::min<uint64_t>(lo, mm[0]);
     hi = std::max<uint64_t>(hi, mm[1]);
   }
-  pd.range = true;
-  *useful = dplan::range_digit(lo, hi, 8 * (int)sizeof(K), &pd.bias, &pd.shift);
+  // pd changes only when the range digit is used: a rejected one leaves the
+  // top-digit partition's PartDigit for the rounds that follow
+  PartDigit rd;
+  rd.range = true;
+  *useful = dplan::range_digit(lo, hi, 8 * (int)sizeof(K), &rd.bias, &rd.shift);
+  if (*useful) pd = rd;
   return true;
 }
 

@@ -17,8 +17,14 @@ test_maximum_size, test_config5_pairs_size), computed with the oracle here
                 element n of the stream) and of the 8-GPU per-rank shape
                 (2^29 keys >> 3, test_gpu_distrib_abi.test_shape8_2pow29).
 
+  2^32:         the sorted hash of the first 2^32 keys of the stream, i.e.
+                configs[3]'s global input (rank r holds elements [r*2^29,
+                (r+1)*2^29)): the concatenated output shards of the 8-rank
+                engine (test_gpu_distrib_full.test_config3_full_8ranks).
+
 Run: python tests/golden/make_big_golden.py          (everything)
      python tests/golden/make_big_golden.py 2pow29   (adds the 2^29 class)
+     python tests/golden/make_big_golden.py 2pow32   (adds the 2^32 stream)
 """
 import hashlib
 import json
@@ -82,8 +88,23 @@ def add_2pow29():
     path.write_text(json.dumps(out, indent=1) + "\n")
 
 
+def add_2pow32():
+    path = ROOT / "tests" / "golden" / "big_golden.json"
+    out = json.loads(path.read_text())
+    gold = json.loads((ROOT / "tests" / "golden" / "pcg_golden.json").read_text())["sha256_prefix"]
+    h = oracle.sorted_pcg_sha256(1 << 20)  # the pin first
+    assert h[:16] == gold[str(1 << 20)]["sorted"], h
+    n = 1 << 32
+    t = time.time()
+    out["sorted_u32"][str(n)] = oracle.sorted_pcg_sha256(n)
+    print(n, out["sorted_u32"][str(n)], "%.0f s" % (time.time() - t), flush=True)
+    path.write_text(json.dumps(out, indent=1) + "\n")
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["2pow29"]:
         add_2pow29()
+    elif sys.argv[1:] == ["2pow32"]:
+        add_2pow32()
     else:
         main()

@@ -84,6 +84,25 @@ def test_provided_cpu_is_std_sort(oracle_mod):
     np.testing.assert_array_equal(y, np.sort(x))
 
 
+def test_config0_provided_cpu_pinned(golden):
+    """configs[0] exactly (1M uint32 keys through the
+    reference's CPU local sort): in a fresh process, the library's own
+    populateInput (utils.cu:65-80) fills 2^20 keys and providedCpu
+    (invokers.cu:68-71) sorts them; the sha256 prefixes of input and output
+    equal the ones the reference itself produced (pcg_golden.json, 1048576)."""
+    g, _ = golden
+    code = ("import sys, ctypes, hashlib; sys.path[:0]=[%r]; import pylibsort, numpy as np; "
+            "L=pylibsort.lib(); x=np.empty(1<<20, dtype=np.uint32); "
+            "L.populateInput(x.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.c_size_t(x.size)); "
+            "a=hashlib.sha256(x.tobytes()).hexdigest()[:16]; "
+            "assert L.providedCpu(x.ctypes.data_as(ctypes.POINTER(ctypes.c_uint)), ctypes.c_size_t(x.size)) == 1; "
+            "print(a, hashlib.sha256(x.tobytes()).hexdigest()[:16])" % str(ROOT / "gpu-radix-sort_amd"))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True).stdout.split()
+    want = g["sha256_prefix"][str(1 << 20)]
+    assert out == [want["input"], want["sorted"]], (out, want)
+    assert want["sorted"] == "cfe37c8a9aed0838"
+
+
 def test_gpu_entry_points_fail_loudly_without_device(capfd):
     import pylibsort
     if pylibsort.gpu_ready():
