@@ -31,6 +31,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstring>
+#include <thread>
 #include <type_traits>
 
 namespace lsort {
@@ -2258,17 +2259,37 @@ constexpr int kRsvRanges = 8;
 constexpr uint32_t kHybSeqWord = 511;
 constexpr uint32_t kHybSeqWord2 = 510;  // k_hyb_children's, after the bucket stats
 
-// Waits until the pinned word *w == v (a kernel's system-scope store).  After
-// ~1 s of polling (a stream with much queued ahead) it synchronises the
-// stream instead, after which the word must hold v.
+// Waits until the pinned word *w == v (a kernel's system-scope store): a
+// pause spin for the first ~100 us (the usual wait: the word arrives while the
+// last queued kernel runs, and the host must see it at once to keep the GPU
+// fed), then yields the core between polls, then (after 20 ms: a stream with
+// much queued ahead, e.g. a round sort behind an exchange) sleeps 50 us per
+// poll.  After LIBSORT_HOST_WAIT_MS (default 1000 ms) it synchronises the
+// stream instead, after which the word must hold v (ADVICE r04;
+// test_gpu_parity.py::test_host_word_wait_fallback forces this branch).
+inline int host_wait_limit_ms() {
+  static const int ms = [] {
+    const char* e = getenv("LIBSORT_HOST_WAIT_MS");
+    return e && *e ? std::max(0, atoi(e)) : 1000;
+  }();
+  return ms;
+}
 inline hipError_t wait_host_word(const uint32_t* w, uint32_t v, hipStream_t st) {
   const volatile uint32_t* p = w;
   const auto t0 = std::chrono::steady_clock::now();
+  const auto limit = std::chrono::milliseconds(host_wait_limit_ms());
   for (uint32_t i = 1; *p != v; ++i) {
-    if ((i & 4095u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
-      const hipError_t e = hipStreamSynchronize(st);
-      if (e != hipSuccess) return e;
-      return *p == v ? hipSuccess : hipErrorUnknown;
+    if ((i & 255u) == 0) {
+      const auto dt = std::chrono::steady_clock::now() - t0;
+      if (dt >= limit) {
+        const hipError_t e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return e;
+        return *p == v ? hipSuccess : hipErrorUnknown;
+      }
+      if (dt > std::chrono::milliseconds(20))
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      else if (dt > std::chrono::microseconds(100))
+        std::this_thread::yield();
     }
     __builtin_ia32_pause();
   }
@@ -2633,6 +2654,10 @@ __global__ __launch_bounds__(256) void k_rsv_tiles(const uint32_t* __restrict__ 
   // nc children (segments x RADIX digits), NS = nc * 8 slices; thread tid
   // holds slices [tid * SPT, (tid + 1) * SPT)
   constexpr uint32_t kMaxSpt = kRsvMaxSlices / 256;
+  // ~65.6 KB of static LDS (4 x 4097 words + s_wsum): gfx950 gives a
+  // workgroup 160 KB; gfx942 and older (64 KB) could not launch this kernel,
+  // and this library is built for gfx950 only (Makefile ARCH)
+  static_assert((4 * kRsvMaxSlices + 2) * 4 + 32 <= 160 * 1024, "k_rsv_tiles: LDS beyond gfx950's 160 KB");
   __shared__ uint32_t s_row0[kRsvMaxSlices + 1];  // first count row per slice (capacity), [NS] = rows
   __shared__ uint32_t s_a0[kRsvMaxSlices + 1];    // first listed tile per slice, [NS] = tiles
   __shared__ uint32_t s_keys[kRsvMaxSlices];
@@ -4489,14 +4514,22 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
     HybPieces pc{dev32, K, nseg, tile, depths, (double)npop / nseg, dev32 + (pcum - h32)};
     bool handled = false;
     NoValue* nv = nullptr;
+    hipError_t e;
     if (bias && digit_bits == 4)
-      LS_TRY((sort_hybrid<4, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, bias, st, &handled, 0, &pc)));
+      e = sort_hybrid<4, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, bias, st, &handled, 0, &pc);
     else if (bias)
-      LS_TRY((sort_hybrid<8, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, bias, st, &handled, 0, &pc)));
+      e = sort_hybrid<8, BiasedDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, bias, st, &handled, 0, &pc);
     else if (digit_bits == 4)
-      LS_TRY((sort_hybrid<4, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, 0u, st, &handled, 0, &pc)));
+      e = sort_hybrid<4, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, 0u, st, &handled, 0, &pc);
     else
-      LS_TRY((sort_hybrid<8, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, 0u, st, &handled, 0, &pc)));
+      e = sort_hybrid<8, RadixDigit>(ws, in, out, tmp, nv, nv, nv, n, bits, 0u, st, &handled, 0, &pc);
+    if (e != hipSuccess) {
+      // a failure may come before the sequence-word wait: guard the staging
+      // with the event after all, so the next call's
+      // hipEventSynchronize(seg_evt) covers this call's upload
+      (void)hipEventRecord(ws.seg_evt, st);
+      return e;
+    }
     if (handled) {
       ws.last_algo = 4;
       return hipSuccess;

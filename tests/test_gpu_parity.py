@@ -710,3 +710,43 @@ def test_merge_u32(dev, na, nb):
     tb = torch.from_numpy(b.view(np.int32)).cuda()
     out = D.merge_u32(ta, tb)
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), np.sort(np.concatenate([a, b])))
+
+
+def test_host_word_wait_fallback(oracle_mod):
+    """The hybrid's host waits (wait_host_word, radix_kernels.hip) poll a
+    pinned word a kernel raises; past LIBSORT_HOST_WAIT_MS they synchronise
+    the stream and re-check instead.  With the limit at 0 every
+    wait longer than a few hundred polls takes that branch; a full sort (the
+    hybrid: sampler + bucket-stat words) and a piece sort (the multi-GPU
+    rounds' entry point) are queued behind a 2^28-key sort so their words
+    arrive late.  Fresh process; exact against the oracle."""
+    import os
+    import pathlib
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    root = pathlib.Path(__file__).resolve().parents[1]
+    code = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [%r, %r]
+import pylibsort.device as D
+from oracle import oracle
+big = D.populate_u32(1 << 28)
+x = oracle.pcg((1 << 27) + 4097, first=11)
+t = torch.from_numpy(x.view(np.int32)).cuda()
+o1 = D.sort_keys_u32(big)      # queued ahead: the next sorts' words arrive late
+o2 = D.sort_keys_u32(t)
+xs = x[np.argsort(x >> np.uint32(24), kind="stable")]  # pieces: the keys grouped by top digit
+cnt = np.bincount(x >> np.uint32(24), minlength=256).astype(np.uint64)
+off = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint64)
+o3 = D.sort_pieces_u32(torch.from_numpy(xs.view(np.int32)).cuda(), off, cnt, np.arange(256, dtype=np.uint32), 256, 24)
+torch.cuda.synchronize()
+want = oracle.sort_u32(x)
+assert np.array_equal(o2.cpu().numpy().view(np.uint32), want), "full sort"
+assert np.array_equal(o3.cpu().numpy().view(np.uint32), want), "piece sort"
+print("OK")
+""" % (str(root), str(root / "gpu-radix-sort_amd"))
+    env = dict(os.environ, LIBSORT_HOST_WAIT_MS="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
