@@ -1008,6 +1008,115 @@ LS_BOOL_ENTRY(libsortPartitionLutScatterU64U32, const uint64_t* d_kin, const uin
              : 0;
 }
 
+// The range-digit partitions (distrib.cpp's re-partition of narrow key
+// ranges, exported for pylibsort.distrib): the table partitions' kernels
+// with a BiasedDigit op.
+static bool range_shift_ok(uint32_t shift, int key_bits, const char* who) {
+  if ((int)shift > key_bits - 8) {
+    set_error(std::string(who) + ": shift must be <= key bits - 8");
+    return false;
+  }
+  return true;
+}
+
+LS_BOOL_ENTRY(libsortPartitionRangeCountU32, const uint32_t* d_in, size_t n, uint32_t bias, uint32_t shift,
+              uint32_t* d_bounds, void* stream) {
+  if (!range_shift_ok(shift, 32, "libsortPartitionRangeCountU32")) return 0;
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(partition_range_u32(ws, d_in, nullptr, n, bias, (int)shift, d_bounds, st, kPartCount),
+                         "libsortPartitionRangeCountU32");
+         })
+             ? 1
+             : 0;
+}
+
+LS_BOOL_ENTRY(libsortPartitionRangeScatterU32, const uint32_t* d_in, uint32_t* d_out, size_t n, uint32_t bias,
+              uint32_t shift, void* stream) {
+  if (!range_shift_ok(shift, 32, "libsortPartitionRangeScatterU32")) return 0;
+  if (n > 0 && (const uint32_t*)d_out == d_in) {
+    set_error("libsortPartitionRangeScatterU32: out of place only");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(partition_range_u32(ws, d_in, d_out, n, bias, (int)shift, nullptr, st, kPartScatter),
+                         "libsortPartitionRangeScatterU32 (needs the matching count call just before it)");
+         })
+             ? 1
+             : 0;
+}
+
+LS_BOOL_ENTRY(libsortPartitionRangeCountU64U32, const uint64_t* d_kin, const uint32_t* d_vin, size_t n,
+              uint64_t bias, uint32_t shift, uint32_t* d_bounds, void* stream) {
+  if (!range_shift_ok(shift, 64, "libsortPartitionRangeCountU64U32")) return 0;
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(partition_range_pairs_u64_u32(ws, d_kin, d_vin, nullptr, nullptr, n, bias, (int)shift,
+                                                       d_bounds, st, kPartCount),
+                         "libsortPartitionRangeCountU64U32");
+         })
+             ? 1
+             : 0;
+}
+
+LS_BOOL_ENTRY(libsortPartitionRangeScatterU64U32, const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
+              uint32_t* d_vout, size_t n, uint64_t bias, uint32_t shift, void* stream) {
+  if (!range_shift_ok(shift, 64, "libsortPartitionRangeScatterU64U32")) return 0;
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(partition_range_pairs_u64_u32(ws, d_kin, d_vin, d_kout, d_vout, n, bias, (int)shift, nullptr,
+                                                       st, kPartScatter),
+                         "libsortPartitionRangeScatterU64U32 (needs the matching count call just before it)");
+         })
+             ? 1
+             : 0;
+}
+
+LS_BOOL_ENTRY(libsortMinMaxU32, const uint32_t* d_keys, size_t n, uint32_t* d_minmax, void* stream) {
+  if (!d_minmax || (n > 0 && !d_keys)) {
+    set_error("libsortMinMaxU32: bad arguments");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(minmax_u32(ws, d_keys, n, d_minmax, st), "libsortMinMaxU32");
+         })
+             ? 1
+             : 0;
+}
+
+LS_BOOL_ENTRY(libsortMinMaxU64, const uint64_t* d_keys, size_t n, uint64_t* d_minmax, void* stream) {
+  if (!d_minmax || (n > 0 && !d_keys)) {
+    set_error("libsortMinMaxU64: bad arguments");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(minmax_u64(ws, d_keys, n, d_minmax, st), "libsortMinMaxU64");
+         })
+             ? 1
+             : 0;
+}
+
+LS_BOOL_ENTRY(libsortSortPiecesRangeU32, const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp, size_t n,
+              const uint64_t* off, const uint64_t* len, const uint32_t* seg, size_t npieces, uint32_t nseg,
+              uint32_t bits, uint32_t bias, void* stream) {
+  if (n > 0 && (!d_in || !d_out || !d_tmp || d_out == d_in || d_tmp == d_out || (const uint32_t*)d_tmp == d_in ||
+                !off || !len || !seg)) {
+    set_error("libsortSortPiecesRangeU32: need d_in, d_out, d_tmp distinct and the three piece tables");
+    return 0;
+  }
+  hipStream_t st = as_stream(stream);
+  return with_current_ws(st, [&](Workspace& ws) {
+           return hip_ok(sort_pieces_u32(ws, d_in, d_out, d_tmp, n, off, len, seg, npieces, nseg, (int)bits,
+                                         g_digit_bits.load(), st, bias),
+                         "libsortSortPiecesRangeU32 (pieces in segment order, seg < nseg, lengths summing to n)");
+         })
+             ? 1
+             : 0;
+}
+
 LS_BOOL_ENTRY(libsortSegmentCopyU32, const uint32_t* d_src, uint32_t* d_dst, size_t nseg,
                                          const uint64_t* src_off, const uint64_t* dst_off,
                                          const uint64_t* len, void* stream) {
@@ -1101,6 +1210,18 @@ LS_BOOL_ENTRY(libsortDistribPlanDigits, const int64_t* counts, uint32_t nranks, 
     }
   dplan::plan_digit_rounds(C, (int)rounds, growth, lut, est);
   return 1;
+}
+
+LS_BOOL_ENTRY(libsortDistribRangeDigit, uint64_t lo, uint64_t hi, uint32_t key_bits, uint64_t* bias,
+              uint32_t* shift) {
+  if (!bias || !shift || (key_bits != 32 && key_bits != 64)) {
+    set_error("libsortDistribRangeDigit: need bias, shift and key_bits 32 or 64");
+    return 0;
+  }
+  int sh = 0;
+  const bool useful = dplan::range_digit(lo, hi, (int)key_bits, bias, &sh);
+  *shift = (uint32_t)sh;
+  return useful ? 1 : 0;
 }
 
 LS_BOOL_ENTRY(gpuDistribSort, uint32_t* h_in, size_t len, int ngpu) {

@@ -73,6 +73,19 @@ _SIGS = [
      [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
     ("libsortPartitionLutScatterU64U32", ctypes.c_int,
      [_vp, _vp, _vp, _vp, ctypes.c_size_t, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp]),
+    ("libsortPartitionRangeCountU32", ctypes.c_int,
+     [_vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp, _vp]),
+    ("libsortPartitionRangeScatterU32", ctypes.c_int,
+     [_vp, _vp, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _vp]),
+    ("libsortPartitionRangeCountU64U32", ctypes.c_int,
+     [_vp, _vp, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32, _vp, _vp]),
+    ("libsortPartitionRangeScatterU64U32", ctypes.c_int,
+     [_vp, _vp, _vp, _vp, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint32, _vp]),
+    ("libsortMinMaxU32", ctypes.c_int, [_vp, ctypes.c_size_t, _vp, _vp]),
+    ("libsortMinMaxU64", ctypes.c_int, [_vp, ctypes.c_size_t, _vp, _vp]),
+    ("libsortSortPiecesRangeU32", ctypes.c_int,
+     [_vp, _vp, _vp, ctypes.c_size_t, _u64p, _u64p, _u32p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.c_uint32, _vp]),
     ("libsortSegmentCopyU32", ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _u64p, _u64p, _u64p, _vp]),
     ("libsortDeltaMaxGapU32", ctypes.c_int, [_vp, ctypes.c_size_t, _vp, _vp]),
     ("libsortDeltaPackU32", ctypes.c_int, [_vp, ctypes.c_size_t, _vp, _vp, _vp]),
@@ -84,6 +97,8 @@ _SIGS = [
      [ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32]),
     ("libsortDistribPlanDigits", ctypes.c_int,
      [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, _vp, _vp]),
+    ("libsortDistribRangeDigit", ctypes.c_int,
+     [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, _u64p, _u32p]),
     ("libsortPopulateDevice", ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_uint64, _vp]),
     ("libsortSetDigitBits", ctypes.c_int, [ctypes.c_int]),
     ("libsortGetDigitBits", ctypes.c_int, []),

@@ -78,12 +78,13 @@ def sort_keys_range_u32(keys, lo, hi, out=None, tmp=None):
     return out
 
 
-def sort_pieces_u32(keys, off, lens, segs, nseg, bits, out=None, tmp=None):
+def sort_pieces_u32(keys, off, lens, segs, nseg, bits, out=None, tmp=None, bias=None):
     """Sort of pre-partitioned uint32 keys (libsortSortPiecesU32): piece p =
     keys[off[p] : off[p] + lens[p]] of segment segs[p] (host arrays, pieces in
     non-decreasing segment order); every key of segment s shares its bits
     [bits, 32), increasing with s.  Returns `out` holding the sum(lens) keys
-    sorted (out and tmp distinct from keys)."""
+    sorted (out and tmp distinct from keys).  bias (range-digit pieces,
+    libsortSortPiecesRangeU32): the shared bits are those of key - bias."""
     _need(keys, _U32, "keys")
     o = np.ascontiguousarray(off, dtype=np.uint64)
     ln = np.ascontiguousarray(lens, dtype=np.uint64)
@@ -100,9 +101,14 @@ def sort_pieces_u32(keys, off, lens, segs, nseg, bits, out=None, tmp=None):
     if out.numel() < n or tmp.numel() < n:
         raise ValueError("out / tmp smaller than the pieces")
     p64 = ctypes.POINTER(ctypes.c_uint64)
-    _check(_lib().libsortSortPiecesU32(_ptr(keys), _ptr(out), _ptr(tmp), n, o.ctypes.data_as(p64),
-                                       ln.ctypes.data_as(p64), sg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
-                                       o.size, int(nseg), int(bits), _stream()), "libsortSortPiecesU32")
+    tabs = (o.ctypes.data_as(p64), ln.ctypes.data_as(p64), sg.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    if bias is None:
+        _check(_lib().libsortSortPiecesU32(_ptr(keys), _ptr(out), _ptr(tmp), n, *tabs, o.size, int(nseg), int(bits),
+                                           _stream()), "libsortSortPiecesU32")
+    else:
+        _check(_lib().libsortSortPiecesRangeU32(_ptr(keys), _ptr(out), _ptr(tmp), n, *tabs, o.size, int(nseg),
+                                                int(bits), int(bias) & 0xFFFFFFFF, _stream()),
+               "libsortSortPiecesRangeU32")
     return out
 
 
@@ -284,6 +290,63 @@ def partition_lut_pairs_scatter_u64_u32(keys, vals, lut, lut_shift, nbuckets, ou
                                                    _ptr(lut), lut_shift, nbuckets, _stream()),
            "libsortPartitionLutScatterU64U32")
     return ok_, ov
+
+
+def partition_range_count_u32(keys, bias, shift, bounds=None):
+    """Count half of the range-digit partition (digit = (key - bias) >> shift,
+    256 buckets): the bucket starts (int32 tensor) while nothing has moved.
+    partition_range_scatter_u32 with the same arguments must follow."""
+    _need(keys, _U32, "keys")
+    bounds = torch.empty(256, dtype=torch.int32, device=keys.device) if bounds is None else bounds
+    _check(_lib().libsortPartitionRangeCountU32(_ptr(keys), keys.numel(), int(bias) & 0xFFFFFFFF, int(shift),
+                                                _ptr(bounds), _stream()), "libsortPartitionRangeCountU32")
+    return bounds
+
+
+def partition_range_scatter_u32(keys, bias, shift, out=None):
+    _need(keys, _U32, "keys")
+    out = torch.empty_like(keys) if out is None else out
+    _need(out, _U32, "out")
+    _check(_lib().libsortPartitionRangeScatterU32(_ptr(keys), _ptr(out), keys.numel(), int(bias) & 0xFFFFFFFF,
+                                                  int(shift), _stream()), "libsortPartitionRangeScatterU32")
+    return out
+
+
+def partition_range_pairs_count_u64_u32(keys, vals, bias, shift, bounds=None):
+    _need(keys, _U64, "keys")
+    _need(vals, _U32, "vals")
+    bounds = torch.empty(256, dtype=torch.int32, device=keys.device) if bounds is None else bounds
+    _check(_lib().libsortPartitionRangeCountU64U32(_ptr(keys), _ptr(vals), keys.numel(), int(bias), int(shift),
+                                                   _ptr(bounds), _stream()), "libsortPartitionRangeCountU64U32")
+    return bounds
+
+
+def partition_range_pairs_scatter_u64_u32(keys, vals, bias, shift, out_keys=None, out_vals=None):
+    _need(keys, _U64, "keys")
+    _need(vals, _U32, "vals")
+    ok_ = torch.empty_like(keys) if out_keys is None else out_keys
+    ov = torch.empty_like(vals) if out_vals is None else out_vals
+    _check(_lib().libsortPartitionRangeScatterU64U32(_ptr(keys), _ptr(vals), _ptr(ok_), _ptr(ov), keys.numel(),
+                                                     int(bias), int(shift), _stream()),
+           "libsortPartitionRangeScatterU64U32")
+    return ok_, ov
+
+
+def minmax_u32(keys, out=None):
+    """(smallest, largest) key as a 2-element int32 tensor holding uint32 bits
+    (n == 0: 0xFFFFFFFF, 0)."""
+    _need(keys, _U32, "keys")
+    out = torch.empty(2, dtype=torch.int32, device=keys.device) if out is None else out
+    _check(_lib().libsortMinMaxU32(_ptr(keys), keys.numel(), _ptr(out), _stream()), "libsortMinMaxU32")
+    return out
+
+
+def minmax_u64(keys, out=None):
+    """(smallest, largest) uint64 key as a 2-element int64 tensor of the bits."""
+    _need(keys, _U64, "keys")
+    out = torch.empty(2, dtype=torch.int64, device=keys.device) if out is None else out
+    _check(_lib().libsortMinMaxU64(_ptr(keys), keys.numel(), _ptr(out), _stream()), "libsortMinMaxU64")
+    return out
 
 
 def segment_copy_u32(src, dst, src_off, dst_off, lens):

@@ -32,6 +32,14 @@ of the globally sorted array, S = ceil(N/R), the reference's equal re-cut):
          piece and sends it gap-coded; the receiver decodes and merges (for
          link-bound world sizes: the bench default at 2 GPUs).
 
+Narrow key ranges (both top-digit schedules and the pair rounds, as the C
+engine, csrc/distrib.cpp): when the top-digit plan is too skewed (IDs,
+timestamps, keys below 2^26 at 8 ranks fill a few of the 256 top digits), the
+rounds re-partition by the 8-bit RANGE digit (key - min) >> shift over the
+populated key range (libsortDistribRangeDigit: the C engine's own rule, min
+and max all-gathered from libsortMinMax*) and run the same plan; only keys
+that stay skewed (one distinct value) take the LSD rounds.
+
 The local operations come from an `ops` backend.  The product backend is
 HipOps (libsort's HIP kernels on torch CUDA tensors).  The CPU tests pass an
 oracle backend explicitly; nothing here falls back to the CPU on its own.
@@ -130,11 +138,39 @@ class HipOps:
         return self.D.partition_lut_pairs_scatter_u64_u32(keys, vals, self._top_lut(), TOP_SHIFT, 256,
                                                           out_keys=self.empty64(n), out_vals=self.empty(n))
 
-    def sort_pieces(self, keys, off, lens, segs, nseg, out):
+    # the range digit (key - bias) >> shift (RangeDigit) of narrow key ranges
+    def minmax_t(self, keys):
+        """(smallest, largest) uint32 key as an int64 device tensor [2]."""
+        return self.D.minmax_u32(keys).to(torch.int64) & 0xFFFFFFFF
+
+    def minmax64_t(self, keys):
+        """(smallest, largest) uint64 key: the int64 bits, device tensor [2]."""
+        return self.D.minmax_u64(keys)
+
+    def range_count_t(self, keys, rd):
+        return self.D.partition_range_count_u32(keys, rd.bias, rd.shift)
+
+    def range_scatter_t(self, keys, rd):
+        return self.D.partition_range_scatter_u32(keys, rd.bias, rd.shift, out=self.empty(keys.numel()))
+
+    def range_pairs_count_t(self, keys, vals, rd):
+        return self.D.partition_range_pairs_count_u64_u32(keys, vals, rd.bias, rd.shift)
+
+    def range_pairs_scatter_t(self, keys, vals, rd):
+        n = keys.numel()
+        return self.D.partition_range_pairs_scatter_u64_u32(keys, vals, rd.bias, rd.shift, out_keys=self.empty64(n),
+                                                            out_vals=self.empty(n))
+
+    def sort_pieces(self, keys, off, lens, segs, nseg, out, rd=None):
         """Round sort straight from the received pieces (libsortSortPiecesU32):
-        segment = top digit - the round's first digit, 24 bits left to sort."""
+        segment = top digit - the round's first digit, 24 bits left to sort;
+        with a range digit rd (libsortSortPiecesRangeU32), segment = range
+        digit - first digit, rd.shift bits of key - rd.bias left."""
         n = int(np.sum(lens)) if len(lens) else 0
-        return self.D.sort_pieces_u32(keys, off, lens, segs, nseg, TOP_SHIFT, out=out, tmp=self._scratch(n))
+        if rd is None:
+            return self.D.sort_pieces_u32(keys, off, lens, segs, nseg, TOP_SHIFT, out=out, tmp=self._scratch(n))
+        return self.D.sort_pieces_u32(keys, off, lens, segs, nseg, rd.shift, out=out, tmp=self._scratch(n),
+                                      bias=rd.bias)
 
     def delta_maxgap(self, keys, out):
         return self.D.delta_maxgap_u32(keys, out=out)
@@ -509,27 +545,77 @@ class _DigitRounds:
         return off, ln, seg, b - a
 
 
-def _digit_partition(keys, ops, group, vals=None):
+class RangeDigit:
+    """The rounds' partition digit over a narrow key range: (key - bias) >>
+    shift (8 bits, < 256 for every key in the populated range)."""
+
+    def __init__(self, bias, shift):
+        self.bias, self.shift = int(bias), int(shift)
+
+
+def _range_digit(keys, ops, group, key_bits):
+    """The range digit over every rank's keys (the C engine's rule,
+    csrc/distrib_plan.h range_digit via libsortDistribRangeDigit): bias = the
+    smallest key, shift = bits(largest - smallest) - 8 (at least 0).  None when
+    it would not split finer than the top digit (every key equal).  One
+    all-gather of the ranks' (min, max) and one host synchronisation -- the
+    decision is identical on every rank."""
+    import ctypes
+    from . import lib
+    mm = ops.minmax_t(keys) if key_bits == 32 else ops.minmax64_t(keys)
+    G = _to_host_async(_allgather_t(mm, group)).wait()      # [R, 2]
+    mask = (1 << key_bits) - 1
+    lo = min(int(v) & mask for v in G[:, 0])
+    hi = max(int(v) & mask for v in G[:, 1])
+    bias, shift = ctypes.c_uint64(), ctypes.c_uint32()
+    if lo > hi or not lib().libsortDistribRangeDigit(lo, hi, key_bits, ctypes.byref(bias), ctypes.byref(shift)):
+        return None
+    return RangeDigit(bias.value, shift.value)
+
+
+def _digit_partition(keys, ops, group, vals=None, rd=None):
     """The prefix of the top-digit round schedules: per-tile counts of the
-    top 8 key bits + column scan (the bucket starts), the stable top-digit
-    scatter queued right behind them, and beside it (side stream) the bucket
-    sizes, their all-gather and ONE small device-to-host copy -- the host
-    plans and issues the exchange while the scatter moves the data.
-    Returns (part, C[R, 256] host int64) or, with vals (pairs: digit =
-    key >> 56), ((part_keys, part_vals), C)."""
+    top 8 key bits (or, rd given, of the range digit) + column scan (the
+    bucket starts), the stable digit scatter queued right behind them, and
+    beside it (side stream) the bucket sizes, their all-gather and ONE small
+    device-to-host copy -- the host plans and issues the exchange while the
+    scatter moves the data.  Returns (part, C[R, 256] host int64) or, with
+    vals (pairs: digit = key >> 56), ((part_keys, part_vals), C)."""
     n = keys.numel()
     if vals is None:
-        b_t = ops.top_count_t(keys)
+        b_t = ops.top_count_t(keys) if rd is None else ops.range_count_t(keys, rd)
         side = _SideWork(b_t)
-        part = ops.top_scatter_t(keys)
+        part = ops.top_scatter_t(keys) if rd is None else ops.range_scatter_t(keys, rd)
     else:
-        b_t = ops.top_pairs_count_t(keys, vals)
+        b_t = ops.top_pairs_count_t(keys, vals) if rd is None else ops.range_pairs_count_t(keys, vals, rd)
         side = _SideWork(b_t)
-        part = ops.top_pairs_scatter_t(keys, vals)
+        part = ops.top_pairs_scatter_t(keys, vals) if rd is None else ops.range_pairs_scatter_t(keys, vals, rd)
     with side:
         sizes_t = _sizes_from_starts(b_t, n)
         pending = _to_host_async(_allgather_t(sizes_t, group))
     return part, pending.wait()
+
+
+def _too_skewed(est, N, S, max_imbalance):
+    return bool(N) and est.max() > max_imbalance * S + 4096
+
+
+def _narrow_range(keys, ops, group, part, C, lut, est, N, S, R, K, growth, max_imbalance, vals=None):
+    """The top-digit plan's skew check and, when it fails, the range-digit
+    re-partition (csrc/distrib.cpp sort_device does the same): returns (part,
+    C, lut, est, rd) of the partition the rounds run on (rd None: the top
+    digit), or part None when the keys stay too skewed for any digit plan
+    (keys: the LSD rounds; pairs never get None -- a heavy digit range only
+    concentrates work)."""
+    if not _too_skewed(est, N, S, max_imbalance):
+        return part, C, lut, est, None
+    rd = _range_digit(keys, ops, group, 32 if vals is None else 64)
+    if rd is not None:
+        part, C = _digit_partition(keys, ops, group, vals=vals, rd=rd)
+        lut, est = plan_digits(C, R, K, growth)
+    if vals is None and (rd is None or _too_skewed(est, N, S, max_imbalance)):
+        return None, C, lut, est, None
+    return part, C, lut, est, rd
 
 
 def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None, self_local=True, trace=None,
@@ -547,7 +633,8 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None
     S, _ = shard_cut(N, R)
     lut, est = plan_digits(C, R, K, growth)
     _mark(trace, "partition+allgather sizes+plan")
-    if N and est.max() > max_imbalance * S + 4096:
+    part, C, lut, est, rd = _narrow_range(keys, ops, group, part, C, lut, est, N, S, R, K, growth, max_imbalance)
+    if part is None:
         return sort_lsd(keys, ops, group)                      # identical decision on every rank
     g = _DigitRounds(C, lut, R, K)
     recv_tot = np.array([int(g.CB[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
@@ -580,7 +667,7 @@ def sort_msd(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=None
         if recv_tot[i]:
             off, ln, seg, nseg = g.pieces(i * R + r)
             a, z = int(roff[i]), int(roff[i + 1])
-            ops.sort_pieces(recv[a:z], off, ln, seg, nseg, out=out[a:z])
+            ops.sort_pieces(recv[a:z], off, ln, seg, nseg, out=out[a:z], rd=rd)
         _mark(trace, "round %d" % i)
     if not balance:
         return out
@@ -668,7 +755,8 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
     S, _ = shard_cut(N, R)
     lut, est = plan_digits(Cd, R, K, GROWTH_Z)
     _mark(trace, "partition+allgather sizes+plan")
-    if N and est.max() > max_imbalance * S + 4096:
+    part, Cd, lut, est, rd = _narrow_range(keys, ops, group, part, Cd, lut, est, N, S, R, K, GROWTH_Z, max_imbalance)
+    if part is None:
         return sort_lsd(keys, ops, group)                      # identical decision on every rank
     g = _DigitRounds(Cd, lut, R, K)
     C = g.CB                                                   # [R, R*K]: keys of rank s for group round*R + dest
@@ -698,7 +786,7 @@ def sort_msdz(keys, ops, group=None, max_imbalance=1.5, balance=True, rounds=Non
                 s0 = int(b[j])
                 off = g.start[r][a0:z0] - s0
                 ops.sort_pieces(part[s0:s0 + int(sizes[j])], off, g.C[r][a0:z0], np.arange(z0 - a0), z0 - a0,
-                                out=srt[s0:s0 + int(sizes[j])])
+                                out=srt[s0:s0 + int(sizes[j])], rd=rd)
         for d in range(R):
             j = i * R + d
             if remote(d) and sizes[j]:
@@ -786,6 +874,12 @@ def _sort_pairs_rounds(keys, vals, ops, group, rounds, self_local=True):
     K = max(1, min(int(ROUNDS if rounds is None else rounds), 256 // R))
     (pk, pv), Cd = _digit_partition(keys, ops, group, vals=vals)
     lut, est = plan_digits(Cd, R, K)
+    N = int(Cd.sum())
+    S, _ = shard_cut(N, R)
+    # keys below 2^56 or sharing their top byte: the range digit (no LSD
+    # fallback for pairs)
+    (pk, pv), Cd, lut, est, _ = _narrow_range(keys, ops, group, (pk, pv), Cd, lut, est, N, S, R, K, None, 1.5,
+                                              vals=vals)
     g = _DigitRounds(Cd, lut, R, K)
     recv_tot = np.array([int(g.CB[:, i * R + r].sum()) for i in range(K)], dtype=np.int64)
     roff = np.concatenate([[0], np.cumsum(recv_tot)])
@@ -840,5 +934,5 @@ def distrib_sort(keys, ops=None, group=None, schedule="auto", **kw):
     raise ValueError("schedule must be 'auto', 'msd', 'msdz' or 'lsd'")
 
 
-__all__ = ["HipOps", "distrib_sort", "distrib_sort_pairs", "sort_lsd", "sort_msd", "sort_msdz", "plan_digits",
-           "shard_cut"]
+__all__ = ["HipOps", "RangeDigit", "distrib_sort", "distrib_sort_pairs", "sort_lsd", "sort_msd", "sort_msdz",
+           "plan_digits", "shard_cut"]

@@ -195,6 +195,34 @@ LIBSORT_API bool libsortPartitionLutScatterU64U32(const uint64_t* d_kin, const u
                                                   const uint8_t* d_lut, uint32_t lut_shift,
                                                   uint32_t nbuckets, void* stream);
 
+/* The same two-call partitions by the 8-bit RANGE digit (key - bias) >> shift
+ * (256 buckets; every key in [bias, bias + 2^(shift + 8)); 0 <= shift <= 24
+ * for u32 keys, <= 56 for u64 keys): the multi-GPU rounds over a key range
+ * narrower than the top digit (IDs, timestamps, keys below 2^26 at 8 GPUs;
+ * bias and shift from libsortDistribRangeDigit over the ranks' smallest and
+ * largest keys).  Same call-order rule as the table partitions above. */
+LIBSORT_API bool libsortPartitionRangeCountU32(const uint32_t* d_in, size_t n, uint32_t bias, uint32_t shift,
+                                               uint32_t* d_bounds, void* stream);
+LIBSORT_API bool libsortPartitionRangeScatterU32(const uint32_t* d_in, uint32_t* d_out, size_t n, uint32_t bias,
+                                                 uint32_t shift, void* stream);
+LIBSORT_API bool libsortPartitionRangeCountU64U32(const uint64_t* d_kin, const uint32_t* d_vin, size_t n,
+                                                  uint64_t bias, uint32_t shift, uint32_t* d_bounds, void* stream);
+LIBSORT_API bool libsortPartitionRangeScatterU64U32(const uint64_t* d_kin, const uint32_t* d_vin, uint64_t* d_kout,
+                                                    uint32_t* d_vout, size_t n, uint64_t bias, uint32_t shift,
+                                                    void* stream);
+
+/* Smallest and largest key: d_minmax[0], d_minmax[1] (device; n == 0 gives
+ * the largest value of the type, then 0). */
+LIBSORT_API bool libsortMinMaxU32(const uint32_t* d_keys, size_t n, uint32_t* d_minmax, void* stream);
+LIBSORT_API bool libsortMinMaxU64(const uint64_t* d_keys, size_t n, uint64_t* d_minmax, void* stream);
+
+/* libsortSortPiecesU32 for pieces partitioned by the range digit: every key of
+ * segment s has the same bits [bits, 32) of key - bias (bits = the range
+ * digit's shift), increasing with s. */
+LIBSORT_API bool libsortSortPiecesRangeU32(const uint32_t* d_in, uint32_t* d_out, uint32_t* d_tmp, size_t n,
+                                           const uint64_t* off, const uint64_t* len, const uint32_t* seg,
+                                           size_t npieces, uint32_t nseg, uint32_t bits, uint32_t bias, void* stream);
+
 /* Gather-copy of nseg segments: dst[dst_off[i] + j] = src[src_off[i] + j] for
  * j < len[i].  The three tables are host arrays.  Used to put exchanged
  * buckets into bucket-major / rank-minor order between distributed rounds. */
@@ -274,6 +302,15 @@ LIBSORT_API bool libsortDistribSortPairsU64U32(int nranks, const int* devices, c
  * rank r receives.  nranks * rounds <= 256.  Host only (no device needed). */
 LIBSORT_API bool libsortDistribPlanDigits(const int64_t* counts, uint32_t nranks, uint32_t rounds, double growth,
                                           uint8_t* lut, int64_t* est);
+
+/* The range digit of the multi-GPU rounds when the top 8 key bits leave the
+ * keys in too few digits (csrc/distrib_plan.h range_digit; both engines use
+ * it): over the ranks' smallest and largest keys [lo, hi] of a key_bits-bit
+ * key (32 or 64), *bias = lo and *shift = max(0, bits(hi - lo) - 8), so every
+ * key's digit (key - lo) >> shift is < 256.  Returns whether that digit splits
+ * finer than the top digit (false when every key is equal).  Host only. */
+LIBSORT_API bool libsortDistribRangeDigit(uint64_t lo, uint64_t hi, uint32_t key_bits, uint64_t* bias,
+                                          uint32_t* shift);
 
 /* Writes elements [first, first+n) of the populateInput stream of a fresh
  * process (state 0x4d595df4d0f33173) to device memory, by LCG skip-ahead. */

@@ -110,15 +110,52 @@ class OracleOps:
         o = np.argsort(k >> np.uint64(56), kind="stable")
         return self.torch.from_numpy(k[o].view(np.int64).copy()), self._t(vals.numpy().view(np.uint32)[o])
 
-    def sort_pieces(self, keys, off, lens, segs, nseg, out):
+    # range digit (pylibsort.distrib.RangeDigit): digit = (key - bias) >> shift
+    def minmax_t(self, keys):
+        x = self._np(keys).astype(np.int64)
+        return self.torch.tensor([x.min(), x.max()] if x.size else [0xFFFFFFFF, 0], dtype=self.torch.int64)
+
+    def minmax64_t(self, keys):
+        k = keys.numpy().view(np.uint64)
+        mm = np.array([k.min(), k.max()] if k.size else [np.iinfo(np.uint64).max, 0], dtype=np.uint64)
+        return self.torch.from_numpy(mm.view(np.int64).copy())
+
+    def _rdig(self, x, rd, bits):
+        if bits == 32:
+            return ((x - np.uint32(rd.bias)) >> np.uint32(rd.shift)).astype(np.int64)
+        return ((x - np.uint64(rd.bias)) >> np.uint64(rd.shift)).astype(np.int64)
+
+    def range_count_t(self, keys, rd):
+        d = self._rdig(self._np(keys), rd, 32)
+        assert d.size == 0 or d.max() < 256, "range digit >= 256"
+        c = np.bincount(d, minlength=256)
+        return self.torch.from_numpy(np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.int64))
+
+    def range_scatter_t(self, keys, rd):
+        x = self._np(keys)
+        return self._t(x[np.argsort(self._rdig(x, rd, 32), kind="stable")])
+
+    def range_pairs_count_t(self, keys, vals, rd):
+        d = self._rdig(keys.numpy().view(np.uint64), rd, 64)
+        assert d.size == 0 or d.max() < 256, "range digit >= 256"
+        c = np.bincount(d, minlength=256)
+        return self.torch.from_numpy(np.concatenate([[0], np.cumsum(c)[:-1]]).astype(np.int64))
+
+    def range_pairs_scatter_t(self, keys, vals, rd):
+        k = keys.numpy().view(np.uint64)
+        o = np.argsort(self._rdig(k, rd, 64), kind="stable")
+        return self.torch.from_numpy(k[o].view(np.int64).copy()), self._t(vals.numpy().view(np.uint32)[o])
+
+    def sort_pieces(self, keys, off, lens, segs, nseg, out, rd=None):
         """libsortSortPiecesU32's contract, checked: every key of a segment
-        shares its top 8 bits and those increase with the segment."""
+        shares its top 8 bits (rd: its range digit) and those increase with
+        the segment."""
         x = self._np(keys)
         parts, tops = [], []
         for o, ln, sg in zip(off, lens, segs):
             p = x[int(o):int(o) + int(ln)]
             if p.size:
-                t = np.unique(p >> np.uint32(24))
+                t = np.unique(p >> np.uint32(24) if rd is None else self._rdig(p, rd, 32))
                 assert t.size == 1, "piece spans several top digits"
                 tops.append((int(sg), int(t[0])))
             parts.append(p)
@@ -209,6 +246,8 @@ def rank_worker(rank, world, port, x, schedule, outdir, use_gpu, kw=None):
     from pylibsort import distrib
     dist.init_process_group("gloo", rank=rank, world_size=world)
     shard = shard_inputs(x, world)[rank]
+    kw = dict(kw or {})
+    no_lsd = kw.pop("no_lsd", False)  # the LSD rounds must not run (range-digit tests)
     if use_gpu:
         torch.cuda.set_device(0)
         ops = distrib.HipOps()
@@ -216,7 +255,11 @@ def rank_worker(rank, world, port, x, schedule, outdir, use_gpu, kw=None):
     else:
         ops = OracleOps()
         keys = torch.from_numpy(shard.view(np.int32).copy())
-    res = distrib.distrib_sort(keys, ops=ops, schedule=schedule, **(kw or {}))
+    if no_lsd:
+        def _forbidden(*a, **k):
+            raise AssertionError("the LSD rounds ran (partial_sort) where the range digit should have")
+        ops.partial_sort = _forbidden
+    res = distrib.distrib_sort(keys, ops=ops, schedule=schedule, **kw)
     np.save(os.path.join(outdir, "rank%d.npy" % rank), res.cpu().numpy().view(np.uint32))
     dist.barrier()
     dist.destroy_process_group()
@@ -235,13 +278,24 @@ def pairs_worker(rank, world, port, k, outdir, use_gpu, kw=None):
     lo, hi = min(N, rank * S), min(N, (rank + 1) * S)
     kt = torch.from_numpy(k[lo:hi].view(np.int64).copy())
     vt = torch.from_numpy(np.arange(lo, hi, dtype=np.uint32).view(np.int32).copy())
+    kw = dict(kw or {})
+    expect_range = kw.pop("expect_range", False)  # the range-digit re-partition must run
     if use_gpu:
         torch.cuda.set_device(0)
         ops = distrib.HipOps()
         kt, vt = kt.cuda(), vt.cuda()
     else:
         ops = OracleOps()
-    rk, rv = distrib.distrib_sort_pairs(kt, vt, ops=ops, **(kw or {}))
+    ran = []
+    if expect_range:
+        inner = ops.range_pairs_count_t
+
+        def counted(*a, **k_):
+            ran.append(1)
+            return inner(*a, **k_)
+        ops.range_pairs_count_t = counted
+    rk, rv = distrib.distrib_sort_pairs(kt, vt, ops=ops, **kw)
+    assert not expect_range or ran, "the range-digit partition did not run"
     np.save(os.path.join(outdir, "k%d.npy" % rank), rk.cpu().numpy().view(np.uint64))
     np.save(os.path.join(outdir, "v%d.npy" % rank), rv.cpu().numpy().view(np.uint32))
     dist.barrier()

@@ -219,3 +219,50 @@ def test_auto_schedule_gloo(tmp_path):
     x = oracle.pcg(20011, first=5)
     shards = run_ranks(x, 2, "auto", tmp_path, port=30190)
     np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))
+
+
+def _narrow_case(case, n=60013, seed=3):
+    rng = np.random.default_rng(seed)
+    if case == "below2pow24":      # every key in top digit 0
+        return rng.integers(0, 1 << 24, n, dtype=np.uint64).astype(np.uint32)
+    if case == "offset_narrow":    # a 2^23-wide range at 2^31: one top digit
+        return (rng.integers(0, 1 << 23, n, dtype=np.uint64) + (1 << 31)).astype(np.uint32)
+    # 40 values a few apart inside one top digit: shift 0, one value per digit
+    return (rng.integers(0, 40, n, dtype=np.uint64) * 3 + 0x7F000000).astype(np.uint32)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("schedule", ["msd", "msdz"])
+@pytest.mark.parametrize("case", ["below2pow24", "offset_narrow", "one_digit_dups"])
+def test_range_digit_gloo(tmp_path, world, schedule, case):
+    """the torch engine re-partitions narrow key ranges
+    by the range digit (key - min) >> shift (libsortDistribRangeDigit, the C
+    engine's rule) instead of the 4-exchange LSD rounds: the LSD rounds must
+    not run (partial_sort raises), the result equals the oracle's sort and the
+    shards are the equal re-cut."""
+    from oracle import oracle
+    x = _narrow_case(case)
+    port = 30100 + 40 * world + 10 * ["msd", "msdz"].index(schedule) + ["below2pow24", "offset_narrow",
+                                                                        "one_digit_dups"].index(case)
+    shards = run_ranks(x, world, schedule, tmp_path, port=port, kw={"no_lsd": True})
+    np.testing.assert_array_equal(np.concatenate(shards), oracle.sort_u32(x))
+    assert [s.size for s in shards] == [s.size for s in shard_inputs(x, world)]
+
+
+@pytest.mark.parametrize("world,case", [(2, "below2pow40"), (3, "stamps")])
+def test_pairs_range_digit_gloo(tmp_path, world, case):
+    """Pair keys below 2^56 or sharing their top byte: the pair rounds
+    re-partition by the range digit (it must run), stable and exact."""
+    from distrib_helpers import run_pair_ranks
+    from oracle import oracle
+    rng = np.random.default_rng(world)
+    n = 30011
+    if case == "below2pow40":
+        k = rng.integers(0, 1 << 40, n, dtype=np.uint64)
+    else:
+        k = np.uint64(0x17A0000000000000) + rng.integers(0, 86400 * 10**9, n, dtype=np.uint64) // np.uint64(1000)
+        k[::7] = k[3]  # ties across ranks
+    ks, vs = run_pair_ranks(k, world, tmp_path, port=30300 + 10 * world, kw={"expect_range": True})
+    rk, rv = oracle.stable_sort_kv64(k, np.arange(n, dtype=np.uint32))
+    np.testing.assert_array_equal(np.concatenate(ks), rk)
+    np.testing.assert_array_equal(np.concatenate(vs), rv)
