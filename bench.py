@@ -56,6 +56,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 def default_engine(world):
     return "torch" if world == 2 else "cabi"
 PASS_KERNELS = "tilepass,onesweep,downsweep"  # the roofline kernel candidates (timed-region events)
+EVENT_STRIDE = 5  # N=1 timed region: events around every 5th pass launch (libsortTimingSample)
 
 
 def parse():
@@ -276,8 +277,13 @@ def main():
     # priced on (every kernel's events cost ~2.5% of the 2^28 sort); the full
     # per-kernel breakdown comes from two more steps after the timed region
     events = os.environ.get("BENCH_KERNEL_EVENTS", "1") != "0"  # "0": A/B of the events' own cost
+    # every EVENT_STRIDE-th pass launch gets its two events: 5 is coprime to
+    # the 4 digit passes of a configs[1] sort, so the sampled launches rotate
+    # over all four (each event stalls the stream ~5 us: 8 per sort cost ~1.5%)
+    stride = EVENT_STRIDE if world == 1 else 1
     D.timing_reset()
     D.timing_filter(PASS_KERNELS)
+    D.timing_sample(stride)
     D.timing_enable(events)
     barrier()
     torch.cuda.synchronize()
@@ -306,6 +312,7 @@ def main():
 
     timed_pass = query(PASS_KERNELS.split(","))
     D.timing_reset()
+    D.timing_sample(1)
     D.timing_filter(None)
     D.timing_enable(events)
     for _ in range(2):
@@ -365,8 +372,9 @@ def main():
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
                         "kernel": "k_%s (rank + scatter pass)" % ds_name, "algorithmic_bytes_per_launch": bytes_per_launch,
                         "avg_launch_us": round(ds["avg_us"], 2), "launches": ds["launches"],
-                        "timing": "live hipEvents around every pass launch of the timed steps (and no other "
-                                  "kernel), on libsort's stream"}
+                        "timing": "live hipEvents around every %s pass launch of the timed steps (and no other "
+                                  "kernel), on libsort's stream" % ("%dth (rotating over a sort's passes)" % stride
+                                                                    if stride > 1 else "")}
             # the committed profiles of THIS round's build and bench command
             # (tools/collect_profiles.sh): HBM bytes per launch from the PMC
             # passes, and the same kernel's average duration in rocprofv3's
@@ -511,23 +519,18 @@ def committed_profile(bytes_per_launch):
 def step_roofline(n, digit_bits, ms_per_step, kern):
     """The whole N=1 step against HBM: the bytes the
     hybrid sort actually moves per step -- one count read (4 B/key; none with
-    the reserved depth 0), 16 /
-    digit_bits digit passes and the bucket sort (read + write, 8 B/key each)
-    -- and SURVEY.md section 8(d)'s LSD-equivalent figure (32 / digit_bits
-    passes x 8 B/key: 64 B/key at 4-bit digits), each / ms_per_step."""
+    the reserved depth 0), 16 / digit_bits digit passes and the bucket sort
+    (read + write, 8 B/key each) -- / ms_per_step.  (Round 4's LSD-equivalent
+    figure priced passes the step does not run; dropped)"""
     passes = 16 // digit_bits if "bucketsort" in kern else 32 // digit_bits
     count = "tilecounts" in kern  # (4-bit keys-only hybrid: reserved depth 0, no count read)
     actual = n * ((4.0 if count else 0.0) + 8.0 * passes + (8.0 if "bucketsort" in kern else 0.0))
-    lsd_eq = n * 8.0 * (32 // digit_bits)
     t = ms_per_step * 1e-3
     return {"actual_bytes_per_key": actual / n, "actual_gbps": round(actual / t / 1e9, 1),
             "actual_frac": round(actual / t / 1e9 / HBM_PEAK_GBPS, 4),
-            "lsd_equivalent_bytes_per_key": lsd_eq / n, "lsd_equivalent_gbps": round(lsd_eq / t / 1e9, 1),
-            "lsd_equivalent_frac": round(lsd_eq / t / 1e9 / HBM_PEAK_GBPS, 4),
-            "note": "whole step (ms_per_step): actual = %s%d digit passes%s; lsd_equivalent = "
-                    "SURVEY 8(d) %d LSD passes x 8 B/key" % ("count read + " if count else "", passes,
-                                                            " + bucket sort" if "bucketsort" in kern else "",
-                                                            32 // digit_bits)}
+            "note": "whole step (ms_per_step): %s%d digit passes%s" % ("count read + " if count else "", passes,
+                                                                       " + bucket sort" if "bucketsort" in kern
+                                                                       else "")}
 
 
 def lsd_variant(torch, pylibsort, D, keys, out, tmp, reps):
@@ -648,6 +651,7 @@ def config_leg(torch, pylibsort, D, which, reps):
         torch.cuda.synchronize()
         D.timing_reset()
         D.timing_filter("tilepass")  # events around the pass only while timed (as the main line)
+        D.timing_sample(3)           # every 3rd launch: rotates over the leg's two digit passes
         D.timing_enable(True)
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -657,6 +661,7 @@ def config_leg(torch, pylibsort, D, which, reps):
         D.timing_enable(False)
         launches, tms, _ = D.timing_query("tilepass")
         D.timing_reset()
+        D.timing_sample(1)
         D.timing_filter(None)
         D.timing_enable(True)
         for _ in range(2):

@@ -281,6 +281,7 @@ void timing_enable(bool on);
 void timing_reset();
 // Records only the kernels named in `csv` ("tilepass,bucketsort"); null or "" = all.
 void timing_filter(const char* csv);
+void timing_sample(uint32_t every);
 bool timing_query(const char* name, uint64_t* launches, double* total_ms, uint64_t* total_keys);
 // Records a start event; returns a token (or -1 when timing is off).
 int timing_start(const char* name, hipStream_t stream, uint64_t keys);

@@ -109,6 +109,7 @@ _SIGS = [
     ("libsortTimingEnable", None, [ctypes.c_bool]),
     ("libsortTimingReset", None, []),
     ("libsortTimingFilter", None, [ctypes.c_char_p]),
+    ("libsortTimingSample", None, [ctypes.c_uint32]),
     ("libsortTimingQuery", ctypes.c_int,
      [ctypes.c_char_p, _u64p, ctypes.POINTER(ctypes.c_double), _u64p]),
     ("libsortReleaseWorkspace", ctypes.c_int, []),

@@ -511,6 +511,11 @@ def timing_filter(kernels=None):
     _lib().libsortTimingFilter(kernels.encode() if kernels else None)
 
 
+def timing_sample(every=1):
+    """Record only every `every`-th filtered launch (libsortTimingSample)."""
+    _lib().libsortTimingSample(int(every))
+
+
 def timing_query(kernel):
     """(launches, total_ms, total_keys) of the recorded launches of `kernel`."""
     n = ctypes.c_uint64()

@@ -375,6 +375,10 @@ LIBSORT_API int libsortSetBoundaryMode(int mode);
 LIBSORT_API void libsortTimingEnable(bool on);
 LIBSORT_API void libsortTimingReset(void);
 LIBSORT_API void libsortTimingFilter(const char* kernels);
+/* Record only every `every`-th launch that passes the filter (counted from the
+ * last reset; 0 or 1 = every launch).  A stride coprime to the launches of
+ * one sort samples each of them in turn with fewer events in the stream. */
+LIBSORT_API void libsortTimingSample(uint32_t every);
 LIBSORT_API bool libsortTimingQuery(const char* kernel, uint64_t* launches, double* total_ms,
                                     uint64_t* total_keys);
 
