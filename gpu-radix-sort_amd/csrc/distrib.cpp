@@ -170,6 +170,7 @@ struct RankState {
   DBuf bounds, part, pv, recv, rv, outb, ov, alt;  // pv / rv / ov: pair payloads
   DBuf mm;                                          // smallest and largest key (range partition)
   DBuf hin, hout;  // staging of the host-pointer entry point
+  uint64_t pn = 0;  // keys in `part` (24-bit planes: the 8-bit plane starts at byte 2 * pn)
   hipEvent_t ev_part = nullptr, ev_bounds = nullptr, ev_done = nullptr;
   hipEvent_t ev_x[kMaxRounds] = {};
 };
@@ -182,6 +183,7 @@ struct Ctx {
   uint32_t* h_bounds = nullptr;                // pinned: R x 256 bucket starts
   uint64_t* h_mm = nullptr;                    // pinned: R x (min, max) keys
   bool distinct = false;
+  std::vector<uint64_t> sent;                  // bytes each rank sent to others in the last sort
 
   ~Ctx() {
     for (ncclComm_t c : comms)
@@ -272,16 +274,20 @@ std::unique_ptr<Ctx> g_ctx;
 // copy (unless self_rccl); across devices RCCL point-to-point (one group for
 // the whole set) or, with `copy`, a peer copy pulled by the receiver.
 bool move_pieces(Ctx& c, const std::vector<dplan::Piece>& ps, const std::vector<const void*>& src,
-                 const std::vector<void*>& dst, size_t esize, bool use_rccl, bool self_rccl) {
-  const ncclDataType_t dt = esize == 8 ? ncclUint64 : ncclUint32;
+                 const std::vector<void*>& dst, size_t esize, bool use_rccl, bool self_rccl, bool count = true) {
+  // (1- and 2-byte elements: the 24-bit key planes, sent as bytes)
+  const ncclDataType_t dt = esize == 8 ? ncclUint64 : esize == 4 ? ncclUint32 : ncclUint8;
+  const uint64_t per = esize >= 4 ? 1 : esize;  // RCCL elements per element
   auto at = [esize](const void* base, uint64_t off) { return static_cast<const char*>(base) + off * esize; };
   auto atw = [esize](void* base, uint64_t off) { return static_cast<char*>(base) + off * esize; };
   std::vector<const dplan::Piece*> net;
+  if (c.sent.size() != c.ranks.size()) c.sent.assign(c.ranks.size(), 0);
   for (const dplan::Piece& p : ps) {
     if (!p.count) continue;
     RankState& a = c.ranks[p.src];
     RankState& b = c.ranks[p.dst];
     const size_t bytes = p.count * esize;
+    if (count && p.src != p.dst) c.sent[p.src] += bytes;
     if (use_rccl && (p.src != p.dst || self_rccl)) {
       net.push_back(&p);
     } else if (a.dev == b.dev) {
@@ -312,9 +318,9 @@ bool move_pieces(Ctx& c, const std::vector<dplan::Piece>& ps, const std::vector<
     RankState& b = c.ranks[p->dst];
     for (uint64_t o = 0; ok && o < p->count; o += chunk) {
       const uint64_t m = std::min(chunk, p->count - o);
-      ok = g_rccl.ok(g_rccl.send(at(src[p->src], p->src_off + o), m, dt, p->dst, c.comms[p->src], a.d->cs),
+      ok = g_rccl.ok(g_rccl.send(at(src[p->src], p->src_off + o), m * per, dt, p->dst, c.comms[p->src], a.d->cs),
                      "ncclSend") &&
-           g_rccl.ok(g_rccl.recv(atw(dst[p->dst], p->dst_off + o), m, dt, p->src, c.comms[p->dst], b.d->cs),
+           g_rccl.ok(g_rccl.recv(atw(dst[p->dst], p->dst_off + o), m * per, dt, p->src, c.comms[p->dst], b.d->cs),
                      "ncclRecv");
     }
   }
@@ -486,9 +492,14 @@ struct PartDigit {
 // 256 bucket starts' copy to the host are queued first, then the scatter, so
 // the host reads the counts while the data moves.  C[r][g] = rank r's keys
 // in digit g.
+// planar (keys, top digit): the scatter writes 24-bit planes into `part`
+// (low 16 bits at byte 0, bits 16..23 at byte 2 * n): the top byte is the
+// partition digit, which every receiver knows from its piece table, so the
+// exchange moves 3 bytes per key instead of 4 (round 5).
 template <typename K>
 bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<const uint32_t*>* vin,
-                   const std::vector<uint64_t>& n, std::vector<std::vector<uint64_t>>& C, const PartDigit& pd) {
+                   const std::vector<uint64_t>& n, std::vector<std::vector<uint64_t>>& C, const PartDigit& pd,
+                   bool planar = false) {
   const int R = (int)c.ranks.size();
   constexpr int NB = dplan::kTopDigits;
   for (int r = 0; r < R; ++r) {
@@ -516,9 +527,13 @@ bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<co
                   "D2H bucket starts") ||
           !ok_hip(hipEventRecord(s.ev_bounds, s.d->st), "hipEventRecord"))
         return false;
+      s.pn = n[r];
       if constexpr (sizeof(K) == 4) {
         e2 = pd.range ? partition_range_u32(ws, in[r], s.part.u32(), n[r], (uint32_t)pd.bias, pd.shift, nullptr,
                                             s.d->st, kPartScatter)
+             : planar ? partition_lut_planar_u32(ws, in[r], static_cast<uint16_t*>(s.part.p),
+                                                 static_cast<uint8_t*>(s.part.p) + 2 * n[r], n[r], lut,
+                                                 dplan::kTopShift, NB, s.d->st)
                       : partition_lut_u32(ws, in[r], s.part.u32(), n[r], lut, dplan::kTopShift, NB, nullptr, s.d->st,
                                           kPartScatter);
       } else {
@@ -591,7 +606,7 @@ bool range_digit(Ctx& c, const std::vector<const K*>& in, const std::vector<uint
 template <typename K>
 bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& out,
                       const std::vector<uint32_t*>* vout, bool use_rccl, bool self_rccl, int bits,
-                      const PartDigit& pd) {
+                      const PartDigit& pd, bool planar = false) {
   const int R = (int)c.ranks.size(), K_ = p.K;
   const bool pairs = vout != nullptr;
   std::map<DevState*, uint64_t> round_max;
@@ -617,6 +632,15 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
     vsrc[r] = c.ranks[r].pv.p;
     vdst[r] = c.ranks[r].rv.p;
   }
+  // planar: the 16-bit planes at the buffers' start, the 8-bit planes after
+  // them (sender: 2 * its partition's keys; receiver: 2 * its received keys)
+  std::vector<const void*> src8(R);
+  std::vector<void*> dst8(R);
+  if (planar)
+    for (int r = 0; r < R; ++r) {
+      src8[r] = static_cast<const char*>(c.ranks[r].part.p) + 2 * c.ranks[r].pn;
+      dst8[r] = static_cast<char*>(c.ranks[r].recv.p) + 2 * p.n_recv[r];
+    }
   // rounds inside the rank's output shard are sorted straight into it; the
   // others into outb, whose pieces move afterwards (dplan::place_rounds)
   const dplan::Placement pl = dplan::place_rounds(p.roff, p.n_recv, K_);
@@ -633,10 +657,16 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
       K* kdst = pl.direct[q] ? out[r] + pl.out_off[q] : static_cast<K*>(s.outb.p) + a;
       uint32_t* vdst = pairs ? (pl.direct[q] ? (*vout)[r] + pl.out_off[q] : s.ov.u32() + a) : nullptr;
       if constexpr (sizeof(K) == 4) {
-        e = sort_pieces_u32(*d.ws, s.recv.u32() + a, kdst, d.tmp.u32(), z - a, p.p_off[q].data(), p.p_len[q].data(),
-                            p.p_seg[q].data(), p.p_off[q].size(),
-                            (uint32_t)(p.hi[(size_t)i * R + r] - p.lo[(size_t)i * R + r]), pd.shift, bits, d.st,
-                            (uint32_t)pd.bias);
+        const uint32_t nsg = (uint32_t)(p.hi[(size_t)i * R + r] - p.lo[(size_t)i * R + r]);
+        if (planar)
+          e = sort_pieces_planar_u32(*d.ws, static_cast<const uint16_t*>(s.recv.p) + a,
+                                     static_cast<const uint8_t*>(s.recv.p) + 2 * p.n_recv[r] + a,
+                                     (uint32_t)p.lo[(size_t)i * R + r], kdst, d.tmp.u32(), z - a, p.p_off[q].data(),
+                                     p.p_len[q].data(), p.p_seg[q].data(), p.p_off[q].size(), nsg, bits, d.st);
+        else
+          e = sort_pieces_u32(*d.ws, s.recv.u32() + a, kdst, d.tmp.u32(), z - a, p.p_off[q].data(),
+                              p.p_len[q].data(), p.p_seg[q].data(), p.p_off[q].size(), nsg, pd.shift, bits, d.st,
+                              (uint32_t)pd.bias);
       } else {
         e = sort_pairs_u64_u32(*d.ws, static_cast<uint64_t*>(s.recv.p) + a, s.rv.u32() + a, kdst, vdst,
                                static_cast<uint64_t*>(d.tmp.p), d.tmpv.u32(), z - a, 0, 64, bits, d.st);
@@ -685,7 +715,9 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
       });
   bool issue_ok = true;
   for (int i = 0; issue_ok && i < K_; ++i) {
-    issue_ok = move_pieces(c, p.rounds[i], src, dst, sizeof(K), use_rccl, self_rccl) &&
+    issue_ok = (planar ? move_pieces(c, p.rounds[i], src, dst, 2, use_rccl, self_rccl) &&
+                             move_pieces(c, p.rounds[i], src8, dst8, 1, use_rccl, self_rccl)
+                       : move_pieces(c, p.rounds[i], src, dst, sizeof(K), use_rccl, self_rccl)) &&
                (!pairs || move_pieces(c, p.rounds[i], vsrc, vdst, 4, use_rccl, self_rccl));
     for (int r = 0; issue_ok && r < R; ++r) {
       RankState& s = c.ranks[r];
@@ -732,8 +764,10 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
     vsrc[r] = c.ranks[r].ov.p;
     vdst[r] = pairs ? (*vout)[r] : nullptr;
   }
-  return move_pieces(c, cut, src, dst, sizeof(K), use_rccl, self_rccl) &&
-         (!pairs || move_pieces(c, cut, vsrc, vdst, 4, use_rccl, self_rccl));
+  // (the re-cut's few surplus keys are not counted in c.sent: the exchange
+  // rounds' bytes are what the wire format changes)
+  return move_pieces(c, cut, src, dst, sizeof(K), use_rccl, self_rccl, false) &&
+         (!pairs || move_pieces(c, cut, vsrc, vdst, 4, use_rccl, self_rccl, false));
 }
 
 // Shared prologue of both entry points: sizes, the output shard counts.
@@ -773,11 +807,21 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
   std::vector<uint32_t*> out(d_out, d_out + R);
   if (N == 0) return hold.finish(true);
   const uint64_t S = dplan::shard_size(N, R);
+  c.sent.assign(R, 0);
   if (flags & kDistribLsd) return hold.finish(run_lsd(c, in, n, out, S, bits, !copy, self_rccl));
   const int K = std::max(1, std::min(kMaxRounds, 256 / R));
   std::vector<std::vector<uint64_t>> C;
   PartDigit pd;
-  if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd)) return hold.finish(false);
+  // 24-bit keys on the wire (top-digit rounds; LIBSORT_DISTRIB_WIRE24=0 or the
+  // WIRE32 flag: 32-bit): planes from the partition scatter, read back by
+  // the round sorts' reserved depth 0 (4-bit digits; 8-bit round sorts of
+  // more than two segments could not take it and would unpack first)
+  static const bool wire24_env = [] {
+    const char* e = getenv("LIBSORT_DISTRIB_WIRE24");
+    return !(e && e[0] == '0');
+  }();
+  const bool planar = wire24_env && !(flags & kDistribWire32) && bits == 4;
+  if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd, planar)) return hold.finish(false);
   std::vector<uint8_t> lut(dplan::kTopDigits);
   std::vector<int64_t> est(R);
   dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
@@ -787,7 +831,7 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
     // LSD rounds from the untouched input
     bool useful = false;
     if (!range_digit<uint32_t>(c, in, n, pd, &useful)) return hold.finish(false);
-    if (useful) {
+    if (useful) {  // (the range digit is not the top byte: 32-bit keys on the wire)
       if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd)) return hold.finish(false);
       dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
     }
@@ -795,7 +839,7 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
       return hold.finish(run_lsd(c, in, n, out, S, bits, !copy, self_rccl));
   }
   return hold.finish(run_digit_rounds<uint32_t>(c, dplan::digit_plan(C, lut.data(), K), out, nullptr, !copy, self_rccl,
-                                                bits, pd));
+                                                bits, pd, planar && !pd.range));
 }
 
 bool sort_device_pairs(Ctx& c, const uint64_t* const* d_kin, const uint32_t* const* d_vin, const size_t* n_in,
@@ -813,6 +857,7 @@ bool sort_device_pairs(Ctx& c, const uint64_t* const* d_kin, const uint32_t* con
   if (!check_sizes(R, n_in, n, N, n_out)) return false;
   Hold hold(c);
   if (!hold.ok) return hold.finish(false);
+  c.sent.assign(R, 0);
   if (N == 0) return hold.finish(true);
   std::vector<const uint64_t*> kin(d_kin, d_kin + R);
   std::vector<const uint32_t*> vin(d_vin, d_vin + R);
@@ -893,6 +938,13 @@ bool distrib_sort_host_u32(uint32_t* h, size_t len, const int* devices, int R, u
                               "D2H shard"));
   }
   return sync_all(*c) && ok;
+}
+
+bool distrib_last_bytes(uint64_t* per_rank, int nranks) {
+  std::lock_guard<std::mutex> glk(g_dist_mu);
+  if (!g_ctx || (int)g_ctx->sent.size() != nranks || !per_rank) return false;
+  for (int r = 0; r < nranks; ++r) per_rank[r] = g_ctx->sent[r];
+  return true;
 }
 
 void distrib_release() {

@@ -1225,6 +1225,14 @@ LS_BOOL_ENTRY(libsortDistribPlanDigits, const int64_t* counts, uint32_t nranks, 
   return 1;
 }
 
+LS_BOOL_ENTRY(libsortDistribLastBytes, int nranks, uint64_t* per_rank) {
+  if (nranks < 1 || !per_rank || !distrib_last_bytes(per_rank, nranks)) {
+    set_error("libsortDistribLastBytes: no distributed sort over nranks ranks has run");
+    return 0;
+  }
+  return 1;
+}
+
 LS_BOOL_ENTRY(libsortDistribRangeDigit, uint64_t lo, uint64_t hi, uint32_t key_bits, uint64_t* bias,
               uint32_t* shift) {
   if (!bias || !shift || (key_bits != 32 && key_bits != 64)) {
@@ -1255,7 +1263,7 @@ LS_BOOL_ENTRY(libsortDistribSortU32, int nranks, const int* devices, const uint3
     set_error("libsortDistribSortU32: need nranks >= 1 and non-NULL tables");
     return 0;
   }
-  if (flags & ~(kDistribLsd | kDistribCopy | kDistribSelfRccl)) {
+  if (flags & ~(kDistribLsd | kDistribCopy | kDistribSelfRccl | kDistribWire32)) {
     set_error("libsortDistribSortU32: unknown flags");
     return 0;
   }

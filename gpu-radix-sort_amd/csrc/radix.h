@@ -174,6 +174,12 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
 hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n,
                            const uint64_t* off, const uint64_t* len, const uint32_t* seg, size_t np, uint32_t nseg,
                            int bits, int digit_bits, hipStream_t stream, uint32_t bias = 0);
+// The same over 24-bit pieces (the multi-GPU exchange's "wire24" format):
+// in16 / in8 hold each key's low 16 bits and bits 16..23 at the key's index,
+// segment s's keys have top byte hi0 + s (bits = 24 below the segment).
+hipError_t sort_pieces_planar_u32(Workspace& ws, const uint16_t* in16, const uint8_t* in8, uint32_t hi0,
+                                  uint32_t* out, uint32_t* tmp, size_t n, const uint64_t* off, const uint64_t* len,
+                                  const uint32_t* seg, size_t np, uint32_t nseg, int digit_bits, hipStream_t stream);
 hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t* vin,
                               uint32_t* kout, uint32_t* vout, uint32_t* ktmp, uint32_t* vtmp,
                               size_t n, int lo, int hi, int digit_bits, hipStream_t stream);
@@ -219,6 +225,12 @@ constexpr int kPartBoth = 0, kPartCount = 1, kPartScatter = 2;
 hipError_t partition_lut_u32(Workspace& ws, const uint32_t* in, uint32_t* out, size_t n, const uint8_t* d_lut,
                              int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t stream,
                              int phase = kPartBoth);
+// The scatter phase of partition_lut_u32 (after its count call, lut_shift 24,
+// 256 buckets) writing 24-bit planes instead of u32 keys: o16[i] = low 16
+// bits, o8[i] = bits 16..23 of the key at partition position i (the top byte
+// is the bucket).
+hipError_t partition_lut_planar_u32(Workspace& ws, const uint32_t* in, uint16_t* o16, uint8_t* o8, size_t n,
+                                   const uint8_t* d_lut, int lut_shift, int nbuckets, hipStream_t stream);
 // The same for (u64 key, u32 value) pairs; bucket = lut[(key >> 32) >> lut_shift].
 hipError_t partition_lut_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
                                        uint32_t* vout, size_t n, const uint8_t* d_lut, int lut_shift, int nbuckets,
@@ -260,9 +272,14 @@ void ws_release_stream(int dev, hipStream_t st);
 constexpr unsigned kDistribLsd = 1u;       // the reference's BSP LSD rounds instead of the range rounds
 constexpr unsigned kDistribCopy = 2u;      // exchanges as peer copies instead of RCCL
 constexpr unsigned kDistribSelfRccl = 4u;  // a rank's own pieces through RCCL too (tests)
+constexpr unsigned kDistribWire32 = 8u;    // 32-bit keys on the wire (default: 24-bit planes, top-digit rounds)
 // Rank r's shard d_in[r] (n_in[r] keys, on device devices[r]; devices may
 // repeat) -> d_out[r] = keys [r*S, (r+1)*S) of the sorted whole, S =
 // ceil(N/R); n_out[r] receives the count.  Synchronous.
+// Bytes each rank sent to other ranks in the exchange rounds of the last
+// distributed sort (own pieces and the re-cut excluded); false if none ran or
+// nranks differs.
+bool distrib_last_bytes(uint64_t* per_rank, int nranks);
 bool distrib_sort_u32(const int* devices, int R, const uint32_t* const* d_in, const size_t* n_in, uint32_t* const* d_out,
                       size_t* n_out, unsigned flags, int digit_bits);
 // (u64 key, u32 payload) pairs, stable (configs[4]): the top-digit rounds on

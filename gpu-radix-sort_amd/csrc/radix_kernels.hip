@@ -1160,6 +1160,16 @@ struct HybridGeo {
   const uint32_t* rslice;    // [3][NS] slice start | capacity | first next-depth tile
   uint32_t* rflag;           // set to 1 when a tile's reservation passed its slice's capacity
   uint32_t rns;              // NS: the slices (RADIX * 8 per segment)
+  // 24-bit keys of the multi-GPU exchange (round 5; distrib.cpp "wire24"):
+  // the partition scatter writes each key's low 16 bits to o16 and bits
+  // 16..23 to o8 instead of kout (its top byte is the partition digit, known
+  // to the receiver from the piece); a piece sort's depth 0 (GEO 5) reads them
+  // back from i16 / i8, the top byte from seghi[segment]
+  uint16_t* o16 = nullptr;
+  uint8_t* o8 = nullptr;
+  const uint16_t* i16 = nullptr;
+  const uint8_t* i8 = nullptr;
+  const uint32_t* seghi = nullptr;  // [segment] its keys' top byte << 24
 };
 
 // The pass kernel of the tile-offset path: the onesweep tile body with the
@@ -1208,7 +1218,7 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   // of their own; after the keys have been written to HBM they are scattered
   // into the key buffer and written from there (LDS 69 KB per block instead
   // of 101 KB: two blocks per CU).
-  constexpr bool STAGE_V = HAS_V && sizeof(K) == 8 && ITEMS == 16;
+  constexpr bool STAGE_V = HAS_V && sizeof(K) == 8 && TILE == 8192;
   static_assert(!STAGE_V || (!FUSE && sizeof(VS) <= sizeof(K)), "staged values: 8-bit pair tiles");
   // LDS per block (occupancy: 160 KiB per CU): the per-wave digit counters
   // are 16-bit, and the destination-tile entries exist only for FUSE.
@@ -1222,6 +1232,8 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   __shared__ uint32_t s_wsum[WAVES];
   __shared__ __attribute__((aligned(16))) uint8_t s_lut[OpLds<Op>::bytes];
   constexpr bool ATOMIC_RANK = ANY_ORDER && LIBSORT_HYB_ATOMIC_RANK && !HAS_V;
+  // (the partition scatter of the 24-bit exchange: geo.o16 / geo.o8)
+  constexpr bool PLANAR_OUT = GEO == 0 && !FUSE && sizeof(K) == 4 && !HAS_V;
   __shared__ uint32_t s_acnt[ATOMIC_RANK ? WAVES : 1][ATOMIC_RANK ? RADIX : 1];
   // GEO & 4: the tile's runs go where it reserves them (an agent-scope add
   // per digit on its range's slice cursor) instead of where a count pass and
@@ -1295,7 +1307,19 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   // keys 2.66 -> 2.62 ms, c3 10.69 -> 10.54 ms, interleaved A/B runs; 4-bit
   // unchanged; pairs 0.6% slower, so not for them)
   if constexpr (!HAS_V) __builtin_amdgcn_s_setprio(2);
-  {
+  // (GEO 5 over 24-bit pieces: geo.i16 / geo.i8 instead of kin)
+  constexpr bool PLANAR_IN = (GEO & 5) == 5 && sizeof(K) == 4 && !HAS_V;
+  if (PLANAR_IN && geo.i8 != nullptr) {
+    const uint32_t hi = geo.seghi[seg];
+    const uint16_t* p16 = geo.i16 + tile_base + wbase + lane;
+    const uint8_t* p8 = geo.i8 + tile_base + wbase + lane;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const bool ok = full || wbase + j * kWave + lane < valid;
+      k[j] = ok ? (K)(hi | ((uint32_t)load_stream(&p8[j * kWave]) << 16) | (uint32_t)load_stream(&p16[j * kWave]))
+                : (K)0;
+    }
+  } else {
     const K* kp = kin + tile_base + wbase + lane;
     const V* vp = HAS_V ? vin + tile_base + wbase + lane : nullptr;
     if (full) {
@@ -1460,7 +1484,12 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
 #pragma unroll
       for (int j = 0; j < SP; ++j) {
         const uint32_t i = tid + (h * SP + j) * BLOCK;
-        kout[ob_base(ob[j]) + i] = kk[j];
+        if (PLANAR_OUT && geo.o16 != nullptr) {
+          geo.o16[ob_base(ob[j]) + i] = (uint16_t)kk[j];
+          geo.o8[ob_base(ob[j]) + i] = (uint8_t)((uint32_t)kk[j] >> 16);
+        } else {
+          kout[ob_base(ob[j]) + i] = kk[j];
+        }
         if constexpr (HAS_V) vout[ob_base(ob[j]) + i] = s_vals[i];
         if constexpr (DOUT)
           if (dout) dout[ob_base(ob[j]) + i] = (uint8_t)op_next(kk[j]);
@@ -1487,7 +1516,12 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
       const K kk = s_keys[i];
       const uint32_t d = op(kk);
       const OB ob = s_ob[d];
-      kout[ob_base(ob) + i] = kk;
+      if (PLANAR_OUT && geo.o16 != nullptr) {
+        geo.o16[ob_base(ob) + i] = (uint16_t)kk;
+        geo.o8[ob_base(ob) + i] = (uint8_t)((uint32_t)kk >> 16);
+      } else {
+        kout[ob_base(ob) + i] = kk;
+      }
       if constexpr (HAS_V) vout[ob_base(ob) + i] = s_vals[i];
       if constexpr (DOUT)
         if (dout) dout[ob_base(ob) + i] = (uint8_t)op_next(kk);
@@ -1606,6 +1640,79 @@ __device__ __forceinline__ uint32_t block_exclusive_scan_in(uint32_t v, uint32_t
 __device__ __forceinline__ uint32_t field2_sum(uint32_t w) {
   return (uint32_t)__builtin_popcount(w & 0x55555555u) + 2u * (uint32_t)__builtin_popcount(w & 0xAAAAAAAAu);
 }
+// The weight up to which an overflowed 2-bit bucket is retried with 3-bit
+// cells (kCnt2F: the threads that saw a count wrap; a uniform bucket's
+// overflow is one value with 4 keys: 1-2).
+constexpr uint32_t kRetryMax = 16;
+// kCnt2F's inline retry (INL) of a lightly overflowed bucket (a value with 4+
+// keys wrapped its 2-bit count: ~4% of the uniform 4096-key buckets of a 2^28
+// sort), in the same 24 KB: 3-bit u64 cells over HALF the cell space at a
+// time (2048 cells = 16 KB), each key counted and placed in the half its cell
+// falls in, the second half's starts after the first half's keys.  Sets rk[j]
+// to every key's position; false when a 3-bit count would wrap too (8+ equal
+// keys: the caller lists the bucket for the LSD steps).  Replaces round 4's
+// separate 3-bit LIST launch over those buckets (~45 us per 2^28 sort: two
+// latency-bound rounds of ~20 us buckets).
+template <int BLOCK, int ITEMS, typename ValFn>
+__device__ __forceinline__ bool retry3_halves(const uint32_t (&k)[ITEMS], uint32_t (&rk)[ITEMS], uint32_t* s_mem,
+                                              uint32_t* s_wsum, uint32_t len, uint32_t wbase, uint32_t lane,
+                                              ValFn val) {
+  constexpr uint32_t HC = kCntCells / 2, PER2 = HC / BLOCK;
+  static_assert(PER2 >= 1 && HC % BLOCK == 0, "half-cells per thread");
+  uint64_t* const s_c = reinterpret_cast<uint64_t*>(s_mem);
+  const uint32_t tid = threadIdx.x;
+  auto ci2 = [&](uint32_t c) -> uint32_t { return (c % PER2) * BLOCK + c / PER2; };
+  uint32_t base = 0;
+#pragma unroll 1
+  for (uint32_t h = 0; h < 2; ++h) {
+    __syncthreads();  // the region's previous use (the 2-bit cells; half 0) is over
+#pragma unroll
+    for (uint32_t q = 0; q < PER2; ++q) s_c[q * BLOCK + tid] = 0ull;
+    __syncthreads();
+    bool ovf = false;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (wbase + j * kWave + lane < len) {
+        const uint32_t v = val(k[j]), c = v >> 4;
+        if ((c / HC) == h) {
+          const uint32_t sh = 3u * (v & 15u);
+          const uint64_t old = atomicAdd((unsigned long long*)&s_c[ci2(c % HC)], (1ull << sh) + (1ull << 48));
+          rk[j] = (uint32_t)(old >> sh) & 7u;
+          ovf |= rk[j] == 7u;
+        }
+      }
+    if (__any(ovf) && lane == 0) atomicOr((unsigned long long*)&s_c[0], 1ull << 63);
+    __syncthreads();
+    if (s_c[0] >> 63) return false;
+    uint64_t cw[PER2];
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < PER2; ++q) {
+      cw[q] = s_c[q * BLOCK + tid];
+      sum += (uint32_t)(cw[q] >> 48);
+    }
+    uint32_t total;
+    uint32_t run = block_exclusive_scan<BLOCK>(sum, s_wsum, total) + base;
+#pragma unroll
+    for (uint32_t q = 0; q < PER2; ++q) {
+      s_c[q * BLOCK + tid] = (cw[q] & 0xFFFFFFFFFFFFull) | ((uint64_t)run << 48);
+      run += (uint32_t)(cw[q] >> 48);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+      if (wbase + j * kWave + lane < len) {
+        const uint32_t v = val(k[j]), c = v >> 4;
+        if ((c / HC) == h) {
+          const uint64_t cc = s_c[ci2(c % HC)];
+          rk[j] += (uint32_t)(cc >> 48) + field3_sum(cc & ((1ull << (3u * (v & 15u))) - 1ull));
+        }
+      }
+    base += total;
+  }
+  return true;
+}
+
 // The counting placement works in exactly the cell words (32 KB: five blocks
 // of 256 threads per CU): the overflow flag is a spare bit of a cell word,
 // the block scan's wave sums borrow cell words once every wave holds its
@@ -1614,7 +1721,7 @@ __device__ __forceinline__ uint32_t field2_sum(uint32_t w) {
 // overflow's weight: kCnt2F the threads that saw a count wrap (a uniform
 // bucket's overflow is one value with 4 keys: 1-2; a duplicate-heavy bucket
 // wraps in most threads), the other modes 1.
-template <int BLOCK, int ITEMS, int MODE, typename Op>
+template <int BLOCK, int ITEMS, int MODE, typename Op, bool INL = false>
 __device__ __forceinline__ uint32_t bucket_count_place(const uint32_t (&k)[ITEMS], uint64_t* s_cw, uint32_t* out,
                                                    uint32_t start, uint32_t len, uint32_t lbits_in, uint32_t bias) {
   constexpr int PER = kCntCells / BLOCK;
@@ -1656,27 +1763,33 @@ __device__ __forceinline__ uint32_t bucket_count_place(const uint32_t (&k)[ITEMS
     const uint64_t bal = __ballot(ovf);
     if (bal && lane == 0) atomicAdd(&s_ws2[BLOCK / kWave], (uint32_t)__popcll(bal));
     __syncthreads();
-    if (const uint32_t sev = s_ws2[BLOCK / kWave]) return sev;
-    uint32_t cnt[PER], sum = 0;
+    if (const uint32_t sev = s_ws2[BLOCK / kWave]) {
+      // light (a few values with 4+ keys): the 3-bit retry inline (INL);
+      // heavy, or a 3-bit wrap: the caller lists the bucket
+      if (!INL || sev > kRetryMax) return sev;
+      if (!retry3_halves<BLOCK, ITEMS>(k, rk, s_keys, s_ws2, len, wbase, lane, val)) return kRetryMax + 1;
+    } else {
+      uint32_t cnt[PER], sum = 0;
 #pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      cnt[q] = field2_sum(s_w[q * BLOCK + tid]);
-      sum += cnt[q];
-    }
-    uint32_t total;
-    uint32_t run = block_exclusive_scan<BLOCK>(sum, s_ws2, total);
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      s_st[q * BLOCK + tid] = (uint16_t)run;
-      run += cnt[q];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j)
-      if (valid(j)) {
-        const uint32_t v = val(k[j]), c = ci(v >> 4);
-        rk[j] += (uint32_t)s_st[c] + field2_sum(s_w[c] & ((1u << (2u * (v & 15u))) - 1u));
+      for (int q = 0; q < PER; ++q) {
+        cnt[q] = field2_sum(s_w[q * BLOCK + tid]);
+        sum += cnt[q];
       }
+      uint32_t total;
+      uint32_t run = block_exclusive_scan<BLOCK>(sum, s_ws2, total);
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        s_st[q * BLOCK + tid] = (uint16_t)run;
+        run += cnt[q];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j)
+        if (valid(j)) {
+          const uint32_t v = val(k[j]), c = ci(v >> 4);
+          rk[j] += (uint32_t)s_st[c] + field2_sum(s_w[c] & ((1u << (2u * (v & 15u))) - 1u));
+        }
+    }
   } else if constexpr (MODE != kCntSmall) {
 #pragma unroll
     for (int q = 0; q < PER; ++q) s_cw[q * BLOCK + tid] = 0ull;
@@ -1789,8 +1902,7 @@ __device__ __forceinline__ uint32_t bucket_count_place(const uint32_t (&k)[ITEMS
 // written nothing and listed: in retry_list when given and its overflow
 // weighs <= kRetryMax (a few values with 4+ keys), else in ovf_list (the LSD
 // steps of k_bucket_sort LIST), so this kernel holds no LSD-step code.
-constexpr uint32_t kRetryMax = 16;
-template <int BLOCK, int ITEMS, typename Op, int MODE, bool LIST = false>
+template <int BLOCK, int ITEMS, typename Op, int MODE, bool LIST = false, bool INL = false>
 __global__ __launch_bounds__(BLOCK)
 __attribute__((amdgpu_waves_per_eu(
     BLOCK >= 1024 && ITEMS <= 17 && MODE != kCntSmall ? 8 : (BLOCK == 256 && ITEMS <= 17 && MODE == kCntSmall) ? 7 : 1,
@@ -1821,9 +1933,9 @@ void k_bucket_count(const uint32_t* in, uint32_t* out, const uint32_t* __restric
       const uint32_t i = wbase + j * kWave + lane;
       k[j] = i < len ? load_stream(&in[(size_t)start + i]) : 0u;
     }
-    const uint32_t sev = bucket_count_place<BLOCK, ITEMS, MODE, Op>(k, s_cw, out, start, len, lbits, bias);
+    const uint32_t sev = bucket_count_place<BLOCK, ITEMS, MODE, Op, INL>(k, s_cw, out, start, len, lbits, bias);
     if (sev && threadIdx.x == 0) {  // (in == out keeps the bucket for the next try)
-      if (retry_list && sev <= kRetryMax)
+      if (!INL && retry_list && sev <= kRetryMax)
         retry_list[atomicAdd(retry_n, 1u)] = b;
       else
         ovf_list[atomicAdd(ovf_n, 1u)] = b;
@@ -1838,6 +1950,167 @@ void k_bucket_count(const uint32_t* in, uint32_t* out, const uint32_t* __restric
   } else {
     if (blockIdx.x >= min(*nb, nb_cap)) return;
     one(ilist ? ilist[blockIdx.x] : blockIdx.x);
+  }
+}
+
+// The counting placement for (u64 key, u32 payload) buckets (configs[4]'s
+// stable pair sort; round 5).  The bucket's pairs share
+// every key bit above lbits; x = bits [lbits - 16, lbits) of key - bias are
+// counted in 4096 u64 cells of 16 3-bit counts (+ the cell's pair count, then
+// its start, in the top 16 bits), one LDS atomic per pair, and each pair is
+// placed at cell start + the counts of the smaller x in its cell + its rank
+// among equal x (atomic order: arbitrary).  Its input slot (u16) goes beside
+// the key, so a run of equal x -- a field count >= 2, found in the cell words
+// the thread scanned (4096 uniform pairs over 2^16 values: ~128 runs of 2) --
+// is insertion-sorted by (key, slot): equal keys end in input order, i.e. the
+// sort is stable without a stable rank.  The keys are written out, then the
+// payloads are put at their input slots over the key array and gathered
+// through the slots.  LDS: 10 B per slot (the cells over the keys); 1024-thread
+// blocks of 5 slots (2^28 pairs) hold 2 blocks per CU at 63 VGPRs
+// (tools/pair_lab: 4096-pair buckets, the two 8-bit ballot steps + fix-up of
+// k_bucket_sort FIX 1762 us per 2^28 pairs, this 14.7-B/slot variant with
+// the payloads placed too 1477 us).  A 3-bit count that would wrap (8+ pairs
+// with equal x) writes nothing and lists the bucket (ovf_list) for
+// k_bucket_sort's LSD steps; a bucket over the block is listed (olist).
+template <int BLOCK, int ITEMS, typename Op>
+__global__ __launch_bounds__(BLOCK) void k_bucket_pairs(const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
+                                                        uint32_t* vout, const uint32_t* __restrict__ bstart,
+                                                        const uint32_t* __restrict__ blen,
+                                                        const uint32_t* __restrict__ nb, uint32_t nb_cap,
+                                                        const uint32_t* __restrict__ ilist, uint32_t lbits,
+                                                        uint64_t bias, uint32_t* __restrict__ oversized,
+                                                        uint32_t* __restrict__ olist, uint32_t olist_cap,
+                                                        uint32_t* __restrict__ ovf_n, uint32_t* __restrict__ ovf_list) {
+  constexpr int CAP = BLOCK * ITEMS, PER = kCntCells / BLOCK;
+  static_assert(CAP >= kCntCells && CAP < 65536 && kCntCells % BLOCK == 0, "cells over the keys; u16 slots");
+  __shared__ uint64_t s_k[CAP];
+  __shared__ uint16_t s_i[CAP];
+  __shared__ uint32_t s_ws[BLOCK / kWave];
+  if (blockIdx.x >= min(*nb, nb_cap)) return;
+  const uint32_t b = ilist ? ilist[blockIdx.x] : blockIdx.x;
+  const uint32_t start = bstart[b], len = blen[b];
+  if (len > (uint32_t)CAP) {
+    if (threadIdx.x == 0) {
+      const uint32_t slot = atomicAdd(oversized, 1u);
+      if (olist && slot < olist_cap) olist[slot] = b;
+    }
+    return;
+  }
+  if (len == 0) return;
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wbase = (tid / kWave) * ITEMS * kWave;
+  uint64_t* const cw = s_k;
+  auto ci = [&](uint32_t c) -> uint32_t { return (c % PER) * BLOCK + c / PER; };
+  const uint32_t fs = lbits - 16;
+  auto xval = [&](uint64_t key) -> uint32_t { return (uint32_t)((uint64_t)(key - bias) >> fs) & 0xFFFFu; };
+  auto valid = [&](int j) { return wbase + j * kWave + lane < len; };
+  uint64_t k[ITEMS];
+  uint32_t v[ITEMS], rk[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t i = wbase + j * kWave + lane;
+    k[j] = i < len ? load_stream(&kin[(size_t)start + i]) : 0ull;
+    v[j] = i < len ? load_stream(&vin[(size_t)start + i]) : 0u;
+  }
+#pragma unroll
+  for (int q = 0; q < PER; ++q) cw[q * BLOCK + tid] = 0ull;
+  __syncthreads();
+  bool ovf = false;
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j)
+    if (valid(j)) {
+      const uint32_t x = xval(k[j]), sh = 3u * (x & 15u);
+      const uint64_t old = atomicAdd((unsigned long long*)&cw[ci(x >> 4)], (1ull << sh) + (1ull << 48));
+      rk[j] = (uint32_t)(old >> sh) & 7u;
+      ovf |= rk[j] == 7u;
+    }
+  // (the overflow flag: bit 63 of cell 0; a pair count uses 13 of 16 bits)
+  if (__any(ovf) && lane == 0) atomicOr((unsigned long long*)&cw[0], 1ull << 63);
+  __syncthreads();
+  if (cw[0] >> 63) {
+    if (tid == 0) ovf_list[atomicAdd(ovf_n, 1u)] = b;  // nothing written: in == out keeps the bucket
+    return;
+  }
+  uint64_t c[PER];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    c[q] = cw[q * BLOCK + tid];
+    sum += (uint32_t)(c[q] >> 48);
+  }
+  uint32_t total;
+  uint32_t run = block_exclusive_scan<BLOCK>(sum, s_ws, total);
+  uint32_t cst[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    cst[q] = run;
+    cw[q * BLOCK + tid] = (c[q] & 0xFFFFFFFFFFFFull) | ((uint64_t)run << 48);
+    run += (uint32_t)(c[q] >> 48);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j)
+    if (valid(j)) {
+      const uint32_t x = xval(k[j]);
+      const uint64_t cc = cw[ci(x >> 4)];
+      rk[j] += (uint32_t)(cc >> 48) + field3_sum(cc & ((1ull << (3u * (x & 15u))) - 1ull));
+    }
+  __syncthreads();  // the pairs take the cells' place
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j)
+    if (valid(j)) {
+      s_k[rk[j]] = k[j];
+      s_i[rk[j]] = (uint16_t)(wbase + j * kWave + lane);
+    }
+  __syncthreads();
+  // runs of equal x: this thread's cells c = tid * PER + q start at cst[q]
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    constexpr uint64_t B0 = 0x249249249249ull;  // bit 0 of each 3-bit field
+    const uint64_t f = c[q] & 0xFFFFFFFFFFFFull;
+    uint64_t m = ((f >> 1) | (f >> 2)) & B0;  // fields whose count is >= 2
+    while (m) {
+      const uint32_t r = (uint32_t)__builtin_ctzll(m) / 3u;
+      m &= m - 1;
+      const uint32_t L = (uint32_t)(f >> (3u * r)) & 7u;
+      const uint32_t p = cst[q] + field3_sum(f & ((1ull << (3u * r)) - 1ull));
+      for (uint32_t a = 1; a < L; ++a) {  // stable by (key, input slot)
+        const uint64_t xk = s_k[p + a];
+        const uint16_t xi = s_i[p + a];
+        const uint64_t xb = xk - bias;
+        uint32_t z = a;
+        while (z > 0) {
+          const uint64_t yk = s_k[p + z - 1];
+          const uint64_t yb = yk - bias;
+          if (yb < xb || (yb == xb && s_i[p + z - 1] < xi)) break;
+          s_k[p + z] = yk;
+          s_i[p + z] = s_i[p + z - 1];
+          --z;
+        }
+        s_k[p + z] = xk;
+        s_i[p + z] = xi;
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t sl[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t p = wbase + j * kWave + lane;
+    sl[j] = 0u;
+    if (p < len) {
+      kout[(size_t)start + p] = s_k[p];
+      sl[j] = s_i[p];
+    }
+  }
+  __syncthreads();  // the payloads take the keys' place, at their input slots
+  uint32_t* const s_v = reinterpret_cast<uint32_t*>(s_k);
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) s_v[wbase + j * kWave + lane] = v[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t p = wbase + j * kWave + lane;
+    if (p < len) vout[(size_t)start + p] = s_v[sl[j]];
   }
 }
 
@@ -2451,7 +2724,9 @@ constexpr uint32_t kRsvMaxSlices = 4096;
 inline int rsv_pc_per(uint32_t nc) { return nc <= 128 ? 4 : nc <= 256 ? 8 : 16; }
 constexpr uint32_t kRsvLdsCum = 2048;
 template <int RADIX, int TILE, int PER, typename Op>
-__global__ __launch_bounds__(256) void k_rsv_sample_pc(const uint32_t* __restrict__ keys, const uint4* __restrict__ pieces,
+__global__ __launch_bounds__(256) void k_rsv_sample_pc(const uint32_t* __restrict__ keys,
+                                                       const uint8_t* __restrict__ keys8,
+                                                       const uint4* __restrict__ pieces,
                                                        const uint32_t* __restrict__ pcum, uint32_t np, uint32_t nseg,
                                                        uint32_t T0, uint32_t n, Op op, uint32_t* part,
                                                        uint32_t* __restrict__ rslice, uint32_t* __restrict__ rcur,
@@ -2550,7 +2825,11 @@ __global__ __launch_bounds__(256) void k_rsv_sample_pc(const uint32_t* __restric
     }
   }
 #pragma unroll
-  for (int q = 0; q < PER; ++q) kv[q] = ok[q] ? keys[(uint32_t)rank[q] + off[q]] : 0u;
+  for (int q = 0; q < PER; ++q) {
+    // (24-bit pieces: depth 0's digit lies in bits 16..23, the i8 plane)
+    const uint32_t at = (uint32_t)rank[q] + off[q];
+    kv[q] = !ok[q] ? 0u : keys8 ? (uint32_t)keys8[at] << 16 : keys[at];
+  }
 #pragma unroll
   for (int q = 0; q < PER; ++q)
     if (ok[q]) atomicAdd(&s_h[sg[q] * RADIX + op(kv[q])], 1u);
@@ -2912,6 +3191,37 @@ __global__ __launch_bounds__(256) void k_segment_copy2d(const uint32_t* __restri
   } else {
     const uint32_t m = (uint32_t)rem;
     for (uint32_t j = threadIdx.x; j < m; j += 256) dp[j] = sp[j];
+  }
+}
+
+// The same gather from 24-bit pieces (distrib.cpp "wire24"): key = hi |
+// lo8 << 16 | lo16; table src_off | dst_off | len | hi (top byte << 24) per
+// segment (the piece sort's fallback, and every round sort the reserved depth
+// 0 cannot take).
+__global__ __launch_bounds__(256) void k_segment_copy2d_planar(const uint16_t* __restrict__ s16,
+                                                               const uint8_t* __restrict__ s8,
+                                                               uint32_t* __restrict__ dst,
+                                                               const uint64_t* __restrict__ tab, uint32_t nseg) {
+  const uint32_t s = blockIdx.y;
+  const uint64_t len = tab[2 * nseg + s];
+  const uint64_t a = (uint64_t)blockIdx.x * kSegPiece;
+  if (a >= len) return;
+  const uint64_t so = tab[s] + a;
+  const uint32_t hi = (uint32_t)tab[3 * nseg + s];
+  uint32_t* dp = dst + tab[nseg + s] + a;
+  const uint64_t rem = len - a;
+  if (rem >= (uint64_t)kSegPiece) {
+    uint32_t v[kSegPiece / 256];
+#pragma unroll
+    for (int j = 0; j < kSegPiece / 256; ++j) {
+      const uint64_t i = so + threadIdx.x + j * 256;
+      v[j] = hi | ((uint32_t)s8[i] << 16) | (uint32_t)s16[i];
+    }
+#pragma unroll
+    for (int j = 0; j < kSegPiece / 256; ++j) dp[threadIdx.x + j * 256] = v[j];
+  } else {
+    const uint32_t m = (uint32_t)rem;
+    for (uint32_t j = threadIdx.x; j < m; j += 256) dp[j] = hi | ((uint32_t)s8[so + j] << 16) | (uint32_t)s16[so + j];
   }
 }
 
@@ -3527,6 +3837,29 @@ inline bool bucket2_on() {
   return on;
 }
 
+// kCnt2F's lightly overflowed buckets retried inline with 3-bit half cells
+// (retry3_halves) instead of by a LIST launch: LIBSORT_BUCKET2_INLINE=1 (A/B
+// only: measured 449 -> 956 us for the bucket phase of a 2^28 sort, 3
+// interleaved runs each, profiles/r05d_bucket2_inline_ab.txt -- the rarely
+// taken branch costs every block its registers and occupancy)
+inline bool bucket2_inline_on() {
+  static const bool on = [] {
+    const char* s = getenv("LIBSORT_BUCKET2_INLINE");
+    return s && s[0] == '1';
+  }();
+  return on;
+}
+
+// (u64 key, u32 payload) buckets by the counting placement (k_bucket_pairs);
+// LIBSORT_PAIR_COUNT=0 keeps the LSD steps + fix-up (A/B).
+inline bool pair_count_on() {
+  static const bool on = [] {
+    const char* s = getenv("LIBSORT_PAIR_COUNT");
+    return !(s && s[0] == '0');
+  }();
+  return on;
+}
+
 inline bool dstream_on() {
   static const bool on = [] {
     const char* s = getenv("LIBSORT_DSTREAM");
@@ -3851,6 +4184,11 @@ struct HybPieces {
   int depths;           // digit passes (the bucket sort covers W - BITS * depths bits)
   double fill;          // populated segments / nseg (sizes the bucket blocks)
   const uint32_t* cum;  // [np + 1] keys before each piece (the reserved depth 0's sampler)
+  // 24-bit pieces (sort_pieces_planar_u32): the low 16 bits, bits 16..23, and
+  // per segment its keys' top byte << 24; null: u32 keys in `in`
+  const uint16_t* i16 = nullptr;
+  const uint8_t* i8 = nullptr;
+  const uint32_t* seghi = nullptr;
 };
 
 // Words of the reserved depth 0's slices: n keys plus each slice's sampled
@@ -3963,6 +4301,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     rmode = 0;
   }
   const bool rsv = rmode != 0;
+  // 24-bit pieces are read by the reserved depth 0 only: otherwise the
+  // caller's gather (which unpacks them) and LSD sort
+  if (pc && pc->i8 && !rsv) return hipSuccess;
   uint32_t rseq = 0;  // the sampler's sequence word (wait_host_word)
   uint32_t sseq = 0;  // the last depth's children (bucket stats)
   // segments of depth k (each child has at most one partial tile)
@@ -4016,7 +4357,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       auto smp = rper == 4 ? k_rsv_sample_pc<RADIX, TILE, 4, Op>
                  : rper == 8 ? k_rsv_sample_pc<RADIX, TILE, 8, Op> : k_rsv_sample_pc<RADIX, TILE, 16, Op>;
       hipLaunchKernelGGL(smp, dim3(kRsvRanges * kRsvBlocks), dim3(256), 0, st,
-                         reinterpret_cast<const uint32_t*>(in), reinterpret_cast<const uint4*>(pc->dev), pc->cum,
+                         reinterpret_cast<const uint32_t*>(in), pc->i8, reinterpret_cast<const uint4*>(pc->dev), pc->cum,
                          pc->np, nseg0, T0, (uint32_t)n, op0, rpart, rslice, rcur, ws.hyb_host, Cn0,
                          BITS == 4 ? tb1 * (uint32_t)RADIX : 0u, ws.tticket + 32, ctr, NB, rmode == 2, rseq);
     } else {
@@ -4064,6 +4405,11 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
         // Reserved depth 0 (sampled above): the pass reserves its runs in the
         // slices; the next depth's tiles and child starts from the cursors
         HybridGeo g0{tiles[0], ctr, nullptr, nullptr, nullptr, rcur, rslice, ctr + 14, rns};
+        if (pc) {
+          g0.i16 = pc->i16;
+          g0.i8 = pc->i8;
+          g0.seghi = pc->seghi;
+        }
         {
           ScopedTimer tm("tilepass", st, n);
           if (pc)
@@ -4219,6 +4565,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     // 64-bit keys: on-chip steps over the top 16 of the 48 bucket bits, then
     // the tie fix-up (k_bucket_sort FIX)
     constexpr int FIXB = sizeof(K) == 8 ? LIBSORT_BUCKET64_FIX : 0;
+    constexpr bool kPairCnt = sizeof(K) == 8 && std::is_same<V, uint32_t>::value && FIXB > 0;
     // the second size's grid: the buckets over the first block, as planned
     // (k_hyb_children's count, the same cap as the first launch lists by);
     // none: no launch
@@ -4235,6 +4582,12 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       // to the LSD steps (flist2, count ctr[7]); other modes list straight
       // for the LSD steps (flist)
       const bool two = C && lbits == 16 && BB == 256 && cls <= 3 && bucket2_on();
+      // (u64 key, u32 payload) pairs: k_bucket_pairs (LIBSORT_PAIR_COUNT=0:
+      // the LSD steps + fix-up of k_bucket_sort FIX)
+      const bool pcnt = kPairCnt && lbits >= 16 && pair_count_on();
+      // (inline: the retry list holds only the buckets over the first block,
+      // so the 3-bit LIST launch runs only when the planning counted any)
+      const bool inl = two && bucket2_inline_on();
       uint32_t* const lsd_n = two ? ctr + 7 : ctr + 15;  // the LSD steps' list
       uint32_t* const lsd_l = two ? flist2 : flist;
       uint32_t* const rty_n = two ? ctr + 15 : nullptr;
@@ -4250,12 +4603,24 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
     else if (lbits != 16)                                                                                        \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt3>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize,  \
                          NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l);                    \
+    else if (B == 256 && two && inl)                                                                             \
+      hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt2F, false, true>), dim3(G), dim3(B), 0, st, ci_, co_,    \
+                         bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l);     \
     else if (B == 256 && two)                                                                                    \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt2F>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize, \
                          NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l);                    \
     else                                                                                                         \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt3F>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize, \
                          NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l);                    \
+  } else if (pcnt) {                                                                                             \
+    if constexpr (kPairCnt) {                                                                                    \
+      /* (u64, u32) pairs: the counting placement, 1024-thread blocks of at least the slots asked for */         \
+      constexpr int PI_ = std::max(4, ((B) * (I) + 1023) / 1024);                                                \
+      hipLaunchKernelGGL((k_bucket_pairs<1024, PI_, Op>), dim3(G), dim3(1024), 0, st,                            \
+                         reinterpret_cast<const uint64_t*>(out), reinterpret_cast<uint64_t*>(out),               \
+                         reinterpret_cast<const uint32_t*>(vout), reinterpret_cast<uint32_t*>(vout), bstart,     \
+                         nsize, NBP, CAPN, IL, lbits, (uint64_t)bias, OV, OL, kListCap, ctr + 15, flist);        \
+    }                                                                                                            \
   } else {                                                                                                       \
     hipLaunchKernelGGL((k_bucket_sort<BITS, B, (I), Op, K, V, FIXB>), dim3(G), dim3(B), 0, st, out, out, vout, vout, \
                        bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, kListCap);                             \
@@ -4279,7 +4644,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       // grid over the list (none listed: the blocks read the count and exit)
 #define LS_BSL(B, I)                                                                                               \
   if constexpr (C) {                                                                                               \
-    if (two) {                                                                                                     \
+    if (two && (!inl || n2 > 0)) {                                                                                 \
       hipLaunchKernelGGL((k_bucket_count<256, (I), Op, kCnt3F, true>),                                             \
                          dim3(std::min<uint32_t>(NB, (uint32_t)std::max(1, ws.num_cus) * 5)), dim3(256), 0, st,    \
                          reinterpret_cast<const uint32_t*>(out), reinterpret_cast<uint32_t*>(out), bstart, nsize,  \
@@ -4291,6 +4656,15 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
                        dim3(std::min<uint32_t>(NB, (uint32_t)std::max(1, ws.num_cus) * 2)), dim3(B), 0, st, out,   \
                        out, vout, vout, bstart, nsize, lsd_n, NB, lsd_l, lbits, bias, ctr + 14, nullptr, 0u);       \
     LS_TRY(hipGetLastError());                                                                                     \
+  } else if constexpr (kPairCnt) {                                                                                 \
+    if (pcnt) {                                                                                                    \
+      /* the pairs whose 3-bit counts would wrap (8+ equal x; their length <= cap, the planning's bound):        \
+         the LSD steps + fix-up, persistent over flist */                                                          \
+      hipLaunchKernelGGL((k_bucket_sort<BITS, B, (I), Op, K, V, FIXB, true>),                                      \
+                         dim3(std::min<uint32_t>(NB, (uint32_t)std::max(1, ws.num_cus) * 2)), dim3(B), 0, st, out, \
+                         out, vout, vout, bstart, nsize, ctr + 15, NB, flist, lbits, bias, ctr + 14, nullptr, 0u);  \
+      LS_TRY(hipGetLastError());                                                                                   \
+    }                                                                                                              \
   }
       switch (cls) {
         case 0: LS_BS2(9); LS_TRY(hipGetLastError()); LS_BSL(BB, (15 * 256 + BB - 1) / BB); break;
@@ -4405,12 +4779,23 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
 // (the hybrid's ~10 launches per depth outweigh its saved passes).
 constexpr size_t kPiecesMinKeys = 1ull << 20;
 
-hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n,
-                           const uint64_t* off, const uint64_t* len, const uint32_t* seg, size_t np, uint32_t nseg,
-                           int bits, int digit_bits, hipStream_t st, uint32_t bias) {
+namespace {
+// 24-bit pieces (sort_pieces_planar_u32): planes of the low 16 bits and bits
+// 16..23; the keys of segment s have top byte hi0 + s
+struct PlanarPieces {
+  const uint16_t* i16 = nullptr;
+  const uint8_t* i8 = nullptr;
+  uint32_t hi0 = 0;
+};
+
+hipError_t sort_pieces_impl(Workspace& ws, const uint32_t* in, const PlanarPieces& pl, uint32_t* out, uint32_t* tmp,
+                            size_t n, const uint64_t* off, const uint64_t* len, const uint32_t* seg, size_t np,
+                            uint32_t nseg, int bits, int digit_bits, hipStream_t st, uint32_t bias) {
+  const bool planar = pl.i8 != nullptr;
   if (n == 0) return hipSuccess;
   if (n > 0xffffffffull || in == out || tmp == out || tmp == in || nseg == 0 || nseg > (1u << 20) || bits < 0 ||
-      bits > 32 || (digit_bits != 4 && digit_bits != 8))
+      bits > 32 || (digit_bits != 4 && digit_bits != 8) ||
+      (planar && (bits != 24 || bias != 0 || !pl.i16 || pl.hi0 + nseg > 256u)))
     return hipErrorInvalidValue;
   // the non-empty pieces, checked: segments non-decreasing and < nseg, offsets
   // below 2^32, lengths summing to n
@@ -4465,10 +4850,14 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   // first tile) | ctile0[nseg + 1] | cstart[nseg] | cum[K + 1] (keys before
   // each piece) | (8-byte aligned) the gather table of the fallback:
   // src_off[K] | dst_off[K] | len[K] (uint64)
+  // (24-bit pieces: a 4th gather column, each piece's top byte << 24, and
+  // after it seghi[nseg] (u32) for the reserved depth 0's loader)
   const uint32_t TILE = (uint32_t)(tp_block<uint32_t>(digit_bits) * tp_items<uint32_t>(digit_bits));
   const size_t w32 = 4 * (size_t)K + 2 * (size_t)nseg + 1 + (size_t)K + 1;
   const size_t g64 = (w32 + 1) / 2;  // first uint64 word of the gather table
-  LS_TRY(ws.ensure_seg(g64 + 3 * (size_t)K));
+  const size_t gcols = planar ? 4 : 3;
+  const size_t words = g64 + gcols * (size_t)K + (planar ? ((size_t)nseg + 1) / 2 : 0);
+  LS_TRY(ws.ensure_seg(words));
   LS_TRY(hipEventSynchronize(ws.seg_evt));  // the staging may still feed the previous upload
   uint32_t* h32 = reinterpret_cast<uint32_t*>(ws.seg_host);
   uint64_t* hg = ws.seg_host + g64;
@@ -4499,12 +4888,15 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
       hg[i] = off[p];
       hg[K + i] = dpos[cs];
       hg[2 * (size_t)K + i] = len[p];
+      if (planar) hg[3 * (size_t)K + i] = (uint64_t)(pl.hi0 + seg[p]) << 24;
       dpos[cs] += len[p];
     }
   }
   pcum[K] = run;
-  LS_TRY(hipMemcpyAsync(ws.seg_dev, ws.seg_host, (g64 + 3 * (size_t)K) * sizeof(uint64_t), hipMemcpyHostToDevice,
-                        st));
+  uint32_t* shi = reinterpret_cast<uint32_t*>(hg + gcols * (size_t)K);
+  if (planar)
+    for (uint32_t i2 = 0; i2 < K; ++i2) shi[cseg[seg[keep[i2]]]] = (pl.hi0 + seg[keep[i2]]) << 24;
+  LS_TRY(hipMemcpyAsync(ws.seg_dev, ws.seg_host, words * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   // seg_evt guards the staging against the next call; a sort the hybrid
   // handled has already waited for a kernel behind this copy (the bucket
   // stats' sequence word), so only the other paths record it (an event
@@ -4512,6 +4904,11 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   if (depths > 0) {
     const uint32_t* dev32 = reinterpret_cast<const uint32_t*>(ws.seg_dev);
     HybPieces pc{dev32, K, nseg, tile, depths, (double)npop / nseg, dev32 + (pcum - h32)};
+    if (planar) {
+      pc.i16 = pl.i16;
+      pc.i8 = pl.i8;
+      pc.seghi = reinterpret_cast<const uint32_t*>(ws.seg_dev + g64 + gcols * (size_t)K);
+    }
     bool handled = false;
     NoValue* nv = nullptr;
     hipError_t e;
@@ -4537,10 +4934,34 @@ hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uin
   }
   LS_TRY(hipEventRecord(ws.seg_evt, st));
   // small or skewed: gather the pieces into segment order, LSD sort in place
-  // (bits == 0: the segments are single values, already in order)
-  LS_TRY(segment_copy_dev_u32(in, out, ws.seg_dev + g64, K, maxlen, n, st));
+  // (bits == 0: the segments are single values, already in order); 24-bit
+  // pieces are unpacked by the gather
+  if (planar) {
+    if (K > 65535) return hipErrorInvalidValue;
+    ScopedTimer tm("segcopy", st, n);
+    hipLaunchKernelGGL(k_segment_copy2d_planar, dim3((uint32_t)((maxlen + kSegPiece - 1) / kSegPiece), K), dim3(256),
+                       0, st, pl.i16, pl.i8, out, ws.seg_dev + g64, K);
+    LS_TRY(hipGetLastError());
+  } else {
+    LS_TRY(segment_copy_dev_u32(in, out, ws.seg_dev + g64, K, maxlen, n, st));
+  }
   if (bits == 0) return hipSuccess;
   return sort_impl<uint32_t, NoValue>(ws, out, out, tmp, nullptr, nullptr, nullptr, n, 0, 32, digit_bits, st);
+}
+}  // namespace
+
+hipError_t sort_pieces_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* tmp, size_t n,
+                           const uint64_t* off, const uint64_t* len, const uint32_t* seg, size_t np, uint32_t nseg,
+                           int bits, int digit_bits, hipStream_t st, uint32_t bias) {
+  return sort_pieces_impl(ws, in, PlanarPieces{}, out, tmp, n, off, len, seg, np, nseg, bits, digit_bits, st, bias);
+}
+
+hipError_t sort_pieces_planar_u32(Workspace& ws, const uint16_t* in16, const uint8_t* in8, uint32_t hi0,
+                                  uint32_t* out, uint32_t* tmp, size_t n, const uint64_t* off, const uint64_t* len,
+                                  const uint32_t* seg, size_t np, uint32_t nseg, int digit_bits, hipStream_t st) {
+  // (in: any pointer distinct from out and tmp; the planes are read instead)
+  return sort_pieces_impl(ws, reinterpret_cast<const uint32_t*>(in16), PlanarPieces{in16, in8, hi0}, out, tmp, n, off,
+                          len, seg, np, nseg, 24, digit_bits, st, 0u);
 }
 
 hipError_t sort_pairs_u32_u32(Workspace& ws, const uint32_t* kin, const uint32_t* vin, uint32_t* kout,
@@ -4668,7 +5089,7 @@ namespace {
 template <int BITS, typename K, typename V, typename Op>
 hipError_t partition_op_impl(Workspace& ws, const K* in, K* out, const V* vin, V* vout, size_t n, Op op,
                              const Workspace::PartToken& tok, int nbuckets, uint32_t* d_bounds, hipStream_t st,
-                             int phase) {
+                             int phase, uint16_t* o16 = nullptr, uint8_t* o8 = nullptr) {
   constexpr int RADIX = 1 << BITS;
   constexpr int B = tp_block<K>(BITS);
   const uint32_t tiles = tp_tiles<K>(n, BITS);
@@ -4689,9 +5110,12 @@ hipError_t partition_op_impl(Workspace& ws, const K* in, K* out, const V* vin, V
   ws.part_pending.valid = false;
   {
     ScopedTimer tm("partition", st, n);
+    HybridGeo g{};
+    g.o16 = o16;  // (24-bit planes instead of out: the multi-GPU exchange)
+    g.o8 = o8;
     hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(BITS), K, V, false, Op>), dim3(tiles), dim3(B), 0, st, in,
                        out, vin, vout, (uint32_t)n, op, RadixDigit{0u, 1u}, ws.tc[0], (const uint32_t*)ws.tb,
-                       (const uint32_t*)tiles_digit_starts(ws, tiles, BITS), ws.tc[1], HybridGeo{});
+                       (const uint32_t*)tiles_digit_starts(ws, tiles, BITS), ws.tc[1], g);
     LS_TRY(hipGetLastError());
   }
   return hipSuccess;
@@ -4794,6 +5218,17 @@ hipError_t partition_lut_u32(Workspace& ws, const uint32_t* in, uint32_t* out, s
                              int lut_shift, int nbuckets, uint32_t* d_bounds, hipStream_t st, int phase) {
   return partition_lut_any<uint32_t, NoValue>(ws, in, out, nullptr, nullptr, n, d_lut, lut_shift, nbuckets, d_bounds,
                                               st, phase);
+}
+
+hipError_t partition_lut_planar_u32(Workspace& ws, const uint32_t* in, uint16_t* o16, uint8_t* o8, size_t n,
+                                   const uint8_t* d_lut, int lut_shift, int nbuckets, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (n > 0xffffffffull || !in || !o16 || !o8 || lut_shift != 24 || nbuckets != 256 || !d_lut) return hipErrorInvalidValue;
+  const Workspace::PartToken tok{in, nullptr, n, d_lut, lut_shift, nbuckets, 0, st, true};
+  // (out: unused -- the planes are written; the scatter follows partition_lut_u32's count call)
+  return partition_op_impl<8, uint32_t, NoValue>(ws, in, reinterpret_cast<uint32_t*>(o16), nullptr, nullptr, n,
+                                                 LutDigit{d_lut, (uint32_t)lut_shift, 255u, nullptr}, tok, nbuckets,
+                                                 nullptr, st, kPartScatter, o16, o8);
 }
 
 hipError_t partition_lut_pairs_u64_u32(Workspace& ws, const uint64_t* kin, const uint32_t* vin, uint64_t* kout,

@@ -95,6 +95,7 @@ _SIGS = [
     ("libsortDistribSortU32", ctypes.c_int, [ctypes.c_int, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32]),
     ("libsortDistribSortPairsU64U32", ctypes.c_int,
      [ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32]),
+    ("libsortDistribLastBytes", ctypes.c_int, [ctypes.c_int, _u64p]),
     ("libsortDistribPlanDigits", ctypes.c_int,
      [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, _vp, _vp]),
     ("libsortDistribRangeDigit", ctypes.c_int,

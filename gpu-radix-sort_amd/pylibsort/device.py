@@ -428,7 +428,15 @@ def merge_u32(a, b, out=None):
     return out
 
 
-LIBSORT_DISTRIB_LSD, LIBSORT_DISTRIB_COPY, LIBSORT_DISTRIB_SELF_RCCL = 1, 2, 4
+LIBSORT_DISTRIB_LSD, LIBSORT_DISTRIB_COPY, LIBSORT_DISTRIB_SELF_RCCL, LIBSORT_DISTRIB_WIRE32 = 1, 2, 4, 8
+
+
+def distrib_last_bytes(nranks):
+    """Bytes each rank sent to the others in the last distributed sort
+    (libsortDistribLastBytes), as a list of ints."""
+    arr = (ctypes.c_uint64 * nranks)()
+    _check(_lib().libsortDistribLastBytes(int(nranks), arr), "libsortDistribLastBytes")
+    return [int(x) for x in arr]
 
 
 def distrib_sort_u32(shards, flags=0):

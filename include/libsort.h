@@ -277,6 +277,12 @@ LIBSORT_API bool gpuDistribSort(uint32_t* h_in, size_t len, int ngpu);
 #define LIBSORT_DISTRIB_LSD 1u
 #define LIBSORT_DISTRIB_COPY 2u
 #define LIBSORT_DISTRIB_SELF_RCCL 4u
+/* LIBSORT_DISTRIB_WIRE32: keys cross the links as 32-bit words.  By default
+ * the top-digit rounds at 4-bit digits send 24 bits per key (two planes: the
+ * low 16 bits and bits 16..23; the top byte is the partition digit the piece
+ * already names), 3 bytes instead of 4; LIBSORT_DISTRIB_WIRE24=0 in the
+ * environment does the same as this flag. */
+#define LIBSORT_DISTRIB_WIRE32 8u
 LIBSORT_API bool libsortDistribSortU32(int nranks, const int* devices, const uint32_t* const* d_in,
                                        const size_t* n_in, uint32_t* const* d_out, size_t* n_out,
                                        uint32_t flags);
@@ -288,6 +294,12 @@ LIBSORT_API bool libsortDistribSortU32(int nranks, const int* devices, const uin
  * order: shard 0 first).  The top-digit rounds on the key's top 8 bits with a
  * stable pair sort per round.  flags: LIBSORT_DISTRIB_COPY /
  * LIBSORT_DISTRIB_SELF_RCCL (not _LSD).  Synchronous. */
+/* Bytes each rank sent to the other ranks in the exchange rounds (its own
+ * pieces and the final re-cut's surplus keys excluded) in the last
+ * libsortDistribSort* / gpuDistribSort call over nranks ranks:
+ * per_rank[0..nranks).  false if none ran. */
+LIBSORT_API bool libsortDistribLastBytes(int nranks, uint64_t* per_rank);
+
 LIBSORT_API bool libsortDistribSortPairsU64U32(int nranks, const int* devices, const uint64_t* const* d_kin,
                                                const uint32_t* const* d_vin, const size_t* n_in,
                                                uint64_t* const* d_kout, uint32_t* const* d_vout, size_t* n_out,

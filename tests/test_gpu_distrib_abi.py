@@ -23,7 +23,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
-LSD, COPY, SELF_RCCL = 1, 2, 4
+LSD, COPY, SELF_RCCL, WIRE32 = 1, 2, 4, 8
 
 
 @pytest.fixture(scope="module")
@@ -173,9 +173,11 @@ def test_host_entry_point_golden(D, golden):
 
 
 @pytest.mark.slow
-def test_reference_size_over_rccl(D, golden):
+def test_reference_size_over_rccl(D, golden, bits):
     """configs[1]'s 2^28 keys through the distributed path (one RCCL rank,
-    every piece through RCCL): the reference's sorted sha256."""
+    every piece through RCCL): the reference's sorted sha256.  At 4-bit digits
+    the keys cross RCCL as 24-bit planes (the default wire format), at 8-bit
+    as 32-bit words."""
     import pylibsort
     g, _ = golden
     n = 1 << 28
@@ -184,6 +186,34 @@ def test_reference_size_over_rccl(D, golden):
     h = hashlib.sha256(out.cpu().numpy().view(np.uint32).tobytes()).hexdigest()[:16]
     assert h == g["sha256_prefix"][str(n)]["sorted"]
     assert pylibsort.lib().libsortDeviceErrors() == 0
+
+
+@pytest.mark.parametrize("R", [1, 3, 8])
+@pytest.mark.parametrize("n", [(1 << 21) + 333, (1 << 23) + 77])
+def test_wire24(D, oracle_mod, R, n):
+    """24-bit keys on the wire: the partition scatter
+    writes each key's low 16 bits and bits 16..23 as two planes, the rounds
+    move 3 bytes per key, and the round sorts' reserved depth 0 (or, for
+    rounds below 2^20 keys, the unpacking gather) rebuilds the key with the
+    piece's digit as its top byte.  Exact against the oracle at both wire
+    formats; every rank's exchange bytes are exactly 3/4 of the 32-bit
+    format's (R = 1: every piece through one RCCL rank, nothing counted)."""
+    import pylibsort
+    prev = pylibsort.setDigitBits(4)
+    try:
+        x = oracle_mod.pcg(n, first=9)
+        flags = SELF_RCCL if R == 1 else COPY
+        o24 = _run(D, x, R, flags)
+        b24 = D.distrib_last_bytes(R)
+        o32 = _run(D, x, R, flags | WIRE32)
+        b32 = D.distrib_last_bytes(R)
+        _check(oracle_mod, x, o24, R, False)
+        _check(oracle_mod, x, o32, R, False)
+        if R > 1:
+            assert sum(b32) > 0 and all(4 * a == 3 * b for a, b in zip(b24, b32)), (b24, b32)
+        assert pylibsort.lib().libsortDeviceErrors() == 0
+    finally:
+        pylibsort.setDigitBits(prev)
 
 
 @pytest.mark.slow

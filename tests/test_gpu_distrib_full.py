@@ -75,9 +75,21 @@ def _keys_input(D, cuts):
     return shards
 
 
-@pytest.mark.parametrize("R, flags, ragged", [(8, COPY, False), (8, COPY | LSD, False), (5, COPY, True)],
-                         ids=["msd-8x2^29", "lsd-8x2^29", "msd-5ragged"])
-def test_config3_full(D, R, flags, ragged):
+@pytest.mark.parametrize("R, flags, ragged, bits", [(8, COPY, False, 8), (8, COPY, False, 4), (8, COPY | LSD, False, 8),
+                                                     (5, COPY, True, 4)],
+                         ids=["msd-8x2^29", "msd-8x2^29-wire24", "lsd-8x2^29", "msd-5ragged-wire24"])
+def test_config3_full(D, R, flags, ragged, bits):
+    """bits = the round sorts' digit width; at 4 the exchange carries 24-bit
+    keys (the default wire format of the top-digit rounds)."""
+    import pylibsort
+    prev = pylibsort.setDigitBits(bits)
+    try:
+        _config3_full(D, R, flags, ragged)
+    finally:
+        pylibsort.setDigitBits(prev)
+
+
+def _config3_full(D, R, flags, ragged):
     import pylibsort
     N = 1 << 32
     if ragged:  # deliberately unequal input shards, one of 2^31 + 5 keys

@@ -158,6 +158,178 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
   }
 }
 
+// cnt2: the same placement with 10 B of LDS per pair instead of 14: keys and
+// slots are placed (cells over the keys); after the runs are fixed the keys
+// are written out, then the payloads are put at their INPUT slots over the
+// key array and gathered through the slots (vout[p] = s_v[s_i[p]]).
+template <int BLOCK, int ITEMS, int WPE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE, 8))) void k_pair_cnt2(
+    const uint64_t* kin, const uint32_t* vin, uint64_t* kout, uint32_t* vout, const uint32_t* bstart,
+    const uint32_t* blen, const uint32_t* nb, uint32_t lbits, uint32_t* ovf_n, uint32_t* ovf_list) {
+  constexpr int CAP = BLOCK * ITEMS, PER = kCntCells / BLOCK;
+  static_assert(CAP >= kCntCells, "cells overlay the keys");
+  __shared__ uint64_t s_k[CAP];
+  __shared__ uint16_t s_i[CAP];
+  __shared__ uint32_t s_ws[BLOCK / kWave];
+  if (blockIdx.x >= *nb) return;
+  const uint32_t b = blockIdx.x, start = bstart[b], len = blen[b];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid / 64;
+  const uint32_t wbase = w * ITEMS * kWave;
+  uint64_t* const cw = s_k;
+  auto ci = [&](uint32_t c) -> uint32_t { return (c % PER) * BLOCK + c / PER; };
+  const uint32_t fs = lbits - 16;
+  uint64_t k[ITEMS];
+  uint32_t v[ITEMS], rk[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t i = wbase + j * kWave + lane;
+    k[j] = i < len ? load_stream(&kin[(size_t)start + i]) : 0ull;
+    v[j] = i < len ? load_stream(&vin[(size_t)start + i]) : 0u;
+  }
+#pragma unroll
+  for (int q = 0; q < PER; ++q) cw[q * BLOCK + tid] = 0ull;
+  __syncthreads();
+  bool ovf = false;
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j)
+    if (wbase + j * kWave + lane < len) {
+      const uint32_t x = (uint32_t)(k[j] >> fs) & 0xFFFFu, sh = 3u * (x & 15u);
+      const uint64_t old = atomicAdd((unsigned long long*)&cw[ci(x >> 4)], (1ull << sh) + (1ull << 48));
+      rk[j] = (uint32_t)(old >> sh) & 7u;
+      ovf |= rk[j] == 7u;
+    }
+  if (__any(ovf) && lane == 0) atomicOr((unsigned long long*)&cw[0], 1ull << 63);
+  __syncthreads();
+  if (cw[0] >> 63) {
+    if (tid == 0) ovf_list[atomicAdd(ovf_n, 1u)] = b;
+    return;
+  }
+  uint64_t c[PER];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    c[q] = cw[q * BLOCK + tid];
+    sum += (uint32_t)(c[q] >> 48);
+  }
+  uint32_t total;
+  uint32_t run = block_exclusive_scan<BLOCK>(sum, s_ws, total);
+  uint32_t cst[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    cst[q] = run;
+    cw[q * BLOCK + tid] = (c[q] & 0xFFFFFFFFFFFFull) | ((uint64_t)run << 48);
+    run += (uint32_t)(c[q] >> 48);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j)
+    if (wbase + j * kWave + lane < len) {
+      const uint32_t x = (uint32_t)(k[j] >> fs) & 0xFFFFu;
+      const uint64_t cc = cw[ci(x >> 4)];
+      rk[j] += (uint32_t)(cc >> 48) + field3_sum(cc & ((1ull << (3u * (x & 15u))) - 1ull));
+    }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j)
+    if (wbase + j * kWave + lane < len) {
+      s_k[rk[j]] = k[j];
+      s_i[rk[j]] = (uint16_t)(wbase + j * kWave + lane);
+    }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    constexpr uint64_t B0 = 0x249249249249ull;
+    const uint64_t f = c[q] & 0xFFFFFFFFFFFFull;
+    uint64_t m = ((f >> 1) | (f >> 2)) & B0;
+    while (m) {
+      const uint32_t r = (uint32_t)__builtin_ctzll(m) / 3u;
+      m &= m - 1;
+      const uint32_t L = (uint32_t)(f >> (3u * r)) & 7u;
+      const uint32_t p = cst[q] + field3_sum(f & ((1ull << (3u * r)) - 1ull));
+      for (uint32_t a = 1; a < L; ++a) {
+        const uint64_t xk = s_k[p + a];
+        const uint16_t xi = s_i[p + a];
+        uint32_t z = a;
+        while (z > 0) {
+          const uint64_t yk = s_k[p + z - 1];
+          if (yk < xk || (yk == xk && s_i[p + z - 1] < xi)) break;
+          s_k[p + z] = yk;
+          s_i[p + z] = s_i[p + z - 1];
+          --z;
+        }
+        s_k[p + z] = xk;
+        s_i[p + z] = xi;
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t sl[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t p = wbase + j * kWave + lane;
+    if (p < len) {
+      kout[(size_t)start + p] = s_k[p];
+      sl[j] = s_i[p];
+    }
+  }
+  __syncthreads();
+  uint32_t* const s_v = reinterpret_cast<uint32_t*>(s_k);
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) s_v[wbase + j * kWave + lane] = v[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t p = wbase + j * kWave + lane;
+    if (p < len) vout[(size_t)start + p] = s_v[sl[j]];
+  }
+}
+
+// copy floor of cnt2's footprint (10 B per pair)
+template <int BLOCK, int ITEMS>
+__global__ __launch_bounds__(BLOCK) void k_pair_copy2(const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
+                                                      uint32_t* vout, const uint32_t* bstart, const uint32_t* blen,
+                                                      const uint32_t* nb) {
+  constexpr int CAP = BLOCK * ITEMS;
+  __shared__ uint64_t s_k[CAP];
+  __shared__ uint16_t s_i[CAP];
+  if (blockIdx.x >= *nb) return;
+  const uint32_t b = blockIdx.x, start = bstart[b], len = blen[b];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid / 64;
+  const uint32_t wbase = w * ITEMS * kWave;
+  uint64_t k[ITEMS];
+  uint32_t v[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t i = wbase + j * kWave + lane;
+    k[j] = i < len ? load_stream(&kin[(size_t)start + i]) : 0ull;
+    v[j] = i < len ? load_stream(&vin[(size_t)start + i]) : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t i = wbase + j * kWave + lane;
+    s_k[(i * 33) % CAP] = k[j];
+    s_i[(i * 33) % CAP] = (uint16_t)i;
+  }
+  __syncthreads();
+  uint32_t sl[ITEMS];
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t p = wbase + j * kWave + lane;
+    if (p < len) kout[(size_t)start + p] = s_k[p];
+    sl[j] = s_i[p];
+  }
+  __syncthreads();
+  uint32_t* const s_v = reinterpret_cast<uint32_t*>(s_k);
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) s_v[wbase + j * kWave + lane] = v[j];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) {
+    const uint32_t p = wbase + j * kWave + lane;
+    if (p < len) vout[(size_t)start + p] = s_v[sl[j] % CAP];
+  }
+}
+
 template <int BLOCK, int ITEMS>
 __global__ __launch_bounds__(BLOCK) void k_pair_copy(const uint64_t* kin, const uint32_t* vin, uint64_t* kout,
                                                      uint32_t* vout, const uint32_t* bstart, const uint32_t* blen,
@@ -231,7 +403,15 @@ int main(int argc, char** argv) {
 #define CNT(B, I, W) vs.push_back({"cnt " #B "x" #I " wpe" #W, true, [&] {                                   \
     CK(hipMemsetAsync(ovn, 0, 4, st));                                                                          \
     hipLaunchKernelGGL((k_pair_cnt<B, I, W>), dim3(m), dim3(B), 0, st, kin, vin, kout, vout, bs, bl, nb, 48u, ovn, ovl); }});
-  CNT(512, 9, 1) CNT(512, 9, 4) CNT(1024, 5, 1) CNT(1024, 5, 8) CNT(256, 17, 1)
+  CNT(512, 9, 1) CNT(1024, 5, 1) CNT(1024, 5, 8)
+#define CNT2(B, I, W) vs.push_back({"cnt2 " #B "x" #I " wpe" #W, true, [&] {                                 \
+    CK(hipMemsetAsync(ovn, 0, 4, st));                                                                          \
+    hipLaunchKernelGGL((k_pair_cnt2<B, I, W>), dim3(m), dim3(B), 0, st, kin, vin, kout, vout, bs, bl, nb, 48u, ovn, ovl); }});
+  CNT2(512, 9, 1) CNT2(512, 9, 6) CNT2(1024, 5, 1) CNT2(1024, 5, 8) CNT2(768, 6, 1)
+  vs.push_back({"copy2 512x9", false, [&] {
+    hipLaunchKernelGGL((k_pair_copy2<512, 9>), dim3(m), dim3(512), 0, st, kin, vin, kout, vout, bs, bl, nb); }});
+  vs.push_back({"copy2 1024x5", false, [&] {
+    hipLaunchKernelGGL((k_pair_copy2<1024, 5>), dim3(m), dim3(1024), 0, st, kin, vin, kout, vout, bs, bl, nb); }});
   vs.push_back({"copy 512x9", false, [&] {
     hipLaunchKernelGGL((k_pair_copy<512, 9>), dim3(m), dim3(512), 0, st, kin, vin, kout, vout, bs, bl, nb); }});
   const char* filt = argc > 1 ? argv[1] : nullptr;
