@@ -129,7 +129,7 @@ def test_u64_oracles_match_numpy(oracle_mod):
 
 def test_counting_sort_restatement_pinned(oracle_mod, golden):
     """oracle.sorted_pcg_sha256 (the counting-sort restatement that produced
-    tests/golden/big_golden.json for 2^30 and 2^32-1 keys) reproduces the
+    tests/golden/big_golden.json for 2^30, 2^32-1 and 2^32 keys) reproduces the
     reference's own sorted hash (pcg_golden.json, recorded from utils.cu +
     std::sort) at 2^20, and agrees with std::sort at an offset."""
     import hashlib
@@ -141,5 +141,6 @@ def test_counting_sort_restatement_pinned(oracle_mod, golden):
     want = hashlib.sha256(oracle_mod.sort_u32(x).astype("<u4").tobytes()).hexdigest()
     assert oracle_mod.sorted_pcg_sha256(70001, first=123) == want
     big = json.loads((pathlib.Path(__file__).resolve().parent / "golden" / "big_golden.json").read_text())
-    assert set(big["sorted_u32"]) == {str(1 << 30), str((1 << 32) - 1)}
+    # 2^30 (configs[2]), 2^32 - 1 (the ABI maximum), 2^32 (configs[3]'s global input, round 5)
+    assert set(big["sorted_u32"]) == {str(1 << 30), str((1 << 32) - 1), str(1 << 32)}
     assert set(big["c5_pairs"][str(1 << 28)]) == {"keys", "payloads"}

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-rank step model of the 8-GPU top-digit schedule.
 
-    python tools/msd_model.py [--partition-ms 1.22] [--gpu-ms 5.00] [--n1 119.3]
+    python tools/msd_model.py [--partition-ms 1.22] [--gpu-ms 5.00] [--n1 121.5] [--wire-bytes 3]
 
 The step is the partition (exposed), round 0's exchange, then each round
 the longer of its sort and the next round's exchange, then the last sort.
@@ -14,7 +14,12 @@ round profile changes.
 import argparse
 
 KEYS_PER_RANK = 1 << 29
-SENT_BYTES = 7 / 8 * KEYS_PER_RANK * 4  # bytes a rank sends at 8 GPUs
+
+
+def sent_bytes(wire_bytes):
+    """bytes a rank sends at 8 GPUs (7/8 of its keys; 4 B per key as 32-bit
+    words, 3 B with the 24-bit wire format of round 5)"""
+    return 7 / 8 * KEYS_PER_RANK * wire_bytes
 
 PROFILES = {
     "K4 x1.2 (built)": [1, 1.2, 1.44, 1.728],
@@ -25,10 +30,10 @@ PROFILES = {
 }
 
 
-def step_ms(weights, rate_gbs, part_ms, sorts_ms, per_round_ms, built_rounds=4):
+def step_ms(weights, rate_gbs, part_ms, sorts_ms, per_round_ms, built_rounds=4, wire_bytes=3):
     t = sum(weights)
     f = [w / t for w in weights]
-    e = SENT_BYTES / (rate_gbs * 1e9) * 1e3
+    e = sent_bytes(wire_bytes) / (rate_gbs * 1e9) * 1e3
     body = sorts_ms - built_rounds * per_round_ms
     s = [x * body + per_round_ms for x in f]
     k = len(f)
@@ -40,13 +45,14 @@ def main():
     ap.add_argument("--partition-ms", type=float, default=1.22)
     ap.add_argument("--gpu-ms", type=float, default=5.00, help="GPU work per rank, 8-GPU shape")
     ap.add_argument("--per-round-ms", type=float, default=0.13)
-    ap.add_argument("--n1", type=float, default=119.3, help="N = 1 line, Gkeys/s")
+    ap.add_argument("--n1", type=float, default=121.5, help="N = 1 line, Gkeys/s (BENCH_r04)")
+    ap.add_argument("--wire-bytes", type=float, default=3.0, help="bytes per key on the links (4: 32-bit words)")
     a = ap.parse_args()
     sorts = a.gpu_ms - a.partition_ms
     for name, w in PROFILES.items():
         cells = []
         for rate in (700, 450, 400, 360, 300):
-            st, e = step_ms(w, rate, a.partition_ms, sorts, a.per_round_ms)
+            st, e = step_ms(w, rate, a.partition_ms, sorts, a.per_round_ms, wire_bytes=a.wire_bytes)
             agg = 8 * KEYS_PER_RANK / (st * 1e-3) / 1e9
             cells.append("%d GB/s: E %.2f step %.2f ms %.0f Gk/s %.2fx" % (rate, e, st, agg, agg / a.n1))
         print("%-16s %s" % (name, " | ".join(cells)))

@@ -60,7 +60,7 @@ def main():
         cabi = os.environ.get("MSD_ENGINE") == "cabi"
         for _ in range(2 + reps):
             if cabi:
-                D.distrib_sort_u32([keys])
+                D.distrib_sort_u32([keys], D.LIBSORT_DISTRIB_WIRE32 if os.environ.get("MSD_WIRE32") else 0)
             else:
                 distrib.sort_msd(keys, ops, rounds=4)
         torch.cuda.synchronize()
@@ -78,8 +78,16 @@ def main():
         res["msd_rounds%d_via_rccl_ms" % K] = timed(lambda: distrib.sort_msd(keys, ops, rounds=K, self_local=False))
     # the C-ABI engine (libsortDistribSortU32) on the same keys: one rank over
     # a one-device RCCL communicator, self pieces as device copies
+    # (4-bit digits: the engine's default wire format is 24-bit planes, so
+    # its self piece is a copy of 3 bytes per key; WIRE32 = 32-bit words)
+    p16, q16 = torch.empty(n, dtype=torch.int16, device="cuda"), torch.empty(n, dtype=torch.int16, device="cuda")
+    p8, q8 = torch.empty(n, dtype=torch.uint8, device="cuda"), torch.empty(n, dtype=torch.uint8, device="cuda")
+    res["selfcopy24_all_keys_ms"] = timed(lambda: (q16.copy_(p16), q8.copy_(p8)))
+    del p16, q16, p8, q8
     res["cabi_rounds4_selfcopy_ms"] = timed(lambda: D.distrib_sort_u32([keys]))
-    res["cabi_rounds4_minus_selfcopy_ms"] = res["cabi_rounds4_selfcopy_ms"] - res["selfcopy_all_keys_ms"]
+    res["cabi_rounds4_minus_selfcopy_ms"] = res["cabi_rounds4_selfcopy_ms"] - res["selfcopy24_all_keys_ms"]
+    res["cabi_wire32_selfcopy_ms"] = timed(lambda: D.distrib_sort_u32([keys], D.LIBSORT_DISTRIB_WIRE32))
+    res["cabi_wire32_minus_selfcopy_ms"] = res["cabi_wire32_selfcopy_ms"] - res["selfcopy_all_keys_ms"]
     if os.environ.get("MSD_DIGIT8", "1") == "1":
         pylibsort.setDigitBits(8)
         res["digit8_msd_rounds4_selfcopy_ms"] = timed(lambda: distrib.sort_msd(keys, ops, rounds=4))
