@@ -1310,15 +1310,50 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   // (GEO 5 over 24-bit pieces: geo.i16 / geo.i8 instead of kin)
   constexpr bool PLANAR_IN = (GEO & 5) == 5 && sizeof(K) == 4 && !HAS_V;
   if (PLANAR_IN && geo.i8 != nullptr) {
+    // the tile's two planes staged through s_keys (free until the scatter):
+    // dword loads from the dword-aligned floor of each plane's byte range (a
+    // piece, hence a tile, starts at any key), then 2- and 1-byte LDS reads.
+    // (Per-key ushort / ubyte global loads -- 2 x 16 small loads per thread
+    // -- ran the depth-0 pass at 361 us against 251 us for u32 keys,
+    // profiles/r05f_shape8_*.)  A read past the 16-bit plane's end lands in
+    // the 8-bit plane, one past that in the receive buffer's unused quarter.
+    static_assert(sizeof(K) * TILE >= 3 * TILE + 8, "staging fits s_keys");
     const uint32_t hi = geo.seghi[seg];
-    const uint16_t* p16 = geo.i16 + tile_base + wbase + lane;
-    const uint8_t* p8 = geo.i8 + tile_base + wbase + lane;
+    uint8_t* const st = reinterpret_cast<uint8_t*>(s_keys);
+    const uint64_t b16 = 2 * tile_base, b8 = tile_base;
+    const uint32_t a16 = (uint32_t)(b16 & 3u), a8 = (uint32_t)(b8 & 3u);
+    const uint32_t* g16 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(geo.i16) + (b16 - a16));
+    const uint32_t* g8 = reinterpret_cast<const uint32_t*>(geo.i8 + (b8 - a8));
+    const uint32_t n16 = (a16 + 2 * valid + 3) / 4, n8 = (a8 + valid + 3) / 4;
+    uint32_t* const st16 = reinterpret_cast<uint32_t*>(st);
+    uint32_t* const st8 = reinterpret_cast<uint32_t*>(st + 2 * TILE + 4);
+    constexpr int Q16 = (2 * TILE + 4 + 4 * BLOCK - 1) / (4 * BLOCK), Q8 = (TILE + 4 + 4 * BLOCK - 1) / (4 * BLOCK);
+    uint32_t w16[Q16], w8[Q8];
+#pragma unroll
+    for (int q = 0; q < Q16; ++q) {
+      const uint32_t i = tid + q * BLOCK;
+      w16[q] = i < n16 ? load_stream(&g16[i]) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < Q8; ++q) {
+      const uint32_t i = tid + q * BLOCK;
+      w8[q] = i < n8 ? load_stream(&g8[i]) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < Q16; ++q)
+      if (tid + q * BLOCK < n16) st16[tid + q * BLOCK] = w16[q];
+#pragma unroll
+    for (int q = 0; q < Q8; ++q)
+      if (tid + q * BLOCK < n8) st8[tid + q * BLOCK] = w8[q];
+    __syncthreads();
+    const uint16_t* const l16 = reinterpret_cast<const uint16_t*>(st + a16);
+    const uint8_t* const l8 = reinterpret_cast<const uint8_t*>(st8) + a8;
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-      const bool ok = full || wbase + j * kWave + lane < valid;
-      k[j] = ok ? (K)(hi | ((uint32_t)load_stream(&p8[j * kWave]) << 16) | (uint32_t)load_stream(&p16[j * kWave]))
-                : (K)0;
+      const uint32_t i = wbase + j * kWave + lane;
+      k[j] = (full || i < valid) ? (K)(hi | ((uint32_t)l8[i] << 16) | (uint32_t)l16[i]) : (K)0;
     }
+    __syncthreads();  // (s_keys is the scatter's next)
   } else {
     const K* kp = kin + tile_base + wbase + lane;
     const V* vp = HAS_V ? vin + tile_base + wbase + lane : nullptr;
@@ -1955,23 +1990,27 @@ void k_bucket_count(const uint32_t* in, uint32_t* out, const uint32_t* __restric
 
 // The counting placement for (u64 key, u32 payload) buckets (configs[4]'s
 // stable pair sort; round 5).  The bucket's pairs share
-// every key bit above lbits; x = bits [lbits - 16, lbits) of key - bias are
-// counted in 4096 u64 cells of 16 3-bit counts (+ the cell's pair count, then
-// its start, in the top 16 bits), one LDS atomic per pair, and each pair is
-// placed at cell start + the counts of the smaller x in its cell + its rank
-// among equal x (atomic order: arbitrary).  Its input slot (u16) goes beside
-// the key, so a run of equal x -- a field count >= 2, found in the cell words
-// the thread scanned (4096 uniform pairs over 2^16 values: ~128 runs of 2) --
-// is insertion-sorted by (key, slot): equal keys end in input order, i.e. the
-// sort is stable without a stable rank.  The keys are written out, then the
-// payloads are put at their input slots over the key array and gathered
-// through the slots.  LDS: 10 B per slot (the cells over the keys); 1024-thread
-// blocks of 5 slots (2^28 pairs) hold 2 blocks per CU at 63 VGPRs
-// (tools/pair_lab: 4096-pair buckets, the two 8-bit ballot steps + fix-up of
-// k_bucket_sort FIX 1762 us per 2^28 pairs, this 14.7-B/slot variant with
-// the payloads placed too 1477 us).  A 3-bit count that would wrap (8+ pairs
-// with equal x) writes nothing and lists the bucket (ovf_list) for
-// k_bucket_sort's LSD steps; a bucket over the block is listed (olist).
+// every bit of key - bias above lbits (<= 48); x = bits [lbits - 16, lbits)
+// are counted in 4096 u64 cells of 16 3-bit counts (+ the cell's pair count,
+// then its start, in the top 16 bits), one LDS atomic per pair, and each pair
+// is placed at cell start + the counts of the smaller x in its cell + its
+// rank among equal x (atomic order: arbitrary).  What goes there is ONE u64,
+// p = (the low lbits of key - bias) << 16 | the pair's input slot, which
+// orders exactly as (key, slot): a run of equal x -- a field count >= 2,
+// found in the cell words the thread scanned (4096 uniform pairs over 2^16
+// values: ~128 runs of 2) -- is insertion-sorted on p, so equal keys end in
+// input order and the sort is stable without a stable rank.  The keys are
+// written out (the shared high bits put back), then the payloads are put at
+// their input slots over the same LDS and gathered through the slots.  LDS: 8
+// B per slot (the 32 KB of cells over them); 1024-thread blocks of 5 slots
+// (2^28 pairs) at 63 VGPRs, two blocks per CU.  tools/pair_lab, 4096-pair
+// buckets of 2^28 pairs (profiles/r05g_pair_lab.txt): the two 8-bit ballot
+// steps + fix-up of k_bucket_sort FIX 1682-1791 us; this layout 1385-1400 us
+// (key and slot in separate LDS arrays 1474-1506 us, payloads placed too
+// 1475-1490 us); a copy through the same LDS footprint 1157 us.  A 3-bit count
+// that would wrap (8+ pairs with equal x) writes nothing and lists the bucket
+// (ovf_list) for k_bucket_sort's LSD steps; a bucket over the block is listed
+// (olist).
 template <int BLOCK, int ITEMS, typename Op>
 __global__ __launch_bounds__(BLOCK) void k_bucket_pairs(const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
                                                         uint32_t* vout, const uint32_t* __restrict__ bstart,
@@ -1982,9 +2021,8 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_pairs(const uint64_t* kin, uin
                                                         uint32_t* __restrict__ olist, uint32_t olist_cap,
                                                         uint32_t* __restrict__ ovf_n, uint32_t* __restrict__ ovf_list) {
   constexpr int CAP = BLOCK * ITEMS, PER = kCntCells / BLOCK;
-  static_assert(CAP >= kCntCells && CAP < 65536 && kCntCells % BLOCK == 0, "cells over the keys; u16 slots");
-  __shared__ uint64_t s_k[CAP];
-  __shared__ uint16_t s_i[CAP];
+  static_assert(CAP >= kCntCells && CAP < 65536 && kCntCells % BLOCK == 0, "cells over the slots; u16 slots");
+  __shared__ uint64_t s_p[CAP];
   __shared__ uint32_t s_ws[BLOCK / kWave];
   if (blockIdx.x >= min(*nb, nb_cap)) return;
   const uint32_t b = ilist ? ilist[blockIdx.x] : blockIdx.x;
@@ -1998,10 +2036,10 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_pairs(const uint64_t* kin, uin
   }
   if (len == 0) return;
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wbase = (tid / kWave) * ITEMS * kWave;
-  uint64_t* const cw = s_k;
+  uint64_t* const cw = s_p;
   auto ci = [&](uint32_t c) -> uint32_t { return (c % PER) * BLOCK + c / PER; };
   const uint32_t fs = lbits - 16;
-  auto xval = [&](uint64_t key) -> uint32_t { return (uint32_t)((uint64_t)(key - bias) >> fs) & 0xFFFFu; };
+  const uint64_t lmask = (1ull << lbits) - 1ull;
   auto valid = [&](int j) { return wbase + j * kWave + lane < len; };
   uint64_t k[ITEMS];
   uint32_t v[ITEMS], rk[ITEMS];
@@ -2011,6 +2049,11 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_pairs(const uint64_t* kin, uin
     k[j] = i < len ? load_stream(&kin[(size_t)start + i]) : 0ull;
     v[j] = i < len ? load_stream(&vin[(size_t)start + i]) : 0u;
   }
+  // (key - bias from here on; subtracted after every load is in flight -- in
+  // the load's select it waited for each load in turn: 1640 vs 1510 us)
+#pragma unroll
+  for (int j = 0; j < ITEMS; ++j) k[j] -= bias;
+  const uint64_t khi = (kin[start] - bias) & ~lmask;  // the bits every pair of the bucket shares
 #pragma unroll
   for (int q = 0; q < PER; ++q) cw[q * BLOCK + tid] = 0ull;
   __syncthreads();
@@ -2018,7 +2061,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_pairs(const uint64_t* kin, uin
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j)
     if (valid(j)) {
-      const uint32_t x = xval(k[j]), sh = 3u * (x & 15u);
+      const uint32_t x = (uint32_t)(k[j] >> fs) & 0xFFFFu, sh = 3u * (x & 15u);
       const uint64_t old = atomicAdd((unsigned long long*)&cw[ci(x >> 4)], (1ull << sh) + (1ull << 48));
       rk[j] = (uint32_t)(old >> sh) & 7u;
       ovf |= rk[j] == 7u;
@@ -2050,17 +2093,14 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_pairs(const uint64_t* kin, uin
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j)
     if (valid(j)) {
-      const uint32_t x = xval(k[j]);
+      const uint32_t x = (uint32_t)(k[j] >> fs) & 0xFFFFu;
       const uint64_t cc = cw[ci(x >> 4)];
       rk[j] += (uint32_t)(cc >> 48) + field3_sum(cc & ((1ull << (3u * (x & 15u))) - 1ull));
     }
-  __syncthreads();  // the pairs take the cells' place
+  __syncthreads();  // the packed pairs take the cells' place
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j)
-    if (valid(j)) {
-      s_k[rk[j]] = k[j];
-      s_i[rk[j]] = (uint16_t)(wbase + j * kWave + lane);
-    }
+    if (valid(j)) s_p[rk[j]] = ((k[j] & lmask) << 16) | (uint64_t)(wbase + j * kWave + lane);
   __syncthreads();
   // runs of equal x: this thread's cells c = tid * PER + q start at cst[q]
 #pragma unroll
@@ -2073,21 +2113,14 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_pairs(const uint64_t* kin, uin
       m &= m - 1;
       const uint32_t L = (uint32_t)(f >> (3u * r)) & 7u;
       const uint32_t p = cst[q] + field3_sum(f & ((1ull << (3u * r)) - 1ull));
-      for (uint32_t a = 1; a < L; ++a) {  // stable by (key, input slot)
-        const uint64_t xk = s_k[p + a];
-        const uint16_t xi = s_i[p + a];
-        const uint64_t xb = xk - bias;
+      for (uint32_t a = 1; a < L; ++a) {  // stable: p orders as (key, input slot)
+        const uint64_t x = s_p[p + a];
         uint32_t z = a;
-        while (z > 0) {
-          const uint64_t yk = s_k[p + z - 1];
-          const uint64_t yb = yk - bias;
-          if (yb < xb || (yb == xb && s_i[p + z - 1] < xi)) break;
-          s_k[p + z] = yk;
-          s_i[p + z] = s_i[p + z - 1];
+        while (z > 0 && s_p[p + z - 1] > x) {
+          s_p[p + z] = s_p[p + z - 1];
           --z;
         }
-        s_k[p + z] = xk;
-        s_i[p + z] = xi;
+        s_p[p + z] = x;
       }
     }
   }
@@ -2095,22 +2128,23 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_pairs(const uint64_t* kin, uin
   uint32_t sl[ITEMS];
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
-    const uint32_t p = wbase + j * kWave + lane;
+    const uint32_t pos = wbase + j * kWave + lane;
     sl[j] = 0u;
-    if (p < len) {
-      kout[(size_t)start + p] = s_k[p];
-      sl[j] = s_i[p];
+    if (pos < len) {
+      const uint64_t x = s_p[pos];
+      kout[(size_t)start + pos] = (khi | (x >> 16)) + bias;
+      sl[j] = (uint32_t)x & 0xFFFFu;
     }
   }
   __syncthreads();  // the payloads take the keys' place, at their input slots
-  uint32_t* const s_v = reinterpret_cast<uint32_t*>(s_k);
+  uint32_t* const s_v = reinterpret_cast<uint32_t*>(s_p);
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) s_v[wbase + j * kWave + lane] = v[j];
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < ITEMS; ++j) {
-    const uint32_t p = wbase + j * kWave + lane;
-    if (p < len) vout[(size_t)start + p] = s_v[sl[j]];
+    const uint32_t pos = wbase + j * kWave + lane;
+    if (pos < len) vout[(size_t)start + pos] = s_v[sl[j]];
   }
 }
 
@@ -4584,7 +4618,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       const bool two = C && lbits == 16 && BB == 256 && cls <= 3 && bucket2_on();
       // (u64 key, u32 payload) pairs: k_bucket_pairs (LIBSORT_PAIR_COUNT=0:
       // the LSD steps + fix-up of k_bucket_sort FIX)
-      const bool pcnt = kPairCnt && lbits >= 16 && pair_count_on();
+      const bool pcnt = kPairCnt && lbits >= 16 && lbits <= 48 && pair_count_on();
       // (inline: the retry list holds only the buckets over the first block,
       // so the 3-bit LIST launch runs only when the planning counted any)
       const bool inl = two && bucket2_inline_on();
