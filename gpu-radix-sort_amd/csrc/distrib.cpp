@@ -153,6 +153,7 @@ struct DBuf {
 };
 
 constexpr int kMaxRounds = 4;
+constexpr int kMaxParts = 2;  // partition parts per rank (partition_top)
 
 struct DevState {
   int dev = -1;
@@ -172,6 +173,7 @@ struct RankState {
   DBuf hin, hout;  // staging of the host-pointer entry point
   uint64_t pn = 0;  // keys in `part` (24-bit planes: the 8-bit plane starts at byte 2 * pn)
   hipEvent_t ev_part = nullptr, ev_bounds = nullptr, ev_done = nullptr;
+  hipEvent_t ev_part0 = nullptr;  // the first partition part written (two parts: partition_top)
   hipEvent_t ev_x[kMaxRounds] = {};
 };
 
@@ -180,7 +182,7 @@ struct Ctx {
   std::vector<std::unique_ptr<DevState>> uniq;  // one per distinct device
   std::vector<RankState> ranks;
   std::vector<ncclComm_t> comms;               // RCCL communicator of each rank (distinct devices only)
-  uint32_t* h_bounds = nullptr;                // pinned: R x 256 bucket starts
+  uint32_t* h_bounds = nullptr;                // pinned: R x kMaxParts x 256 bucket starts
   uint64_t* h_mm = nullptr;                    // pinned: R x (min, max) keys
   bool distinct = false;
   std::vector<uint64_t> sent;                  // bytes each rank sent to others in the last sort
@@ -192,7 +194,7 @@ struct Ctx {
       for (DBuf* b : {&r.bounds, &r.part, &r.pv, &r.recv, &r.rv, &r.outb, &r.ov, &r.alt, &r.mm, &r.hin, &r.hout})
         b->release();
       (void)hipSetDevice(r.dev);
-      for (hipEvent_t e : {r.ev_part, r.ev_bounds, r.ev_done})
+      for (hipEvent_t e : {r.ev_part, r.ev_bounds, r.ev_done, r.ev_part0})
         if (e) (void)hipEventDestroy(e);
       for (hipEvent_t e : r.ev_x)
         if (e) (void)hipEventDestroy(e);
@@ -247,13 +249,15 @@ struct Ctx {
       s.dev = d[r];
       s.d = by_dev[d[r]];
       if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice")) return false;
-      for (hipEvent_t* e : {&s.ev_part, &s.ev_bounds, &s.ev_done})
+      for (hipEvent_t* e : {&s.ev_part, &s.ev_bounds, &s.ev_done, &s.ev_part0})
         if (!ok_hip(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate")) return false;
       for (hipEvent_t& e : s.ev_x)
         if (!ok_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate")) return false;
-      if (!s.bounds.ensure(s.dev, dplan::kTopDigits * 4) || !s.mm.ensure(s.dev, 2 * sizeof(uint64_t))) return false;
+      if (!s.bounds.ensure(s.dev, kMaxParts * dplan::kTopDigits * 4) || !s.mm.ensure(s.dev, 2 * sizeof(uint64_t)))
+        return false;
     }
-    return ok_hip(hipHostMalloc(&h_bounds, (size_t)R * dplan::kTopDigits * sizeof(uint32_t), 0), "hipHostMalloc") &&
+    return ok_hip(hipHostMalloc(&h_bounds, (size_t)R * kMaxParts * dplan::kTopDigits * sizeof(uint32_t), 0),
+                  "hipHostMalloc") &&
            ok_hip(hipHostMalloc(&h_mm, (size_t)R * 2 * sizeof(uint64_t), 0), "hipHostMalloc");
   }
 
@@ -496,12 +500,19 @@ struct PartDigit {
 // (low 16 bits at byte 0, bits 16..23 at byte 2 * n): the top byte is the
 // partition digit, which every receiver knows from its piece table, so the
 // exchange moves 3 bytes per key instead of 4 (round 5).
+// H = 2 parts (round 5): the rank's keys [0, cut) and
+// [cut, n) (dplan::part_split) are partitioned one after the other into the
+// same ranges of `part` (count, scatter, count, scatter), ev_part0 marks the
+// first part written, and Cp[r * H + h] / first[r * H + h] are each part's
+// digit counts and start, so the first part's exchange can run while the
+// second is partitioned (run_digit_rounds).
 template <typename K>
 bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<const uint32_t*>* vin,
                    const std::vector<uint64_t>& n, std::vector<std::vector<uint64_t>>& C, const PartDigit& pd,
-                   bool planar = false) {
+                   bool planar, int H, std::vector<std::vector<uint64_t>>& Cp, std::vector<uint64_t>& first) {
   const int R = (int)c.ranks.size();
   constexpr int NB = dplan::kTopDigits;
+  first.assign((size_t)R * H + 1, 0);
   for (int r = 0; r < R; ++r) {
     RankState& s = c.ranks[r];
     if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !s.part.ensure(s.dev, std::max<uint64_t>(n[r], 1) * sizeof(K)) ||
@@ -509,52 +520,64 @@ bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<co
       return false;
     const uint8_t* lut = static_cast<const uint8_t*>(s.d->lut.p);
     Workspace& ws = *s.d->ws;
-    if (n[r]) {
+    s.pn = n[r];
+    for (int h = 0; h < H; ++h) {
+      const uint64_t a = H == 1 ? 0 : h == 0 ? 0 : dplan::part_split(n[r]);
+      const uint64_t m = H == 1 ? n[r] : h == 0 ? dplan::part_split(n[r]) : n[r] - a;
+      first[(size_t)r * H + h] = a;
+      const K* ik = in[r] + a;
+      const uint32_t* iv = vin ? (*vin)[r] + a : nullptr;
+      uint32_t* const bnd = s.bounds.u32() + (size_t)h * NB;
       hipError_t e1, e2;
       if constexpr (sizeof(K) == 4) {
-        e1 = pd.range ? partition_range_u32(ws, in[r], nullptr, n[r], (uint32_t)pd.bias, pd.shift, s.bounds.u32(),
-                                            s.d->st, kPartCount)
-                      : partition_lut_u32(ws, in[r], nullptr, n[r], lut, dplan::kTopShift, NB, s.bounds.u32(),
-                                          s.d->st, kPartCount);
+        e1 = pd.range ? partition_range_u32(ws, ik, nullptr, m, (uint32_t)pd.bias, pd.shift, bnd, s.d->st, kPartCount)
+                      : partition_lut_u32(ws, ik, nullptr, m, lut, dplan::kTopShift, NB, bnd, s.d->st, kPartCount);
       } else {
-        e1 = pd.range ? partition_range_pairs_u64_u32(ws, in[r], (*vin)[r], nullptr, nullptr, n[r], pd.bias, pd.shift,
-                                                      s.bounds.u32(), s.d->st, kPartCount)
-                      : partition_lut_pairs_u64_u32(ws, in[r], (*vin)[r], nullptr, nullptr, n[r], lut,
-                                                    dplan::kTopShift, NB, s.bounds.u32(), s.d->st, kPartCount);
+        e1 = pd.range ? partition_range_pairs_u64_u32(ws, ik, iv, nullptr, nullptr, m, pd.bias, pd.shift, bnd, s.d->st,
+                                                      kPartCount)
+                      : partition_lut_pairs_u64_u32(ws, ik, iv, nullptr, nullptr, m, lut, dplan::kTopShift, NB, bnd,
+                                                    s.d->st, kPartCount);
       }
       if (!ok_hip(e1, "partition counts") ||
-          !ok_hip(hipMemcpyAsync(c.h_bounds + (size_t)r * NB, s.bounds.p, NB * 4, hipMemcpyDeviceToHost, s.d->st),
+          !ok_hip(hipMemcpyAsync(c.h_bounds + ((size_t)r * H + h) * NB, bnd, NB * 4, hipMemcpyDeviceToHost, s.d->st),
                   "D2H bucket starts") ||
-          !ok_hip(hipEventRecord(s.ev_bounds, s.d->st), "hipEventRecord"))
+          (h == H - 1 && !ok_hip(hipEventRecord(s.ev_bounds, s.d->st), "hipEventRecord")))
         return false;
-      s.pn = n[r];
       if constexpr (sizeof(K) == 4) {
-        e2 = pd.range ? partition_range_u32(ws, in[r], s.part.u32(), n[r], (uint32_t)pd.bias, pd.shift, nullptr,
-                                            s.d->st, kPartScatter)
-             : planar ? partition_lut_planar_u32(ws, in[r], static_cast<uint16_t*>(s.part.p),
-                                                 static_cast<uint8_t*>(s.part.p) + 2 * n[r], n[r], lut,
+        uint32_t* const ok = s.part.u32() + a;
+        e2 = pd.range ? partition_range_u32(ws, ik, ok, m, (uint32_t)pd.bias, pd.shift, nullptr, s.d->st, kPartScatter)
+             : planar ? partition_lut_planar_u32(ws, ik, static_cast<uint16_t*>(s.part.p) + a,
+                                                 static_cast<uint8_t*>(s.part.p) + 2 * n[r] + a, m, lut,
                                                  dplan::kTopShift, NB, s.d->st)
-                      : partition_lut_u32(ws, in[r], s.part.u32(), n[r], lut, dplan::kTopShift, NB, nullptr, s.d->st,
-                                          kPartScatter);
+                      : partition_lut_u32(ws, ik, ok, m, lut, dplan::kTopShift, NB, nullptr, s.d->st, kPartScatter);
       } else {
-        e2 = pd.range ? partition_range_pairs_u64_u32(ws, in[r], (*vin)[r], static_cast<uint64_t*>(s.part.p),
-                                                      s.pv.u32(), n[r], pd.bias, pd.shift, nullptr, s.d->st,
-                                                      kPartScatter)
-                      : partition_lut_pairs_u64_u32(ws, in[r], (*vin)[r], static_cast<uint64_t*>(s.part.p),
-                                                    s.pv.u32(), n[r], lut, dplan::kTopShift, NB, nullptr, s.d->st,
-                                                    kPartScatter);
+        uint64_t* const ok = static_cast<uint64_t*>(s.part.p) + a;
+        e2 = pd.range ? partition_range_pairs_u64_u32(ws, ik, iv, ok, s.pv.u32() + a, m, pd.bias, pd.shift, nullptr,
+                                                      s.d->st, kPartScatter)
+                      : partition_lut_pairs_u64_u32(ws, ik, iv, ok, s.pv.u32() + a, m, lut, dplan::kTopShift, NB,
+                                                    nullptr, s.d->st, kPartScatter);
       }
       if (!ok_hip(e2, "partition scatter")) return false;
+      if (h == 0 && !ok_hip(hipEventRecord(s.ev_part0, s.d->st), "hipEventRecord")) return false;
     }
     if (!ok_hip(hipEventRecord(s.ev_part, s.d->st), "hipEventRecord")) return false;
   }
   C.assign(R, std::vector<uint64_t>(NB, 0));
+  Cp.assign((size_t)R * H, std::vector<uint64_t>(NB, 0));
   for (int r = 0; r < R; ++r) {
     if (!n[r]) continue;
     if (!ok_hip(hipEventSynchronize(c.ranks[r].ev_bounds), "hipEventSynchronize")) return false;
-    const uint32_t* b = c.h_bounds + (size_t)r * NB;
-    for (int g = 0; g < NB; ++g) C[r][g] = (g + 1 < NB ? (uint64_t)b[g + 1] : n[r]) - b[g];
+    for (int h = 0; h < H; ++h) {
+      const size_t v = (size_t)r * H + h;
+      const uint64_t m = (h + 1 < H ? first[v + 1] : n[r]) - first[v];
+      const uint32_t* b = c.h_bounds + v * NB;
+      for (int g = 0; g < NB; ++g) {
+        Cp[v][g] = m ? (g + 1 < NB ? (uint64_t)b[g + 1] : m) - b[g] : 0;
+        C[r][g] += Cp[v][g];
+      }
+    }
   }
+  first.pop_back();
   return true;
 }
 
@@ -606,7 +629,7 @@ bool range_digit(Ctx& c, const std::vector<const K*>& in, const std::vector<uint
 template <typename K>
 bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& out,
                       const std::vector<uint32_t*>* vout, bool use_rccl, bool self_rccl, int bits,
-                      const PartDigit& pd, bool planar = false) {
+                      const PartDigit& pd, bool planar, int H) {
   const int R = (int)c.ranks.size(), K_ = p.K;
   const bool pairs = vout != nullptr;
   std::map<DevState*, uint64_t> round_max;
@@ -623,7 +646,8 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
     if (!kv.first->tmp.ensure(kv.first->dev, std::max<uint64_t>(kv.second, 1) * sizeof(K)) ||
         (pairs && !kv.first->tmpv.ensure(kv.first->dev, std::max<uint64_t>(kv.second, 1) * 4)))
       return false;
-  if (!comm_waits(c, &RankState::ev_part)) return false;
+  // (two parts: the first part's pieces wait for that part only)
+  if (!comm_waits(c, H > 1 ? &RankState::ev_part0 : &RankState::ev_part)) return false;
   std::vector<const void*> src(R), vsrc(R);
   std::vector<void*> dst(R), vdst(R);
   for (int r = 0; r < R; ++r) {
@@ -713,22 +737,47 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
           err[u] = last_error();
         }
       });
-  bool issue_ok = true;
-  for (int i = 0; issue_ok && i < K_; ++i) {
-    issue_ok = (planar ? move_pieces(c, p.rounds[i], src, dst, 2, use_rccl, self_rccl) &&
-                             move_pieces(c, p.rounds[i], src8, dst8, 1, use_rccl, self_rccl)
-                       : move_pieces(c, p.rounds[i], src, dst, sizeof(K), use_rccl, self_rccl)) &&
-               (!pairs || move_pieces(c, p.rounds[i], vsrc, vdst, 4, use_rccl, self_rccl));
-    for (int r = 0; issue_ok && r < R; ++r) {
-      RankState& s = c.ranks[r];
-      issue_ok = ok_hip(hipSetDevice(s.dev), "hipSetDevice") && ok_hip(hipEventRecord(s.ev_x[i], s.d->cs), "record");
+  // the pieces of round i that come from partition part `part` (-1: all)
+  auto issue = [&](int i, int part) -> bool {
+    std::vector<dplan::Piece> sel;
+    const std::vector<dplan::Piece>* ps = &p.rounds[i];
+    if (part >= 0) {
+      for (const dplan::Piece& q : p.rounds[i])
+        if (q.part == part) sel.push_back(q);
+      ps = &sel;
     }
-    if (issue_ok && threaded) {
+    return (planar ? move_pieces(c, *ps, src, dst, 2, use_rccl, self_rccl) &&
+                         move_pieces(c, *ps, src8, dst8, 1, use_rccl, self_rccl)
+                   : move_pieces(c, *ps, src, dst, sizeof(K), use_rccl, self_rccl)) &&
+           (!pairs || move_pieces(c, *ps, vsrc, vdst, 4, use_rccl, self_rccl));
+  };
+  // round i has been issued: its arrival event, then its sorts may go
+  auto issued_round = [&](int i) -> bool {
+    for (int r = 0; r < R; ++r) {
+      RankState& s = c.ranks[r];
+      if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !ok_hip(hipEventRecord(s.ev_x[i], s.d->cs), "record"))
+        return false;
+    }
+    if (threaded) {
       std::lock_guard<std::mutex> lk(mu);
       issued = i + 1;
       cv.notify_all();
     }
+    return true;
+  };
+  bool issue_ok = true;
+  int next = 0;  // first round not issued yet
+  if (H > 1) {
+    // the first part of rounds 0 and 1 while the ranks partition their second
+    // part (each link busy from the end of the first part's scatter: round 0
+    // alone is shorter than the second scatter), then the second parts
+    const int early = std::min(K_, 2);
+    for (int i = 0; issue_ok && i < early; ++i) issue_ok = issue(i, 0);
+    issue_ok = issue_ok && comm_waits(c, &RankState::ev_part);
+    for (int i = 0; issue_ok && i < early; ++i) issue_ok = issue(i, 1) && issued_round(i);
+    next = early;
   }
+  for (int i = next; issue_ok && i < K_; ++i) issue_ok = issue(i, -1) && issued_round(i);
   if (threaded) {
     {
       std::lock_guard<std::mutex> lk(mu);
@@ -768,6 +817,16 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
   // rounds' bytes are what the wire format changes)
   return move_pieces(c, cut, src, dst, sizeof(K), use_rccl, self_rccl, false) &&
          (!pairs || move_pieces(c, cut, vsrc, vdst, 4, use_rccl, self_rccl, false));
+}
+
+// Partition parts per rank: two when there is an exchange to overlap (R > 1;
+// LIBSORT_DISTRIB_PARTS=1 keeps one).
+int parts_for(int R) {
+  static const int env = [] {
+    const char* e = getenv("LIBSORT_DISTRIB_PARTS");
+    return e && e[0] == '1' ? 1 : kMaxParts;
+  }();
+  return R > 1 ? env : 1;
 }
 
 // Shared prologue of both entry points: sizes, the output shard counts.
@@ -821,7 +880,10 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
     return !(e && e[0] == '0');
   }();
   const bool planar = wire24_env && !(flags & kDistribWire32) && bits == 4;
-  if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd, planar)) return hold.finish(false);
+  const int H = parts_for(R);
+  std::vector<std::vector<uint64_t>> Cp;
+  std::vector<uint64_t> first;
+  if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd, planar, H, Cp, first)) return hold.finish(false);
   std::vector<uint8_t> lut(dplan::kTopDigits);
   std::vector<int64_t> est(R);
   dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
@@ -832,14 +894,14 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
     bool useful = false;
     if (!range_digit<uint32_t>(c, in, n, pd, &useful)) return hold.finish(false);
     if (useful) {  // (the range digit is not the top byte: 32-bit keys on the wire)
-      if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd)) return hold.finish(false);
+      if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd, false, H, Cp, first)) return hold.finish(false);
       dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
     }
     if (!useful || dplan::msd_too_skewed(est.data(), R, N))
       return hold.finish(run_lsd(c, in, n, out, S, bits, !copy, self_rccl));
   }
-  return hold.finish(run_digit_rounds<uint32_t>(c, dplan::digit_plan(C, lut.data(), K), out, nullptr, !copy, self_rccl,
-                                                bits, pd, planar && !pd.range));
+  return hold.finish(run_digit_rounds<uint32_t>(c, dplan::digit_plan_parts(Cp, H, first, lut.data(), K), out, nullptr,
+                                                !copy, self_rccl, bits, pd, planar && !pd.range, H));
 }
 
 bool sort_device_pairs(Ctx& c, const uint64_t* const* d_kin, const uint32_t* const* d_vin, const size_t* n_in,
@@ -866,7 +928,10 @@ bool sort_device_pairs(Ctx& c, const uint64_t* const* d_kin, const uint32_t* con
   const int K = std::max(1, std::min(kMaxRounds, 256 / R));
   std::vector<std::vector<uint64_t>> C;
   PartDigit pd;
-  if (!partition_top<uint64_t>(c, kin, &vin, n, C, pd)) return hold.finish(false);
+  const int H = parts_for(R);
+  std::vector<std::vector<uint64_t>> Cp;
+  std::vector<uint64_t> first;
+  if (!partition_top<uint64_t>(c, kin, &vin, n, C, pd, false, H, Cp, first)) return hold.finish(false);
   std::vector<uint8_t> lut(dplan::kTopDigits);
   std::vector<int64_t> est(R);
   dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
@@ -878,12 +943,12 @@ bool sort_device_pairs(Ctx& c, const uint64_t* const* d_kin, const uint32_t* con
     bool useful = false;
     if (!range_digit<uint64_t>(c, kin, n, pd, &useful)) return hold.finish(false);
     if (useful) {
-      if (!partition_top<uint64_t>(c, kin, &vin, n, C, pd)) return hold.finish(false);
+      if (!partition_top<uint64_t>(c, kin, &vin, n, C, pd, false, H, Cp, first)) return hold.finish(false);
       dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
     }
   }
-  return hold.finish(run_digit_rounds<uint64_t>(c, dplan::digit_plan(C, lut.data(), K), kout, &vout, !copy,
-                                                self_rccl, bits, pd));
+  return hold.finish(run_digit_rounds<uint64_t>(c, dplan::digit_plan_parts(Cp, H, first, lut.data(), K), kout, &vout,
+                                                !copy, self_rccl, bits, pd, false, H));
 }
 
 }  // namespace

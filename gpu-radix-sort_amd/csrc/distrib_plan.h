@@ -108,6 +108,7 @@ inline bool msd_too_skewed(const int64_t* est, int R, uint64_t N, double max_imb
 struct Piece {
   int src, dst;
   uint64_t src_off, dst_off, count;
+  int part = 0;  // the sender's partition part it comes from (digit_plan_parts)
 };
 
 // ---------------------------------------------------------------------------
@@ -177,17 +178,30 @@ struct DigitPlan {
   std::vector<std::vector<uint32_t>> p_seg;
 };
 
-inline DigitPlan digit_plan(const std::vector<std::vector<uint64_t>>& C, const uint8_t* lut, int K) {
+// Parts (round 5): a rank may partition its keys in H
+// parts one after the other (part h = its input keys [first[h], first[h+1]),
+// stably partitioned into the same range of its send buffer), so that the
+// exchange of the first part can start while the next is partitioned.  Cp
+// holds R * H rows (row s * H + h: part h of rank s); lut comes from the
+// rank totals.  A (rank, round) piece becomes one piece per part, in part
+// order, so a receiver still gets every source's keys in input order (the
+// pair sort's stability) and its round sort sees (source, part, digit)
+// pieces.  H = 1 is digit_plan.
+inline DigitPlan digit_plan_parts(const std::vector<std::vector<uint64_t>>& Cp, int H,
+                                  const std::vector<uint64_t>& first, const uint8_t* lut, int K) {
   DigitPlan p;
-  const int R = (int)C.size();
+  const int V = (int)Cp.size(), R = H > 0 ? V / H : 0;  // V: (rank, part) sources
   p.R = R;
   p.K = K;
   p.lo.assign((size_t)R * K, 0);
   p.hi.assign((size_t)R * K, 0);
   for (int c = 0; c < R * K; ++c) digit_range(lut, c, &p.lo[c], &p.hi[c]);
-  std::vector<std::vector<uint64_t>> start(R, std::vector<uint64_t>(kTopDigits + 1, 0));
-  for (int s = 0; s < R; ++s)
-    for (int g = 0; g < kTopDigits; ++g) start[s][g + 1] = start[s][g] + C[s][g];
+  // start[v][g]: digit g of source v in its rank's send buffer
+  std::vector<std::vector<uint64_t>> start(V, std::vector<uint64_t>(kTopDigits + 1, 0));
+  for (int v = 0; v < V; ++v) {
+    start[v][0] = first.empty() ? 0 : first[v];
+    for (int g = 0; g < kTopDigits; ++g) start[v][g + 1] = start[v][g] + Cp[v][g];
+  }
   p.roff.assign((size_t)R * (K + 1), 0);
   p.n_recv.assign(R, 0);
   p.rounds.assign(K, {});
@@ -199,19 +213,19 @@ inline DigitPlan digit_plan(const std::vector<std::vector<uint64_t>>& C, const u
     for (int i = 0; i < K; ++i) {
       p.roff[(size_t)d * (K + 1) + i] = run;
       const int a = p.lo[(size_t)i * R + d], b = p.hi[(size_t)i * R + d];
-      std::vector<uint64_t> base(R, 0);
+      std::vector<uint64_t> base(V, 0);
       uint64_t at = 0;
-      for (int s = 0; s < R; ++s) {
-        base[s] = at;
-        const uint64_t m = start[s][b] - start[s][a];
-        if (m) p.rounds[i].push_back(Piece{s, d, start[s][a], run + at, m});
+      for (int v = 0; v < V; ++v) {
+        base[v] = at;
+        const uint64_t m = start[v][b] - start[v][a];
+        if (m) p.rounds[i].push_back(Piece{v / H, d, start[v][a], run + at, m, v % H});
         at += m;
       }
       const size_t q = (size_t)d * K + i;
       for (int g = a; g < b; ++g)
-        for (int s = 0; s < R; ++s) {
-          p.p_off[q].push_back(base[s] + (start[s][g] - start[s][a]));
-          p.p_len[q].push_back(C[s][g]);
+        for (int v = 0; v < V; ++v) {
+          p.p_off[q].push_back(base[v] + (start[v][g] - start[v][a]));
+          p.p_len[q].push_back(Cp[v][g]);
           p.p_seg[q].push_back((uint32_t)(g - a));
         }
       run += at;
@@ -221,6 +235,15 @@ inline DigitPlan digit_plan(const std::vector<std::vector<uint64_t>>& C, const u
   }
   return p;
 }
+
+inline DigitPlan digit_plan(const std::vector<std::vector<uint64_t>>& C, const uint8_t* lut, int K) {
+  return digit_plan_parts(C, 1, {}, lut, K);
+}
+
+// Where a rank's keys are cut into two partition parts: half, rounded down to
+// whole 8192-key tiles (the second part's tiles stay 16-byte aligned for the
+// count kernel's vector loads); 0 (one part) below two tiles.
+inline uint64_t part_split(uint64_t n) { return (n / 2) & ~(uint64_t)8191; }
 
 // The equal re-cut without copying what stays.  Rank r's sorted rounds hold
 // global positions [G_r + roff[r][i], G_r + roff[r][i+1]) (G_r = keys of the

@@ -55,7 +55,10 @@ static void apply(const std::vector<Piece>& ps, const std::vector<Vec>& src, std
 // the rounds (the receiver's piece table checked piece by piece: inside the
 // round, the right digit, covering the round exactly), re-cut.  balanced:
 // the plan must not be too skewed (msd_too_skewed false).
-static bool run_msd(const Vec& x, int R, int K, double growth, bool range = false, bool balanced = false) {
+// H = 2: every rank partitions its keys in two parts (dplan::part_split,
+// each part stably partitioned into its own range of the send buffer), the
+// plan and pieces from digit_plan_parts, as the engine does with R > 1.
+static bool run_msd(const Vec& x, int R, int K, double growth, bool range = false, bool balanced = false, int H = 1) {
   std::vector<Vec> in = split(x, R);
   uint64_t bias = 0;
   int shift = kTopShift;
@@ -68,14 +71,25 @@ static bool run_msd(const Vec& x, int R, int K, double growth, bool range = fals
     CHECK(range_digit(lo, hi, 32, &bias, &shift), "range digit not useful");
   }
   auto dig = [&](uint32_t k) -> uint32_t { return ((k - (uint32_t)bias) >> shift) & (kTopDigits - 1); };
-  std::vector<std::vector<uint64_t>> C(R, std::vector<uint64_t>(kTopDigits, 0));
+  std::vector<std::vector<uint64_t>> C(R, std::vector<uint64_t>(kTopDigits, 0)),
+      Cp((size_t)R * H, std::vector<uint64_t>(kTopDigits, 0));
+  std::vector<uint64_t> first((size_t)R * H, 0);
   std::vector<Vec> part(R);
   for (int r = 0; r < R; ++r) {
-    for (uint32_t k : in[r]) C[r][dig(k)]++;
-    std::vector<uint64_t> at(kTopDigits + 1, 0);
-    for (int g = 0; g < kTopDigits; ++g) at[g + 1] = at[g] + C[r][g];
     part[r].resize(in[r].size());
-    for (uint32_t k : in[r]) part[r][at[dig(k)]++] = k;  // stable
+    const uint64_t n = in[r].size(), cut = H == 1 ? n : part_split(n);
+    for (int h = 0; h < H; ++h) {
+      const uint64_t a = h == 0 ? 0 : cut, b = h == 0 ? cut : n;
+      const size_t v = (size_t)r * H + h;
+      first[v] = a;
+      for (uint64_t i = a; i < b; ++i) Cp[v][dig(in[r][i])]++;
+      std::vector<uint64_t> at(kTopDigits + 1, a);
+      for (int g = 0; g < kTopDigits; ++g) {
+        at[g + 1] = at[g] + Cp[v][g];
+        C[r][g] += Cp[v][g];
+      }
+      for (uint64_t i = a; i < b; ++i) part[r][at[dig(in[r][i])]++] = in[r][i];  // stable
+    }
   }
   std::vector<uint8_t> lut(kTopDigits);
   std::vector<int64_t> est(R);
@@ -89,7 +103,14 @@ static bool run_msd(const Vec& x, int R, int K, double growth, bool range = fals
     const int c0 = lut[g - 1] % R * K + lut[g - 1] / R, c1 = lut[g] % R * K + lut[g] / R;
     CHECK(c1 >= c0, "plan not monotone at %d", g);
   }
-  DigitPlan p = digit_plan(C, lut.data(), K);
+  DigitPlan p = digit_plan_parts(Cp, H, first, lut.data(), K);
+  for (int i = 0; i < K; ++i)
+    for (const Piece& q : p.rounds[i]) {
+      CHECK(q.part >= 0 && q.part < H, "piece part %d", q.part);
+      const uint64_t a = first[(size_t)q.src * H + q.part];
+      const uint64_t b = q.part + 1 < H ? first[(size_t)q.src * H + q.part + 1] : in[q.src].size();
+      CHECK(q.src_off >= a && q.src_off + q.count <= b, "piece outside its part");
+    }
   std::vector<Vec> recv(R), out(R);
   for (int r = 0; r < R; ++r) {
     recv[r].assign(p.n_recv[r], 0xdeadbeefu);
@@ -363,6 +384,7 @@ int main() {
         Vec x = make(k, n, n * 31 + R);
         for (int K : {1, 3, 4}) {
           run_msd(x, R, K, K == 4 ? 1.2 : 0.6);
+          if (R > 1) run_msd(x, R, K, K == 4 ? 1.2 : 0.6, false, false, 2);
           ++cases;
         }
         if (n <= 40001) {
@@ -375,6 +397,7 @@ int main() {
   for (const char* k : {"below26", "offset", "skewtop"})
     for (int R : {2, 3, 5, 8}) {
       run_msd(make(k, 300007, R), R, 4, 1.2, true, true);
+      run_msd(make(k, 300007, R), R, 4, 1.2, true, true, 2);
       ++cases;
     }
   // R * K = 256 groups (the table limit): most digits a group of their own

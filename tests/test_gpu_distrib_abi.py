@@ -336,11 +336,15 @@ def test_config5_share_over_rccl(D):
     assert sha(vo[0], np.uint32) == want["payloads"]
 
 
-def test_threaded_round_issue(oracle_mod):
+@pytest.mark.parametrize("parts", ["2", "1"], ids=["two-parts", "one-part"])
+def test_threaded_round_issue(oracle_mod, parts):
     """The multi-device issue path of the C engine (one host thread per
     device sorting round i as soon as round i's exchange is issued) on the
     one-GPU box, forced by LIBSORT_DISTRIB_THREADS=1 in a fresh process: one
-    RCCL rank, 3 ranks sharing the GPU, keys and pairs, against the oracle."""
+    RCCL rank, 3 ranks sharing the GPU, keys and pairs, against the oracle.
+    parts: the ranks' partition in two parts (the default with R > 1: the
+    first part's pieces of rounds 0 and 1 go before the second part is
+    written) or, LIBSORT_DISTRIB_PARTS=1, in one."""
     import os
     import pathlib
     import subprocess
@@ -370,6 +374,6 @@ for R, flags in ((1, 4), (3, 2)):
     assert np.array_equal(np.concatenate([t.cpu().numpy().view(np.uint32) for t in vo]), rv), R
 print("OK")
 """ % (str(root), str(root / "gpu-radix-sort_amd"))
-    env = dict(os.environ, LIBSORT_DISTRIB_THREADS="1")
+    env = dict(os.environ, LIBSORT_DISTRIB_THREADS="1", LIBSORT_DISTRIB_PARTS=parts)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
