@@ -294,16 +294,21 @@ LIBSORT_API bool libsortDistribSortU32(int nranks, const int* devices, const uin
  * order: shard 0 first).  The top-digit rounds on the key's top 8 bits with a
  * stable pair sort per round.  flags: LIBSORT_DISTRIB_COPY /
  * LIBSORT_DISTRIB_SELF_RCCL (not _LSD).  Synchronous. */
+LIBSORT_API bool libsortDistribSortPairsU64U32(int nranks, const int* devices, const uint64_t* const* d_kin,
+                                               const uint32_t* const* d_vin, const size_t* n_in,
+                                               uint64_t* const* d_kout, uint32_t* const* d_vout, size_t* n_out,
+                                               uint32_t flags);
+
+/* Both engines above, nranks > 1: each rank partitions its keys in two parts
+ * (the first half, then the rest) so that the exchange of the first part's
+ * pieces starts while the second part is partitioned; results are the same.
+ * LIBSORT_DISTRIB_PARTS=1 in the environment keeps one part. */
+
 /* Bytes each rank sent to the other ranks in the exchange rounds (its own
  * pieces and the final re-cut's surplus keys excluded) in the last
  * libsortDistribSort* / gpuDistribSort call over nranks ranks:
  * per_rank[0..nranks).  false if none ran. */
 LIBSORT_API bool libsortDistribLastBytes(int nranks, uint64_t* per_rank);
-
-LIBSORT_API bool libsortDistribSortPairsU64U32(int nranks, const int* devices, const uint64_t* const* d_kin,
-                                               const uint32_t* const* d_vin, const size_t* n_in,
-                                               uint64_t* const* d_kout, uint32_t* const* d_vout, size_t* n_out,
-                                               uint32_t flags);
 
 /* Host plan of the multi-GPU top-digit rounds (pylibsort.distrib and the
  * single-process engine above both run it; csrc/distrib_plan.h).
