@@ -244,6 +244,7 @@ def main():
             dist.barrier()
 
     engine_note = None
+    cabi_first = None  # the line's record of the C engine's verified first step (N > 1)
     if cabi:
         # first step of the C engine, verified; if it fails or its output is
         # wrong on rank 0 (distinct-device paths run only on a multi-GPU
@@ -258,6 +259,8 @@ def main():
                     (first[0] if pairs else first)[0][:1] = 0 if pairs else -1
                 if not args.no_verify and not verify_cabi(torch, shards, first, vshards if pairs else None):
                     failed, engine_note = 1, "C-ABI engine's first step failed verification; torch engine measured"
+                else:
+                    cabi_first = "verified" if not args.no_verify else "not verified (--no-verify)"
                 del first
             except RuntimeError as e:
                 failed, engine_note = 1, "C-ABI engine failed its first step (%s); torch engine measured" % e
@@ -481,8 +484,17 @@ def main():
         if world > 1:
             line["engine"] = ("cabi: rank 0 drives all %d GPUs through the C ABI" % world if cabi else
                               "torch: one process per GPU")
+            # the C engine's first step, always stated: a failure there is
+            # measured on the torch engine but shows in the line
+            line["cabi_first_step"] = (engine_note and "FAILED: " + engine_note) or cabi_first or \
+                "not run (torch engine chosen)"
             if engine_note:
                 line["engine_note"] = engine_note
+            if cabi:
+                try:  # (bytes each rank sent in the last step's exchange rounds)
+                    line["exchange_bytes_per_rank"] = D.distrib_last_bytes(world)
+                except RuntimeError:
+                    pass
         if rehearsal:
             line["rehearsal"] = "gloo, all ranks on one GPU: exercises the N>1 path, not a measurement"
         print(json.dumps(line), flush=True)

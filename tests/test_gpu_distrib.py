@@ -171,6 +171,9 @@ def test_bench_cabi_engine_rehearsal(world, pairs):
     assert line["n_gpus"] == world and line["verified"] is True
     assert "C-ABI engine" in line["config"]["workload"]
     assert "engine_note" not in line and line["engine"].startswith("cabi")
+    assert line["cabi_first_step"] == "verified"
+    sent = line["exchange_bytes_per_rank"]
+    assert len(sent) == world and all(b > 0 for b in sent), sent
 
 
 def test_bench_cabi_bad_first_step_falls_back_to_torch():
@@ -198,6 +201,7 @@ def test_bench_cabi_bad_first_step_falls_back_to_torch():
     line = json.loads(lines[0])
     assert line["verified"] is True
     assert "failed verification" in line["engine_note"] and not line["engine"].startswith("cabi")
+    assert line["cabi_first_step"].startswith("FAILED")
 
 
 def test_bench_single_gpu_line_contract():
