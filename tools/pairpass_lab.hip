@@ -146,7 +146,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
 // TPB consecutive tiles per block, the tile loop fully unrolled (straight-line
 // code: the register allocation of the one-tile kernel plus the prefetched
 // next keys / payloads), prefetch as in k_pair_pass_pf
-template <int BLOCK, int ITEMS, bool DOUT, int TPB>
+// ABL (ablations, wrong results): 1 = order-free LDS-atomic rank instead of
+// the stable ballot rank, 2 = no key stores, 3 = no payload staging / stores
+template <int BLOCK, int ITEMS, bool DOUT, int TPB, int ABL = 0>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_pair_pass_tpb(const uint64_t* __restrict__ kin, uint64_t* __restrict__ kout,
                                                          const uint32_t* __restrict__ vin, uint32_t* __restrict__ vout,
                                                          uint8_t* __restrict__ dout, const uint32_t* __restrict__ gofs,
@@ -177,7 +179,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
     if (s) __syncthreads();
     for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = 0u;
     uint32_t rk[ITEMS];
-    rank_items_t<8, true, ITEMS>(k, rk, s_whist[w], 0u, wbase, lane, op);
+    if constexpr (ABL == 1) {
+      uint32_t* const cw = reinterpret_cast<uint32_t*>(s_keys) + w * RADIX;  // (free until the scatter)
+      for (int d = lane; d < RADIX; d += kWave) cw[d] = 0u;
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) rk[j] = atomicAdd(&cw[op(k[j])], 1u);
+      for (int d = lane; d < RADIX; d += kWave) s_whist[w][d] = (WaveCount)cw[d];
+    } else {
+      rank_items_t<8, true, ITEMS>(k, rk, s_whist[w], 0u, wbase, lane, op);
+    }
     __syncthreads();
     uint32_t cnt_d = 0;
     if (tid < RADIX) {
@@ -216,8 +226,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4, 4))) v
       const uint32_t i = tid + j * BLOCK;
       const uint64_t kk = s_keys[i];
       obk[j] = s_ob[op(kk)];
-      kout[obk[j] + i] = kk;
+      if constexpr (ABL == 2) asm volatile("" ::"v"(kk), "v"(obk[j]));
+      else kout[obk[j] + i] = kk;
       if constexpr (DOUT) dout[obk[j] + i] = (uint8_t)op_next(kk);
+    }
+    if constexpr (ABL == 3) {
+#pragma unroll
+      for (int j = 0; j < ITEMS; ++j) asm volatile("" ::"v"(v[j]), "v"(rk[j]), "v"(obk[j]));
+      continue;
     }
     __syncthreads();
     uint32_t* const s_v = reinterpret_cast<uint32_t*>(s_keys);
@@ -325,14 +341,20 @@ int main(int argc, char** argv) {
                                 dout, gofs, T, op, opn);                                                           \
       else hipLaunchKernelGGL((k_pair_pass_pf<B, I, false, KPF>), dim3(G), dim3(B), 0, st, kin, kout, vin, vout,   \
                               dout, gofs, T, op, opn); }});
-    PF(512, 16, 1, 2)
 #define TPBV(N)                                                                                                    \
     vs.push_back({std::string("tpb" #N) + (D ? " dout" : ""), D ? 2 : 1, [=] {                                      \
       if (D) hipLaunchKernelGGL((k_pair_pass_tpb<512, 16, true, N>), dim3(T / N), dim3(512), 0, st, kin, kout, vin,  \
                                 vout, dout, gofs, op, opn);                                                        \
       else hipLaunchKernelGGL((k_pair_pass_tpb<512, 16, false, N>), dim3(T / N), dim3(512), 0, st, kin, kout, vin,   \
                               vout, dout, gofs, op, opn); }});
-    TPBV(1) TPBV(2) TPBV(4)
+    TPBV(1)
+#define ABLV(A)                                                                                                    \
+    vs.push_back({std::string("tpb1 ABL" #A) + (D ? " dout" : ""), -1, [=] {                                       \
+      if (D) hipLaunchKernelGGL((k_pair_pass_tpb<512, 16, true, 1, A>), dim3(T), dim3(512), 0, st, kin, kout, vin,   \
+                                vout, dout, gofs, op, opn);                                                        \
+      else hipLaunchKernelGGL((k_pair_pass_tpb<512, 16, false, 1, A>), dim3(T), dim3(512), 0, st, kin, kout, vin,    \
+                              vout, dout, gofs, op, opn); }});
+    ABLV(1) ABLV(2) ABLV(3)
   }
   vs.push_back({"copy", -1, [=] {
     hipLaunchKernelGGL((k_pair_copy<512, 16>), dim3(T), dim3(512), 0, st, kin, kout, vin, vout); }});
