@@ -1214,11 +1214,12 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   static_assert(RADIX <= BLOCK, "one digit per thread in the block phase");
   static_assert(!FUSE || (BITS == 4 && NEXT % BLOCK == 0), "fused next-pass counts: 4-bit digits");
 
-  // STAGE_V (pair tiles of 8192 64-bit keys): the values are not given LDS
-  // of their own; after the keys have been written to HBM they are scattered
-  // into the key buffer and written from there (LDS 69 KB per block instead
-  // of 101 KB: two blocks per CU).
-  constexpr bool STAGE_V = HAS_V && sizeof(K) == 8 && TILE == 8192;
+  // STAGE_V (pair tiles of 8192 or 16384 64-bit keys): the values are not
+  // given LDS of their own; after the keys have been written to HBM they are
+  // scattered into the key buffer and written from there (8192-pair tiles:
+  // LDS 69 KB per block instead of 101 KB, two blocks per CU; 16384: 137 KB,
+  // one block of 1024 threads).
+  constexpr bool STAGE_V = HAS_V && sizeof(K) == 8 && (TILE == 8192 || TILE == 16384);
   static_assert(!STAGE_V || (!FUSE && sizeof(VS) <= sizeof(K)), "staged values: 8-bit pair tiles");
   // LDS per block (occupancy: 160 KiB per CU): the per-wave digit counters
   // are 16-bit, and the destination-tile entries exist only for FUSE.
@@ -3773,11 +3774,16 @@ int choose_algorithm(size_t n, int bits) {
 // the next pass's counts fused into the pass kernel.  8-bit digits: 512-thread
 // tiles of 8192 keys (longer digit runs, fewer count rows) and a separate
 // per-tile count kernel per pass.
-// Pairs with 64-bit keys at 8-bit digits: 512 x 16 tiles (8192 pairs, 32-pair
-// runs), their values staged through the key buffer after the keys are
-// written (k_tile_pass STAGE_V).  A compute-free skeleton of the pair scatter
-// (tools/run_probe, 2^28 pairs) runs 1219 us with 16-pair runs and 1096 us
-// with 32-pair runs.  LIBSORT_TP8_PAIR_ITEMS=8 keeps the 4096-pair tiles.
+// Pairs with 64-bit keys at 8-bit digits: 16 pairs per thread, their values
+// staged through the key buffer after the keys are written (k_tile_pass
+// STAGE_V).  A compute-free skeleton of the pair scatter (tools/run_probe,
+// 2^28 pairs) runs 1219 us with 16-pair runs and 1096 us with 32-pair runs.
+// (u64, u32) pairs: 1024-thread tiles of 16384 pairs (64-pair runs; LDS 137
+// KB, one block per CU): the pass is its two run-scatter store phases
+// (tools/pairpass_lab ablations), and longer runs cost less: 1406 vs 1505 us
+// per 2^28-pair pass in the lab, profiles/r05o_pairpass_t16k.txt.
+// LIBSORT_TP8_PAIR_BLOCK=512 keeps the 8192-pair tiles, LIBSORT_TP8_PAIR_ITEMS=8
+// halves either.
 #ifndef LIBSORT_TP8_PAIR_ITEMS
 #define LIBSORT_TP8_PAIR_ITEMS 16
 #endif
@@ -3794,13 +3800,29 @@ constexpr int tp_items(int bits) {
 #ifndef LIBSORT_TP4_BLOCK
 #define LIBSORT_TP4_BLOCK 256  // threads of a 4-bit tile (A/B knob)
 #endif
-template <typename K>
+#ifndef LIBSORT_TP8_PAIR_BLOCK
+#define LIBSORT_TP8_PAIR_BLOCK 1024  // threads of an 8-bit tile of (u64, u32) pairs
+#endif
+template <typename K, typename V = NoValue>
 constexpr int tp_block(int bits) {
-  return bits == 4 ? LIBSORT_TP4_BLOCK : (sizeof(K) == 8 ? LIBSORT_TP8_BLOCK64 : LIBSORT_TP8_BLOCK);
+  return bits == 4 ? LIBSORT_TP4_BLOCK
+         : sizeof(K) == 8 ? (std::is_same<V, uint32_t>::value ? LIBSORT_TP8_PAIR_BLOCK : LIBSORT_TP8_BLOCK64)
+                          : LIBSORT_TP8_BLOCK;
+}
+// The MSD hybrid's depths >= 1 of (u64, u32) pairs keep 512-thread tiles of
+// 8192 pairs: their tiles come from a table, and the table load that gives
+// a tile its first key precedes every key load, a latency that one block per
+// CU cannot hide (the 16384-pair pass there: 1440 -> 1530 us; at depth 0 and
+// in the LSD passes, which compute their tiles, 1622 -> 1530 us with the
+// digit stream).
+template <typename K, typename V = NoValue>
+constexpr int tp_block_tab(int bits) {
+  return (bits == 8 && sizeof(K) == 8 && std::is_same<V, uint32_t>::value) ? LIBSORT_TP8_BLOCK64
+                                                                           : tp_block<K, V>(bits);
 }
 template <typename K, typename V = NoValue>
 uint32_t tp_tiles(size_t n, int bits) {
-  const uint64_t t = (uint64_t)tp_block<K>(bits) * tp_items<K, V>(bits);
+  const uint64_t t = (uint64_t)tp_block<K, V>(bits) * tp_items<K, V>(bits);
   return (uint32_t)((n + t - 1) / t);
 }
 inline uint32_t tp_chunks(uint32_t tiles, int bits) {
@@ -3814,7 +3836,7 @@ hipError_t tiles_counts(Workspace& ws, const K* in, size_t n, Op op, uint32_t ti
   // the same tiles as the pass kernel, a different block shape: 4-bit u32
   // tiles are counted by 512 threads x 8 keys (179 -> 170 us at 2^28 keys,
   // interleaved A/B; the pass itself is faster as 256 x 16)
-  constexpr int B = tp_block<K>(BITS);
+  constexpr int B = tp_block<K, V>(BITS);
   constexpr int CB = (BITS == 4 && sizeof(K) == 4) ? 512 : B;
   constexpr int CI = B * tp_items<K, V>(BITS) / CB;
   static_assert(CB * CI == B * tp_items<K, V>(BITS), "count tiles = pass tiles");
@@ -3918,10 +3940,9 @@ hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, 
 
 // Counts of an 8-bit pass from the digit stream (tiles: the pass's tiles, or
 // a hybrid depth's table when tab != null).
-template <typename K, typename V, bool TAB = false>
+template <typename K, typename V, bool TAB = false, int B = tp_block<K, V>(8)>
 hipError_t tiles_counts_u8(Workspace& ws, size_t n, uint32_t rows, uint32_t* C, const uint4* tab,
                            const uint32_t* ntab, hipStream_t st) {
-  constexpr int B = tp_block<K>(8);
   constexpr int TILE = B * tp_items<K, V>(8);
   ScopedTimer tm("tilecounts", st, n);
   hipLaunchKernelGGL((k_tile_counts_u8<B, TILE, TAB>), dim3(rows), dim3(B), 0, st, ws.dstream, (uint32_t)n, C, tab,
@@ -3932,7 +3953,7 @@ hipError_t tiles_counts_u8(Workspace& ws, size_t n, uint32_t rows, uint32_t* C, 
 template <int BITS, typename K, typename V, typename Op = RadixDigit>
 hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout, size_t n, int p, int P,
                       int lo, int hi, hipStream_t st, uint32_t bias = 0) {
-  constexpr int B = tp_block<K>(BITS);
+  constexpr int B = tp_block<K, V>(BITS);
   const uint32_t tiles = tp_tiles<K, V>(n, BITS);
   const int shift = lo + BITS * p;
   const int nb = std::min(BITS, hi - shift);
@@ -4263,9 +4284,14 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
                        uint32_t bias, hipStream_t st, bool* handled, uint64_t span = 0,
                        const HybPieces* pc = nullptr) {
   constexpr int RADIX = 1 << BITS;
-  constexpr int B = tp_block<K>(BITS);
+  // depths >= 1 (tiles from a table) and depth 0 of a whole array (tiles
+  // computed: B0 threads, TILE0 keys; the same but for (u64, u32) pairs)
+  constexpr int B = tp_block_tab<K, V>(BITS);
   constexpr int ITEMS = tp_items<K, V>(BITS);
   constexpr int TILE = B * ITEMS;
+  constexpr int B0 = tp_block<K, V>(BITS);
+  constexpr int TILE0 = B0 * ITEMS;
+  static_assert(TILE0 == TILE || !std::is_same<V, NoValue>::value, "keys-only: one tile size");
   // digit passes: 16 / BITS over the top 16 of the W bits, or (pieces) the
   // caller's count; the last one writes out: depth k writes out when
   // depths - 1 - k is even, tmp otherwise (depth 0 reads in)
@@ -4308,7 +4334,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   const int extra = cls == 5 ? 24 : cls == 4 ? 12 : 6;  // second block: 6 (12, 24) x 256 more slots
   const uint32_t cap1 = (uint32_t)BBc * (((uint32_t)kItems1[cls] * 256u + BBc - 1) / BBc);
   const uint32_t cap = (uint32_t)BBc * (((uint32_t)(kItems1[cls] + extra) * 256u + BBc - 1) / BBc);
-  const uint32_t T0 = pc ? pc->tiles : (uint32_t)((n + TILE - 1) / TILE);
+  const uint32_t T0 = pc ? pc->tiles : (uint32_t)((n + TILE0 - 1) / TILE0);  // depth 0's tiles
+  const uint32_t Tt = pc ? pc->tiles : (uint32_t)((n + TILE - 1) / TILE);    // n in table-depth tiles
   // reserved depth 0 (32-bit keys only, in != out: the fallback re-reads in):
   // no count pass; depth 0 writes slices of ws.rsv (tile rows of depth 1
   // numbered by slice capacity, at most tb1)
@@ -4342,7 +4369,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
   uint32_t sseq = 0;  // the last depth's children (bucket stats)
   // segments of depth k (each child has at most one partial tile)
   auto nseg_at = [&](int k) { return nseg0 << (BITS * k); };
-  auto tbound = [&](int k) { return k == 0 ? T0 : (k == 1 && rsv) ? tb1 : T0 + nseg_at(k); };
+  auto tbound = [&](int k) { return k == 0 ? T0 : (k == 1 && rsv) ? tb1 : Tt + nseg_at(k); };
   uint32_t TB = 0;
   for (int k = 0; k < DEPTHS; ++k) TB = std::max(TB, tbound(k));
   LS_TRY(ws.ensure_tiles((size_t)TB * RADIX, ((size_t)tp_chunks(TB, BITS) + 1) * RADIX));
@@ -4487,7 +4514,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
                                            BITS == 4 ? T0 * (uint32_t)RADIX : 0u, st)));
     } else if (BITS == 8 && dstream && k > 0) {
       // the digits depth k - 1 wrote (1 B per key)
-      LS_TRY((tiles_counts_u8<K, V, true>(ws, n, rows, C, tiles[k & 1], ctr + k, st)));
+      LS_TRY((tiles_counts_u8<K, V, true, B>(ws, n, rows, C, tiles[k & 1], ctr + k, st)));
     } else if (BITS == 8 || k == 0) {
       ScopedTimer tm("tilecounts", st, n);
       hipLaunchKernelGGL((k_tile_counts<BITS, B, ITEMS, K, Op, true>), dim3(rows), dim3(B), 0, st, src,
@@ -4535,16 +4562,16 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       ScopedTimer tm("tilepass", st, n);
       if (BITS == 4 && !last) {
         if (!tab)
-          hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 2, kAnyOrder>),
-                             dim3(rows), dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C,
+          hipLaunchKernelGGL((k_tile_pass<BITS, B0, ITEMS, K, V, BITS == 4, Op, Op, 2, kAnyOrder>),
+                             dim3(rows), dim3(B0), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C,
                              ws.tb, segbase, Cn, geo);
         else
           hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, BITS == 4, Op, Op, 3, kAnyOrder>),
                              dim3(rows), dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C,
                              ws.tb, segbase, Cn, geo);
       } else if (!tab) {
-        hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, false, Op, Op, 0, kAnyOrder>), dim3(rows),
-                           dim3(B), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase,
+        hipLaunchKernelGGL((k_tile_pass<BITS, B0, ITEMS, K, V, false, Op, Op, 0, kAnyOrder>), dim3(rows),
+                           dim3(B0), 0, st, src, dst, vsrc, vdst, (uint32_t)n, op, op_next, C, ws.tb, segbase,
                            Cn, geo);
       } else {
         hipLaunchKernelGGL((k_tile_pass<BITS, B, ITEMS, K, V, false, Op, Op, 1, kAnyOrder>), dim3(rows),

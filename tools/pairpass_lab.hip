@@ -288,12 +288,13 @@ int main(int argc, char** argv) {
   const char* filt = argc > 1 ? argv[1] : nullptr;
   const RadixDigit op{56, 255}, opn{48, 255};
   uint64_t *kin, *kout;
-  uint32_t *vin, *vout, *gofs, *C, *Bz, *Dz;
+  uint32_t *vin, *vout, *gofs, *gofs16, *C, *Bz, *Dz;
   uint8_t* dout;
   CK(hipMalloc(&kin, n * 8)); CK(hipMalloc(&kout, n * 8));
   CK(hipMalloc(&vin, n * 4)); CK(hipMalloc(&vout, n * 4));
   CK(hipMalloc(&dout, n));
   CK(hipMalloc(&gofs, (size_t)T * 256 * 4));
+  CK(hipMalloc(&gofs16, (size_t)(T / 2) * 256 * 4));
   CK(hipMalloc(&C, (size_t)T * 256 * 4));
   CK(hipMalloc(&Bz, (size_t)T * 256 * 4));
   CK(hipMalloc(&Dz, 256 * 4));
@@ -306,11 +307,13 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill, dim3((n + 255) / 256), dim3(256), 0, st, kin, vin, n);
   CK(hipStreamSynchronize(st));
   // run offsets on the host: gofs[t][d] = digit start + keys of digit d in tiles < t
-  {
+  // (gofs16: the same over 16384-pair tiles)
+  for (int tl : {TILE, 2 * TILE}) {
+    const uint32_t T = (uint32_t)(n / tl);
     std::vector<uint64_t> hk(n);
     CK(hipMemcpy(hk.data(), kin, n * 8, hipMemcpyDeviceToHost));
     std::vector<uint32_t> cnt((size_t)T * 256, 0), g((size_t)T * 256);
-    for (size_t i = 0; i < n; ++i) cnt[(i / TILE) * 256 + (hk[i] >> 56)]++;
+    for (size_t i = 0; i < n; ++i) cnt[(i / tl) * 256 + (hk[i] >> 56)]++;
     std::vector<uint64_t> tot(256, 0);
     for (uint32_t t = 0; t < T; ++t)
       for (int d = 0; d < 256; ++d) tot[d] += cnt[(size_t)t * 256 + d];
@@ -322,8 +325,12 @@ int main(int argc, char** argv) {
         g[(size_t)t * 256 + d] = (uint32_t)cur[d];
         cur[d] += cnt[(size_t)t * 256 + d];
       }
-    CK(hipMemcpy(gofs, g.data(), g.size() * 4, hipMemcpyHostToDevice));
-    CK(hipMemcpy(C, g.data(), g.size() * 4, hipMemcpyHostToDevice));
+    if (tl == TILE) {
+      CK(hipMemcpy(gofs, g.data(), g.size() * 4, hipMemcpyHostToDevice));
+      CK(hipMemcpy(C, g.data(), g.size() * 4, hipMemcpyHostToDevice));
+    } else {
+      CK(hipMemcpy(gofs16, g.data(), g.size() * 4, hipMemcpyHostToDevice));
+    }
   }
   struct V { std::string name; int check; std::function<void()> launch; };
   std::vector<V> vs;
@@ -355,6 +362,12 @@ int main(int argc, char** argv) {
       else hipLaunchKernelGGL((k_pair_pass_tpb<512, 16, false, 1, A>), dim3(T), dim3(512), 0, st, kin, kout, vin,    \
                               vout, dout, gofs, op, opn); }});
     ABLV(1) ABLV(2) ABLV(3)
+    // 16384-pair tiles (64-pair runs), one 1024-thread block per CU (LDS 137 KB)
+    vs.push_back({std::string("t16k 1024x16") + (D ? " dout" : ""), D ? 2 : 1, [=] {
+      if (D) hipLaunchKernelGGL((k_pair_pass_tpb<1024, 16, true, 1>), dim3(T / 2), dim3(1024), 0, st, kin, kout, vin,
+                                vout, dout, gofs16, op, opn);
+      else hipLaunchKernelGGL((k_pair_pass_tpb<1024, 16, false, 1>), dim3(T / 2), dim3(1024), 0, st, kin, kout, vin,
+                              vout, dout, gofs16, op, opn); }});
   }
   vs.push_back({"copy", -1, [=] {
     hipLaunchKernelGGL((k_pair_copy<512, 16>), dim3(T), dim3(512), 0, st, kin, kout, vin, vout); }});
