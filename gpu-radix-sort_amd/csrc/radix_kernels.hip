@@ -1342,10 +1342,10 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
     }
 #pragma unroll
     for (int q = 0; q < Q16; ++q)
-      if (tid + q * BLOCK < n16) st16[tid + q * BLOCK] = w16[q];
+      if ((uint32_t)(tid + q * BLOCK) < n16) st16[tid + q * BLOCK] = w16[q];
 #pragma unroll
     for (int q = 0; q < Q8; ++q)
-      if (tid + q * BLOCK < n8) st8[tid + q * BLOCK] = w8[q];
+      if ((uint32_t)(tid + q * BLOCK) < n8) st8[tid + q * BLOCK] = w8[q];
     __syncthreads();
     const uint16_t* const l16 = reinterpret_cast<const uint16_t*>(st + a16);
     const uint8_t* const l8 = reinterpret_cast<const uint8_t*>(st8) + a8;
@@ -3806,7 +3806,8 @@ constexpr int tp_items(int bits) {
 template <typename K, typename V = NoValue>
 constexpr int tp_block(int bits) {
   return bits == 4 ? LIBSORT_TP4_BLOCK
-         : sizeof(K) == 8 ? (std::is_same<V, uint32_t>::value ? LIBSORT_TP8_PAIR_BLOCK : LIBSORT_TP8_BLOCK64)
+         : sizeof(K) == 8 ? ((bits == 8 && std::is_same<V, uint32_t>::value) ? LIBSORT_TP8_PAIR_BLOCK
+                                                                             : LIBSORT_TP8_BLOCK64)
                           : LIBSORT_TP8_BLOCK;
 }
 // The MSD hybrid's depths >= 1 of (u64, u32) pairs keep 512-thread tiles of
@@ -3830,13 +3831,13 @@ inline uint32_t tp_chunks(uint32_t tiles, int bits) {
   return (tiles + ch - 1) / ch;
 }
 
-template <int BITS, typename K, typename Op = RadixDigit, typename V = NoValue>
+template <int BITS, typename K, typename Op = RadixDigit, typename V = NoValue, int B = tp_block<K, V>(BITS)>
 hipError_t tiles_counts(Workspace& ws, const K* in, size_t n, Op op, uint32_t tiles, uint32_t* C,
                         uint32_t* zero, uint32_t zero_words, hipStream_t st) {
-  // the same tiles as the pass kernel, a different block shape: 4-bit u32
-  // tiles are counted by 512 threads x 8 keys (179 -> 170 us at 2^28 keys,
-  // interleaved A/B; the pass itself is faster as 256 x 16)
-  constexpr int B = tp_block<K, V>(BITS);
+  // the same tiles as the pass kernel (B threads of tp_items keys), a
+  // different block shape: 4-bit u32 tiles are counted by 512 threads x 8
+  // keys (179 -> 170 us at 2^28 keys, interleaved A/B; the pass itself is
+  // faster as 256 x 16)
   constexpr int CB = (BITS == 4 && sizeof(K) == 4) ? 512 : B;
   constexpr int CI = B * tp_items<K, V>(BITS) / CB;
   static_assert(CB * CI == B * tp_items<K, V>(BITS), "count tiles = pass tiles");
@@ -5152,11 +5153,16 @@ hipError_t partition_op_impl(Workspace& ws, const K* in, K* out, const V* vin, V
                              const Workspace::PartToken& tok, int nbuckets, uint32_t* d_bounds, hipStream_t st,
                              int phase, uint16_t* o16 = nullptr, uint8_t* o8 = nullptr) {
   constexpr int RADIX = 1 << BITS;
-  constexpr int B = tp_block<K>(BITS);
-  const uint32_t tiles = tp_tiles<K>(n, BITS);
+  // ((u64, u32) pairs at 8 bits: 8192-pair tiles whose payloads are staged
+  // through the key buffer; per 2^28 pairs, count + scatter 1.73 ms against
+  // 1.82 with the sort's 16384-pair tiles and 1.90 with 4096-pair tiles and
+  // LDS of their own, tools/partition_time.py, profiles/r05t_*)
+  constexpr int B = tp_block_tab<K, V>(BITS);
+  constexpr int TILE = B * tp_items<K, V>(BITS);
+  const uint32_t tiles = (uint32_t)((n + TILE - 1) / TILE);
   if (phase != kPartScatter) {
     LS_TRY(ws.ensure_tiles((size_t)tiles * RADIX, ((size_t)tp_chunks(tiles, BITS) + 1) * RADIX));
-    LS_TRY((tiles_counts<BITS, K, Op>(ws, in, n, op, tiles, ws.tc[0], nullptr, 0, st)));
+    LS_TRY((tiles_counts<BITS, K, Op, V, B>(ws, in, n, op, tiles, ws.tc[0], nullptr, 0, st)));
     LS_TRY(tiles_colscan<BITS>(ws, ws.tc[0], tiles, st));
     if (d_bounds)
       LS_TRY(hipMemcpyAsync(d_bounds, tiles_digit_starts(ws, tiles, BITS), (size_t)nbuckets * sizeof(uint32_t),
@@ -5174,7 +5180,7 @@ hipError_t partition_op_impl(Workspace& ws, const K* in, K* out, const V* vin, V
     HybridGeo g{};
     g.o16 = o16;  // (24-bit planes instead of out: the multi-GPU exchange)
     g.o8 = o8;
-    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K>(BITS), K, V, false, Op>), dim3(tiles), dim3(B), 0, st, in,
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K, V>(BITS), K, V, false, Op>), dim3(tiles), dim3(B), 0, st, in,
                        out, vin, vout, (uint32_t)n, op, RadixDigit{0u, 1u}, ws.tc[0], (const uint32_t*)ws.tb,
                        (const uint32_t*)tiles_digit_starts(ws, tiles, BITS), ws.tc[1], g);
     LS_TRY(hipGetLastError());
