@@ -9,7 +9,7 @@ OUT=${1:-gpurun_out/pmc_c5}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 B=(python3 bench.py --workload c5 --steps 4 --warmup 1 --no-variants --no-cpu-baseline --no-host-abi --no-legs)
-RE="tile_pass|bucket_sort|tile_counts"
+RE="tile_pass|bucket_sort|bucket_pairs|tile_counts"
 bash tools/pmc_cmd.sh "$OUT" "$RE" "${B[@]}" || exit 1
 timeout -s KILL 90 rocprofv3 --kernel-trace --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
   TCP_UTCL1_REQUEST_sum TCP_UTCL1_PERMISSION_MISS_sum -d "$OUT/p_tlb" -o run --output-format csv \
