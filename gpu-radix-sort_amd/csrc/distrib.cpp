@@ -512,7 +512,7 @@ bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<co
                    bool planar, int H, std::vector<std::vector<uint64_t>>& Cp, std::vector<uint64_t>& first) {
   const int R = (int)c.ranks.size();
   constexpr int NB = dplan::kTopDigits;
-  first.assign((size_t)R * H + 1, 0);
+  first.assign((size_t)R * H, 0);
   for (int r = 0; r < R; ++r) {
     RankState& s = c.ranks[r];
     if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !s.part.ensure(s.dev, std::max<uint64_t>(n[r], 1) * sizeof(K)) ||
@@ -569,7 +569,7 @@ bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<co
     if (!ok_hip(hipEventSynchronize(c.ranks[r].ev_bounds), "hipEventSynchronize")) return false;
     for (int h = 0; h < H; ++h) {
       const size_t v = (size_t)r * H + h;
-      const uint64_t m = (h + 1 < H ? first[v + 1] : n[r]) - first[v];
+      const uint64_t m = (h + 1 < H ? first[v + 1] : n[r]) - first[v];  // (part h's keys)
       const uint32_t* b = c.h_bounds + v * NB;
       for (int g = 0; g < NB; ++g) {
         Cp[v][g] = m ? (g + 1 < NB ? (uint64_t)b[g + 1] : m) - b[g] : 0;
@@ -577,7 +577,6 @@ bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<co
       }
     }
   }
-  first.pop_back();
   return true;
 }
 
