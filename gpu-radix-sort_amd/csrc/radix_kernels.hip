@@ -3907,6 +3907,15 @@ inline bool bucket2_inline_on() {
   return on;
 }
 
+// Threads of the 3-bit retry blocks over the 2-bit kernel's overflowed
+// buckets (a persistent LIST launch).  512 (half the keys per thread, twice
+// the threads per CU at the same register budget): headline bucket phase
+// 440-445 -> 434-437 us, 3 interleaved runs each (profiles/r05y_*).
+#ifndef LIBSORT_RETRY_BLOCK
+#define LIBSORT_RETRY_BLOCK 512
+#endif
+constexpr int kRetryBlock = LIBSORT_RETRY_BLOCK;
+
 // (u64 key, u32 payload) buckets by the counting placement (k_bucket_pairs);
 // LIBSORT_PAIR_COUNT=0 keeps the LSD steps + fix-up (A/B).
 inline bool pair_count_on() {
@@ -4707,8 +4716,8 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
 #define LS_BSL(B, I)                                                                                               \
   if constexpr (C) {                                                                                               \
     if (two && (!inl || n2 > 0)) {                                                                                 \
-      hipLaunchKernelGGL((k_bucket_count<256, (I), Op, kCnt3F, true>),                                             \
-                         dim3(std::min<uint32_t>(NB, (uint32_t)std::max(1, ws.num_cus) * 5)), dim3(256), 0, st,    \
+      hipLaunchKernelGGL((k_bucket_count<kRetryBlock, ((I) * 256 + kRetryBlock - 1) / kRetryBlock, Op, kCnt3F, true>), \
+                         dim3(std::min<uint32_t>(NB, (uint32_t)std::max(1, ws.num_cus) * 5)), dim3(kRetryBlock), 0, st, \
                          reinterpret_cast<const uint32_t*>(out), reinterpret_cast<uint32_t*>(out), bstart, nsize,  \
                          ctr + 15, NB, flist, lbits, bias, ctr + 10, nullptr, 0u, ctr + 7, flist2, nullptr,        \
                          nullptr);                                                                                 \
