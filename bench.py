@@ -430,6 +430,12 @@ def main():
         host_abi = None
         if world == 1 and not args.no_host_abi and args.workload == "c2":
             host_abi = host_abi_leg(torch, pylibsort, keys, out)
+        if world == 1 and not args.no_variants and not args.no_legs and args.workload == "c2" and args.keys_log2 == 28:
+            # gpuPartial at the reference's own benchmark workload (these
+            # overwrite `out`: after every use of the line's sorted keys)
+            for w in (8, 16):
+                variants["partial%d" % w] = partial_leg(torch, pylibsort, D, keys, out, tmp, w,
+                                                        max(5, args.steps // 2))
         sched = ""
         if world > 1:
             sname = args.schedule
@@ -708,6 +714,117 @@ def config_leg(torch, pylibsort, D, which, reps):
     finally:
         pylibsort.setDigitBits(prev)
         torch.cuda.empty_cache()
+
+
+# The reference's only published numbers are gpuPartial at 2^28 keys
+# (analysis/libsort8b.csv:6-12, libsort16b.csv:6-12).
+REF_PARTIAL = {8: {"kernels_gkeys_s": 0.361, "with_memcpy_gkeys_s": 0.193,
+                   "source": "analysis/libsort8b.csv:6-12 (743.9 ms kernels, 1,392 ms with memcpy)"},
+               16: {"kernels_gkeys_s": 0.182, "with_memcpy_gkeys_s": None,
+                    "source": "analysis/libsort16b.csv:6-12 (1,475 ms kernels)"}}
+
+
+def partial_leg(torch, pylibsort, D, keys, out, tmp, width, reps, calls=3):
+    """gpuPartial at the reference's own benchmark workload
+    (localTest/benchmarks.cpp:38-51,212-215: the first 2^28 PCG keys, offset
+    0, width 16; libsort8b.csv is the same call at width 8).  Device-resident
+    (libsortSortKeysU32 with d_boundaries: the stable partition + the 2^width
+    group boundaries) with live per-kernel events, and the host ABI gpuPartial
+    on a pageable buffer (PCIe-inclusive).  Checked: the output equals the
+    input stably sorted by the group (torch.sort(stable=True) on the device),
+    the boundaries equal the exclusive prefix of the group counts, and the
+    host ABI returns the same data and boundaries."""
+    import ctypes
+    import numpy as np
+    n = keys.numel()
+    b = torch.empty(1 << width, dtype=torch.int32, device="cuda")
+
+    def step():
+        return D.sort_keys_u32(keys, out=out, tmp=tmp, offset=0, width=width, boundaries=b)
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    D.timing_reset()
+    D.timing_filter("tilepass")
+    D.timing_sample(1)
+    D.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    D.timing_enable(False)
+    launches, tms, tk = D.timing_query("tilepass")
+    D.timing_reset()
+    D.timing_filter(None)
+    D.timing_enable(True)
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    D.timing_enable(False)
+    kern = {}
+    for name in ("tilecounts", "colscan", "tilepass", "onesweep", "whist", "bounds"):
+        l_, ms_, _ = D.timing_query(name)
+        if l_:
+            kern[name] = {"launches": l_, "avg_us": round(1e3 * ms_ / l_, 2), "from": "2 steps after the timed ones"}
+    if launches:
+        kern["tilepass"] = {"launches": launches, "avg_us": round(1e3 * tms / launches, 2),
+                            "keys_per_launch": tk / launches, "from": "the timed steps"}
+    # checks (outside the timed region)
+    mask = (1 << width) - 1
+    grp = keys & mask
+    _, idx = torch.sort(grp, stable=True)
+    ok = bool(torch.equal(keys[idx], out))
+    del idx
+    cnt = torch.bincount(grp.to(torch.int64), minlength=1 << width)
+    pref = torch.cumsum(cnt, 0) - cnt
+    ok = ok and bool(torch.equal(pref.to(torch.int32), b))
+    del grp, cnt, pref
+    ms = 1e3 * (t1 - t0) / reps
+    leg = {"call": "libsortSortKeysU32(d_keys, ..., offset 0, width %d, d_boundaries): device-resident gpuPartial"
+                   % width,
+           "ms_per_step": round(ms, 4), "value": round(n / (ms * 1e-3) / 1e9, 3), "unit": "Gkeys/s",
+           "digit_bits": pylibsort.getDigitBits(), "kernels": kern, "verified": ok,
+           "reference": dict(REF_PARTIAL[width], note="agpu1 (2 x 4 GiB GPUs, model unnamed), same call and keys")}
+    leg["vs_reference_kernels"] = round(leg["value"] / REF_PARTIAL[width]["kernels_gkeys_s"], 1)
+    tp = kern.get("tilepass")
+    if tp and tp.get("keys_per_launch"):
+        ach = 8.0 * tp["keys_per_launch"] / (tp["avg_us"] * 1e-6) / 1e9
+        leg["pass_roofline"] = {"achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                                "frac": round(ach / HBM_PEAK_GBPS, 4), "bytes_per_key": 8.0}
+    # the whole call against HBM: per digit pass one count read (4 B/key) and
+    # the pass (8 B/key); the boundaries are 2^width words
+    passes = -(-width // pylibsort.getDigitBits())
+    step_bytes = n * 12.0 * passes
+    leg["step_roofline"] = {"bytes_per_key": 12.0 * passes, "achieved": round(step_bytes / (ms * 1e-3) / 1e9, 1),
+                            "frac": round(step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                            "note": "%d digit pass(es), each a 4 B/key count read + an 8 B/key pass" % passes}
+    # host ABI (pageable buffer: H2D + partition + boundaries + D2H)
+    src = keys.cpu().numpy()
+    want = out.cpu().numpy()
+    want_b = b.cpu().numpy().view(np.uint32).copy()
+    buf = np.empty_like(src)
+    bnd = (ctypes.c_uint32 * (1 << width))()
+    L = pylibsort.lib()
+    ts = []
+    for _ in range(calls):
+        np.copyto(buf, src)
+        h0 = time.perf_counter()
+        if L.gpuPartial(buf.ctypes.data, ctypes.addressof(bnd), buf.size, 0, width) != 1:
+            raise RuntimeError("gpuPartial failed: %s" % pylibsort.last_error())
+        ts.append(time.perf_counter() - h0)
+    same = bool(np.array_equal(buf, want)) and bool(np.array_equal(np.frombuffer(bnd, dtype=np.uint32), want_b))
+    t = sorted(ts)[len(ts) // 2]
+    leg["host_abi"] = {"call": "gpuPartial (libsort.h, invokers.cu:15-41) on a pageable host buffer",
+                       "ms": round(t * 1e3, 2), "value": round(n / t / 1e9, 3), "calls": calls,
+                       "equal_to_device_result": same,
+                       "note": "PCIe-inclusive (H2D + partition + boundaries + D2H), median of %d calls" % calls}
+    if REF_PARTIAL[width]["with_memcpy_gkeys_s"]:
+        leg["host_abi"]["vs_reference_with_memcpy"] = round(leg["host_abi"]["value"] /
+                                                            REF_PARTIAL[width]["with_memcpy_gkeys_s"], 1)
+    if not (ok and same):
+        raise RuntimeError("partial%d leg failed verification (device %s, host ABI %s)" % (width, ok, same))
+    return leg
 
 
 def host_abi_leg(torch, pylibsort, keys, sorted_keys, calls=3):

@@ -44,10 +44,13 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>  // types only: the functions are resolved with dlsym
+#include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <map>
 #include <memory>
@@ -69,6 +72,37 @@ bool ok_hip(hipError_t e, const char* what) {
   (void)hipGetLastError();
   return false;
 }
+
+// ---------------------------------------------------------------------------
+// Stage trace (libsortSetDistribTrace / LIBSORT_DISTRIB_TRACE=1): one stderr
+// line per stage, so that a multi-GPU run that hangs names the stage it
+// stopped at.  While tracing, the round sorts wait on the
+// host for their round's arrival and completion (serialised: diagnostics).
+// ---------------------------------------------------------------------------
+std::atomic<int> g_trace{[] {
+  const char* e = getenv("LIBSORT_DISTRIB_TRACE");
+  return e && e[0] == '1' ? 1 : 0;
+}()};
+std::mutex g_trace_mu;
+std::chrono::steady_clock::time_point g_trace_t0 = std::chrono::steady_clock::now();
+
+bool tracing() { return g_trace.load(std::memory_order_relaxed) != 0; }
+
+__attribute__((format(printf, 1, 2))) void trace(const char* fmt, ...) {
+  if (!tracing()) return;
+  const double ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - g_trace_t0).count();
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  fprintf(stderr, "libsort distrib [%9.3f ms] ", ms);
+  va_list ap;
+  va_start(ap, fmt);
+  vfprintf(stderr, fmt, ap);
+  va_end(ap);
+  fputc('\n', stderr);
+  fflush(stderr);
+}
+
+void trace_start() { g_trace_t0 = std::chrono::steady_clock::now(); }
 
 // ---------------------------------------------------------------------------
 // RCCL, loaded on first use: libsort.so does not link it, so callers that
@@ -265,7 +299,10 @@ struct Ctx {
     if (!comms.empty()) return true;
     if (!g_rccl.load()) return false;
     comms.assign(devs.size(), nullptr);
-    return g_rccl.ok(g_rccl.commInitAll(comms.data(), (int)devs.size(), devs.data()), "ncclCommInitAll");
+    trace("RCCL: ncclCommInitAll over %zu devices", devs.size());
+    const bool ok = g_rccl.ok(g_rccl.commInitAll(comms.data(), (int)devs.size(), devs.data()), "ncclCommInitAll");
+    trace("RCCL: communicators %s", ok ? "ready" : "FAILED");
+    return ok;
   }
 };
 
@@ -400,6 +437,7 @@ bool run_lsd(Ctx& c, const std::vector<const uint32_t*>& in, const std::vector<u
           !ok_hip(hipEventRecord(s.ev_part, s.d->st), "hipEventRecord"))
         return false;
     }
+    trace("lsd step %d: local partial sorts issued", step);
     std::vector<std::vector<uint64_t>> C(R, std::vector<uint64_t>(256));
     for (int r = 0; r < R; ++r) {
       if (!ok_hip(hipEventSynchronize(c.ranks[r].ev_part), "hipEventSynchronize")) return false;
@@ -414,7 +452,9 @@ bool run_lsd(Ctx& c, const std::vector<const uint32_t*>& in, const std::vector<u
       src[r] = c.ranks[r].part.p;
       dst[r] = c.ranks[r].recv.p;
     }
+    trace("lsd step %d: bucket counts read, exchange of %zu pieces", step, o.pieces.size());
     if (!move_pieces(c, o.pieces, src, dst, 4, use_rccl, self_rccl)) return false;
+    trace("lsd step %d: exchange issued", step);
     // gather into bucket-major / rank-minor order on the compute stream.
     // Every compute stream waits for EVERY device's communication stream: a
     // peer copy (copy mode across devices) is pulled on the receiver's stream
@@ -433,6 +473,7 @@ bool run_lsd(Ctx& c, const std::vector<const uint32_t*>& in, const std::vector<u
       cur[r] = nxt;
       n_cur[r] = o.n_next[r];
     }
+    trace("lsd step %d: segment gathers issued", step);
   }
   return true;
 }
@@ -473,8 +514,10 @@ struct Hold {
       if (!ws_acquire_stream(u->dev, u->st)) ok = false;
   }
   bool finish(bool result) {
+    trace("finish: waiting for every stream");
     const bool synced = sync_all(c);
     for (auto& u : c.uniq) ws_release_stream(u->dev, u->st);
+    trace("done: %s", result && synced ? "ok" : last_error());
     return result && synced;
   }
 };
@@ -562,6 +605,8 @@ bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<co
     }
     if (!ok_hip(hipEventRecord(s.ev_part, s.d->st), "hipEventRecord")) return false;
   }
+  trace("partition (%s digit%s, %d part%s): counts + scatter issued on %d ranks", pd.range ? "range" : "top",
+        planar ? ", 24-bit planes" : "", H, H > 1 ? "s" : "", R);
   C.assign(R, std::vector<uint64_t>(NB, 0));
   Cp.assign((size_t)R * H, std::vector<uint64_t>(NB, 0));
   for (int r = 0; r < R; ++r) {
@@ -577,6 +622,7 @@ bool partition_top(Ctx& c, const std::vector<const K*>& in, const std::vector<co
       }
     }
   }
+  trace("partition: bucket counts read");
   return true;
 }
 
@@ -674,6 +720,10 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
       if (s.d != &d) continue;
       const uint64_t a = p.roff[(size_t)r * (K_ + 1) + i], z = p.roff[(size_t)r * (K_ + 1) + i + 1];
       if (!ok_hip(hipStreamWaitEvent(d.st, s.ev_x[i], 0), "wait")) return false;
+      if (tracing()) {
+        if (!ok_hip(hipEventSynchronize(s.ev_x[i]), "hipEventSynchronize")) return false;
+        trace("round %d rank %d: arrived (%llu keys)", i, r, (unsigned long long)(z - a));
+      }
       if (z == a) continue;
       hipError_t e;
       const size_t q = (size_t)r * K_ + i;
@@ -695,6 +745,10 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
                                static_cast<uint64_t*>(d.tmp.p), d.tmpv.u32(), z - a, 0, 64, bits, d.st);
       }
       if (!ok_hip(e, "round sort")) return false;
+      if (tracing()) {
+        if (!ok_hip(hipStreamSynchronize(d.st), "hipStreamSynchronize")) return false;
+        trace("round %d rank %d: sorted", i, r);
+      }
     }
     return true;
   };
@@ -752,6 +806,7 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
   };
   // round i has been issued: its arrival event, then its sorts may go
   auto issued_round = [&](int i) -> bool {
+    trace("round %d: exchange issued (%zu pieces)", i, p.rounds[i].size());
     for (int r = 0; r < R; ++r) {
       RankState& s = c.ranks[r];
       if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !ok_hip(hipEventRecord(s.ev_x[i], s.d->cs), "record"))
@@ -806,6 +861,7 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
   }
   if (!comm_waits(c, &RankState::ev_done)) return false;
   const std::vector<dplan::Piece>& cut = pl.moves;
+  trace("rounds sorted; re-cut of %zu pieces", cut.size());
   for (int r = 0; r < R; ++r) {
     src[r] = c.ranks[r].outb.p;
     dst[r] = out[r];
@@ -818,14 +874,19 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
          (!pairs || move_pieces(c, cut, vsrc, vdst, 4, use_rccl, self_rccl, false));
 }
 
-// Partition parts per rank: two when there is an exchange to overlap (R > 1;
-// LIBSORT_DISTRIB_PARTS=1 keeps one).
-int parts_for(int R) {
+// Partition parts per rank: two when there is an RCCL exchange between
+// distinct GPUs to overlap with the second part's partition; one otherwise
+// (ranks sharing a GPU exchange by device copies, which two parts only double:
+// +32 us of kernels per rank, 6.9 -> 7.7 ms in DESIGN.md 3d).
+// The two-part gain comes from tools/msd_model.py and has not been measured
+// across GPUs.  LIBSORT_DISTRIB_PARTS=1 / 2 forces one / two (tests, A/B).
+int parts_for(int R, bool rccl_between_gpus) {
   static const int env = [] {
     const char* e = getenv("LIBSORT_DISTRIB_PARTS");
-    return e && e[0] == '1' ? 1 : kMaxParts;
+    return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
   }();
-  return R > 1 ? env : 1;
+  if (R <= 1) return 1;
+  return env ? env : rccl_between_gpus ? kMaxParts : 1;
 }
 
 // Shared prologue of both entry points: sizes, the output shard counts.
@@ -855,6 +916,9 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
   const int R = (int)c.ranks.size();
   const bool copy = (flags & kDistribCopy) != 0 || !c.distinct;
   const bool self_rccl = (flags & kDistribSelfRccl) != 0 && !copy;
+  trace_start();
+  trace("sort u32: %d ranks on %zu devices, exchanges by %s, %d-bit digits, flags 0x%x", R, c.uniq.size(),
+        copy ? "device/peer copies" : "RCCL", bits, flags);
   if (!copy && !c.ensure_comms()) return false;
   std::vector<uint64_t> n;
   uint64_t N = 0;
@@ -863,9 +927,9 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
   if (!hold.ok) return hold.finish(false);
   std::vector<const uint32_t*> in(d_in, d_in + R);
   std::vector<uint32_t*> out(d_out, d_out + R);
+  c.sent.assign(R, 0);  // (before the empty return: libsortDistribLastBytes covers this call)
   if (N == 0) return hold.finish(true);
   const uint64_t S = dplan::shard_size(N, R);
-  c.sent.assign(R, 0);
   if (flags & kDistribLsd) return hold.finish(run_lsd(c, in, n, out, S, bits, !copy, self_rccl));
   const int K = std::max(1, std::min(kMaxRounds, 256 / R));
   std::vector<std::vector<uint64_t>> C;
@@ -879,14 +943,17 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
     return !(e && e[0] == '0');
   }();
   const bool planar = wire24_env && !(flags & kDistribWire32) && bits == 4;
-  const int H = parts_for(R);
+  const int H = parts_for(R, c.distinct && !copy);
   std::vector<std::vector<uint64_t>> Cp;
   std::vector<uint64_t> first;
   if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd, planar, H, Cp, first)) return hold.finish(false);
   std::vector<uint8_t> lut(dplan::kTopDigits);
   std::vector<int64_t> est(R);
   dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
+  trace("plan: %d rounds per rank, %llu keys, largest rank %lld", K, (unsigned long long)N,
+        (long long)*std::max_element(est.begin(), est.end()));
   if (dplan::msd_too_skewed(est.data(), R, N)) {
+    trace("plan: too skewed for the top digit");
     // the top digit leaves the keys in too few digits: the 8-bit digit over
     // the populated key range, if that is finer; else (or still skewed) the
     // LSD rounds from the untouched input
@@ -896,8 +963,10 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
       if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd, false, H, Cp, first)) return hold.finish(false);
       dplan::plan_digit_rounds(C, K, 1.2, lut.data(), est.data());
     }
-    if (!useful || dplan::msd_too_skewed(est.data(), R, N))
+    if (!useful || dplan::msd_too_skewed(est.data(), R, N)) {
+      trace("plan: LSD rounds");
       return hold.finish(run_lsd(c, in, n, out, S, bits, !copy, self_rccl));
+    }
   }
   return hold.finish(run_digit_rounds<uint32_t>(c, dplan::digit_plan_parts(Cp, H, first, lut.data(), K), out, nullptr,
                                                 !copy, self_rccl, bits, pd, planar && !pd.range, H));
@@ -912,6 +981,9 @@ bool sort_device_pairs(Ctx& c, const uint64_t* const* d_kin, const uint32_t* con
     set_error("distributed pair sort: the LSD rounds are for keys only");
     return false;
   }
+  trace_start();
+  trace("sort pairs u64/u32: %d ranks on %zu devices, exchanges by %s, %d-bit digits", R, c.uniq.size(),
+        copy ? "device/peer copies" : "RCCL", bits);
   if (!copy && !c.ensure_comms()) return false;
   std::vector<uint64_t> n;
   uint64_t N = 0;
@@ -927,7 +999,7 @@ bool sort_device_pairs(Ctx& c, const uint64_t* const* d_kin, const uint32_t* con
   const int K = std::max(1, std::min(kMaxRounds, 256 / R));
   std::vector<std::vector<uint64_t>> C;
   PartDigit pd;
-  const int H = parts_for(R);
+  const int H = parts_for(R, c.distinct && !copy);
   std::vector<std::vector<uint64_t>> Cp;
   std::vector<uint64_t> first;
   if (!partition_top<uint64_t>(c, kin, &vin, n, C, pd, false, H, Cp, first)) return hold.finish(false);
@@ -1010,6 +1082,8 @@ bool distrib_last_bytes(uint64_t* per_rank, int nranks) {
   for (int r = 0; r < nranks; ++r) per_rank[r] = g_ctx->sent[r];
   return true;
 }
+
+int set_distrib_trace(int on) { return g_trace.exchange(on ? 1 : 0); }
 
 void distrib_release() {
   std::lock_guard<std::mutex> glk(g_dist_mu);

@@ -1233,6 +1233,8 @@ LS_BOOL_ENTRY(libsortDistribLastBytes, int nranks, uint64_t* per_rank) {
   return 1;
 }
 
+LIBSORT_EXPORT int libsortSetDistribTrace(int on) { return set_distrib_trace(on ? 1 : 0); }
+
 LS_BOOL_ENTRY(libsortDistribRangeDigit, uint64_t lo, uint64_t hi, uint32_t key_bits, uint64_t* bias,
               uint32_t* shift) {
   if (!bias || !shift || (key_bits != 32 && key_bits != 64)) {

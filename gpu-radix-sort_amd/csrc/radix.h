@@ -280,6 +280,8 @@ constexpr unsigned kDistribWire32 = 8u;    // 32-bit keys on the wire (default: 
 // distributed sort (own pieces and the re-cut excluded); false if none ran or
 // nranks differs.
 bool distrib_last_bytes(uint64_t* per_rank, int nranks);
+// stage trace on stderr (libsortSetDistribTrace); returns the previous setting
+int set_distrib_trace(int on);
 bool distrib_sort_u32(const int* devices, int R, const uint32_t* const* d_in, const size_t* n_in, uint32_t* const* d_out,
                       size_t* n_out, unsigned flags, int digit_bits);
 // (u64 key, u32 payload) pairs, stable (configs[4]): the top-digit rounds on

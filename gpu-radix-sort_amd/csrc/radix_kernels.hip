@@ -1321,10 +1321,14 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
     static_assert(sizeof(K) * TILE >= 3 * TILE + 8, "staging fits s_keys");
     const uint32_t hi = geo.seghi[seg];
     uint8_t* const st = reinterpret_cast<uint8_t*>(s_keys);
-    const uint64_t b16 = 2 * tile_base, b8 = tile_base;
-    const uint32_t a16 = (uint32_t)(b16 & 3u), a8 = (uint32_t)(b8 & 3u);
-    const uint32_t* g16 = reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(geo.i16) + (b16 - a16));
-    const uint32_t* g8 = reinterpret_cast<const uint32_t*>(geo.i8 + (b8 - a8));
+    // (aligned on the ABSOLUTE address: a plane starts at any byte of the
+    // receive buffer -- round offset a, 2 * n_recv + a)
+    const uint8_t* const p16 = reinterpret_cast<const uint8_t*>(geo.i16) + 2 * tile_base;
+    const uint8_t* const p8 = geo.i8 + tile_base;
+    const uint32_t a16 = (uint32_t)(reinterpret_cast<uintptr_t>(p16) & 3u);
+    const uint32_t a8 = (uint32_t)(reinterpret_cast<uintptr_t>(p8) & 3u);
+    const uint32_t* g16 = reinterpret_cast<const uint32_t*>(p16 - a16);
+    const uint32_t* g8 = reinterpret_cast<const uint32_t*>(p8 - a8);
     const uint32_t n16 = (a16 + 2 * valid + 3) / 4, n8 = (a8 + valid + 3) / 4;
     uint32_t* const st16 = reinterpret_cast<uint32_t*>(st);
     uint32_t* const st8 = reinterpret_cast<uint32_t*>(st + 2 * TILE + 4);
@@ -3895,14 +3899,18 @@ inline bool bucket2_on() {
 }
 
 // kCnt2F's lightly overflowed buckets retried inline with 3-bit half cells
-// (retry3_halves) instead of by a LIST launch: LIBSORT_BUCKET2_INLINE=1 (A/B
-// only: measured 449 -> 956 us for the bucket phase of a 2^28 sort, 3
-// interleaved runs each, profiles/r05d_bucket2_inline_ab.txt -- the rarely
-// taken branch costs every block its registers and occupancy)
+// (retry3_halves) instead of by a LIST launch: an A/B build only
+// (-DLIBSORT_BUCKET2_INLINE_AB=1, then LIBSORT_BUCKET2_INLINE=1): measured
+// 449 -> 956 us for the bucket phase of a 2^28 sort, 3 interleaved runs each,
+// profiles/r05d_bucket2_inline_ab.txt -- the rarely taken branch costs every
+// block its registers and occupancy.  The product build does not instantiate it.
+#ifndef LIBSORT_BUCKET2_INLINE_AB
+#define LIBSORT_BUCKET2_INLINE_AB 0
+#endif
 inline bool bucket2_inline_on() {
   static const bool on = [] {
     const char* s = getenv("LIBSORT_BUCKET2_INLINE");
-    return s && s[0] == '1';
+    return LIBSORT_BUCKET2_INLINE_AB && s && s[0] == '1';
   }();
   return on;
 }
@@ -4663,6 +4671,13 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       uint32_t* const lsd_l = two ? flist2 : flist;
       uint32_t* const rty_n = two ? ctr + 15 : nullptr;
       uint32_t* const rty_l = two ? flist : nullptr;
+#if LIBSORT_BUCKET2_INLINE_AB
+#define LS_BS_INL(B, I, G, NBP, CAPN, IL, OV, OL)                                                            \
+  hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt2F, false, true>), dim3(G), dim3(B), 0, st, ci_, co_, \
+                     bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l)
+#else
+#define LS_BS_INL(B, I, G, NBP, CAPN, IL, OV, OL) (void)0
+#endif
 #define LS_BSX(B, I, G, NBP, CAPN, IL, OV, OL)                                                                   \
   if constexpr (C) {                                                                                             \
     const uint32_t* ci_ = reinterpret_cast<const uint32_t*>(out);                                                \
@@ -4675,8 +4690,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt3>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize,  \
                          NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l);                    \
     else if (B == 256 && two && inl)                                                                             \
-      hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt2F, false, true>), dim3(G), dim3(B), 0, st, ci_, co_,    \
-                         bstart, nsize, NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l);     \
+      LS_BS_INL(B, I, G, NBP, CAPN, IL, OV, OL);                                                                 \
     else if (B == 256 && two)                                                                                    \
       hipLaunchKernelGGL((k_bucket_count<B, (I), Op, kCnt2F>), dim3(G), dim3(B), 0, st, ci_, co_, bstart, nsize, \
                          NBP, CAPN, IL, lbits, bias, OV, OL, ocap_, lsd_n, lsd_l, rty_n, rty_l);                    \
@@ -5009,10 +5023,22 @@ hipError_t sort_pieces_impl(Workspace& ws, const uint32_t* in, const PlanarPiece
   // pieces are unpacked by the gather
   if (planar) {
     if (K > 65535) return hipErrorInvalidValue;
-    ScopedTimer tm("segcopy", st, n);
-    hipLaunchKernelGGL(k_segment_copy2d_planar, dim3((uint32_t)((maxlen + kSegPiece - 1) / kSegPiece), K), dim3(256),
-                       0, st, pl.i16, pl.i8, out, ws.seg_dev + g64, K);
-    LS_TRY(hipGetLastError());
+    {
+      ScopedTimer tm("segcopy", st, n);
+      hipLaunchKernelGGL(k_segment_copy2d_planar, dim3((uint32_t)((maxlen + kSegPiece - 1) / kSegPiece), K),
+                         dim3(256), 0, st, pl.i16, pl.i8, out, ws.seg_dev + g64, K);
+      LS_TRY(hipGetLastError());
+    }
+    // the unpacked keys lie in [top byte of the first populated segment,
+    // that of the last + 1) << 24: a range sort of that span (the range
+    // hybrid for large rounds) instead of a 32-bit LSD sort -- the rounds of
+    // more than 32 segments or without the reserved depth 0
+    const uint32_t s0 = seg[keep[0]], s1 = seg[keep[K - 1]];
+    const uint32_t lo_key = (pl.hi0 + s0) << 24;
+    const uint64_t span = (uint64_t)(s1 - s0 + 1) << 24;
+    int W = 24;
+    while (((uint64_t)1 << W) < span) ++W;
+    return sort_u32(ws, out, out, tmp, n, 0, W, digit_bits, nullptr, st, lo_key, true, span);
   } else {
     LS_TRY(segment_copy_dev_u32(in, out, ws.seg_dev + g64, K, maxlen, n, st));
   }

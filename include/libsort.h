@@ -299,10 +299,21 @@ LIBSORT_API bool libsortDistribSortPairsU64U32(int nranks, const int* devices, c
                                                uint64_t* const* d_kout, uint32_t* const* d_vout, size_t* n_out,
                                                uint32_t flags);
 
-/* Both engines above, nranks > 1: each rank partitions its keys in two parts
- * (the first half, then the rest) so that the exchange of the first part's
- * pieces starts while the second part is partitioned; results are the same.
- * LIBSORT_DISTRIB_PARTS=1 in the environment keeps one part. */
+/* Both engines above, nranks > 1 on distinct GPUs over RCCL: each rank
+ * partitions its keys in two parts (the first half, then the rest) so that
+ * the exchange of the first part's pieces starts while the second part is
+ * partitioned; ranks sharing a GPU (device-copy exchanges) keep one part.
+ * Results are the same.  LIBSORT_DISTRIB_PARTS=1 / 2 in the environment
+ * forces one / two parts. */
+
+/* Stage trace of the multi-GPU engines on stderr (what a hang would stop at):
+ * one line per stage -- partition counts / scatter issued, counts read, plan,
+ * round k issued, round k arrived and sorted on each rank, re-cut -- with the
+ * milliseconds since the call started.  Tracing waits for each round's
+ * arrival on the host, so it serialises the overlap: a diagnostic, not a
+ * timing mode.  on: 1 / 0; returns the previous setting (initially
+ * LIBSORT_DISTRIB_TRACE=1 in the environment). */
+LIBSORT_API int libsortSetDistribTrace(int on);
 
 /* Bytes each rank sent to the other ranks in the exchange rounds (its own
  * pieces and the final re-cut's surplus keys excluded) in the last

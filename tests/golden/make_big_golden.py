@@ -22,9 +22,22 @@ test_maximum_size, test_config5_pairs_size), computed with the oracle here
                 (r+1)*2^29)): the concatenated output shards of the 8-rank
                 engine (test_gpu_distrib_full.test_config3_full_8ranks).
 
+  partial:      the reference's own benchmark workload (localTest/benchmarks.cpp:
+                38-51, 212-215: gpuPartialProfile of the first 2^28 keys of
+                the stream, offset 0, width 16; analysis/libsort8b.csv is the
+                same call at width 8): sha256 of the data after the stable
+                partition (oracle_partial_u32, a counting sort) and of the
+                2^width boundaries (exclusive prefix of the group counts), for
+                widths 8 and 16; the reference's GetBoundaries quirk output
+                (sort.cu:367-394, oracle_ref_boundaries) is checked equal to the
+                prefix and the exact emulation of the reference's Step kernels
+                (oracle_ref_step_u32) equal to the data first (group 1 is
+                non-empty in both).
+
 Run: python tests/golden/make_big_golden.py          (everything)
      python tests/golden/make_big_golden.py 2pow29   (adds the 2^29 class)
      python tests/golden/make_big_golden.py 2pow32   (adds the 2^32 stream)
+     python tests/golden/make_big_golden.py partial  (adds the partial workload)
 """
 import hashlib
 import json
@@ -101,8 +114,42 @@ def add_2pow32():
     path.write_text(json.dumps(out, indent=1) + "\n")
 
 
+def add_partial():
+    path = ROOT / "tests" / "golden" / "big_golden.json"
+    out = json.loads(path.read_text())
+    gold = json.loads((ROOT / "tests" / "golden" / "pcg_golden.json").read_text())["sha256_prefix"]
+    for n in (1 << 20, 1 << 28):  # the pin first
+        h = oracle.sorted_pcg_sha256(n)
+        assert h[:16] == gold[str(n)]["sorted"], (n, h)
+    n = 1 << 28
+    x = oracle.pcg(n)
+    assert hashlib.sha256(x.astype("<u4").tobytes()).hexdigest()[:16] == gold[str(n)]["input"]
+    at = out.setdefault("partial_u32", {})
+    for width in (8, 16):
+        t = time.time()
+        data, bounds = oracle.partial_u32(x, 0, width)
+        ref_b = oracle.ref_boundaries(data, 0, width)
+        assert np.array_equal(ref_b, bounds), "reference GetBoundaries quirk differs from the prefix"
+        # the exact emulation of the reference's Step kernels (2-bit passes
+        # over 128-key blocks, oracle_ref_step_u32) gives the same data
+        emu = oracle.ref_step_u32(x, 0, width)
+        assert np.array_equal(emu, data), "reference kernel emulation differs from the counting partition"
+        del emu
+        at["%d/0/%d" % (n, width)] = {
+            "data": hashlib.sha256(data.astype("<u4").tobytes()).hexdigest(),
+            "boundaries": hashlib.sha256(bounds.astype("<u4").tobytes()).hexdigest(),
+            "boundaries_head": [int(v) for v in bounds[:4]],
+            "boundaries_tail": [int(v) for v in bounds[-4:]],
+        }
+        print(width, at["%d/0/%d" % (n, width)], "%.0f s" % (time.time() - t), flush=True)
+        del data
+    path.write_text(json.dumps(out, indent=1) + "\n")
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["2pow29"]:
+    if sys.argv[1:] == ["partial"]:
+        add_partial()
+    elif sys.argv[1:] == ["2pow29"]:
         add_2pow29()
     elif sys.argv[1:] == ["2pow32"]:
         add_2pow32()

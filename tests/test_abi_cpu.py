@@ -177,6 +177,11 @@ def test_tunables_validate():
     assert pylibsort.lib().libsortSetAlgorithm(9) == -1
     prev = pylibsort.setAlgorithm("tiles")
     assert pylibsort.setAlgorithm(prev) == "tiles"
+    # the multi-GPU stage trace switch (no device needed)
+    L = pylibsort.lib()
+    prev = L.libsortSetDistribTrace(1)
+    assert L.libsortSetDistribTrace(0) == 1
+    assert L.libsortSetDistribTrace(prev) == 0
 
 
 def test_host_checkers():

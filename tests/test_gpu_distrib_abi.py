@@ -216,6 +216,38 @@ def test_wire24(D, oracle_mod, R, n):
         pylibsort.setDigitBits(prev)
 
 
+@pytest.mark.parametrize("reserve", ["on", "nomem"])
+def test_wire24_reserved_depth0_odd_offsets(D, oracle_mod, reserve):
+    """Two ranks, 2^24 + 77 keys: rounds of ~2^21 keys over <= 32 segments, so
+    the round sorts read the 24-bit planes through the reserved depth 0's
+    planar loader, at round offsets (and 8-bit plane starts 2 n_recv + a) that
+    are not multiples of 4 (the loader aligns on the absolute
+    address).  reserve=nomem: the reserved depth 0 is unavailable, so the
+    rounds take the unpacking gather and then the range sort of their span
+    (not a 32-bit LSD sort).  Exact against the oracle."""
+    import os
+    import pylibsort
+    prev = pylibsort.setDigitBits(4)
+    old = os.environ.get("LIBSORT_HYB_RESERVE")
+    if reserve == "nomem":
+        os.environ["LIBSORT_HYB_RESERVE"] = "nomem"
+    try:
+        x = oracle_mod.pcg((1 << 24) + 77, first=11)
+        outs, (nrsv, nseg) = _timed_names(D, lambda: _run(D, x, 2, COPY), "rsvsample", "segcopy")
+        _check(oracle_mod, x, outs, 2, False)
+        if reserve == "on":
+            assert nrsv > 0, nrsv
+        else:
+            assert nrsv == 0 and nseg > 0, (nrsv, nseg)
+        assert pylibsort.lib().libsortDeviceErrors() == 0
+    finally:
+        if old is None:
+            os.environ.pop("LIBSORT_HYB_RESERVE", None)
+        else:
+            os.environ["LIBSORT_HYB_RESERVE"] = old
+        pylibsort.setDigitBits(prev)
+
+
 @pytest.mark.slow
 def test_shape8_2pow29(D):
     """configs[3]'s per-rank size in the 8-GPU shape (2^29 keys of the stream
@@ -377,3 +409,46 @@ print("OK")
     env = dict(os.environ, LIBSORT_DISTRIB_THREADS="1", LIBSORT_DISTRIB_PARTS=parts)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-4000:])
+
+
+@pytest.mark.parametrize("lsd", [False, True], ids=["rounds", "lsd"])
+def test_stage_trace(D, oracle_mod, capfd, lsd):
+    """libsortSetDistribTrace(1) (LIBSORT_DISTRIB_TRACE=1): the engine names
+    every stage on stderr -- the partition, the plan, each round's exchange
+    issue, its arrival and sort on every rank, the re-cut, the end -- so a
+    multi-GPU run that hangs shows where.  The traced sort
+    is still exact."""
+    import re
+    import pylibsort
+    L = pylibsort.lib()
+    prev = L.libsortSetDistribTrace(1)
+    try:
+        x = oracle_mod.pcg((1 << 21) + 5, first=3)
+        capfd.readouterr()
+        outs = _run(D, x, 4, COPY | (LSD if lsd else 0))
+        err = capfd.readouterr().err
+    finally:
+        L.libsortSetDistribTrace(prev)
+    _check(oracle_mod, x, outs, 4, lsd)
+    lines = [ln for ln in err.splitlines() if ln.startswith("libsort distrib [")]
+    text = "\n".join(lines)
+    assert re.search(r"sort u32: 4 ranks on 1 devices, exchanges by device/peer copies", text), text
+    assert "done: ok" in text, text
+    if lsd:
+        for step in range(4):
+            assert "lsd step %d: exchange issued" % step in text, text
+    else:
+        assert "partition (top digit, 24-bit planes, 1 part)" in text or "partition (top digit, 1 part)" in text, text
+        assert "plan: 4 rounds per rank" in text, text
+        for i in range(4):
+            assert "round %d: exchange issued" % i in text, text
+            for r in range(4):
+                assert re.search(r"round %d rank %d: arrived" % (i, r), text), text
+        assert "re-cut" in text, text
+    # stamps non-decreasing
+    ms = [float(re.match(r"libsort distrib \[\s*([0-9.]+) ms\]", ln).group(1)) for ln in lines]
+    assert ms == sorted(ms)
+    # tracing off: silent
+    capfd.readouterr()
+    _run(D, x, 4, COPY)
+    assert "libsort distrib [" not in capfd.readouterr().err

@@ -562,6 +562,47 @@ def _device_sorted_and_checksums(x, out):
     return ok, sums(x) == sums(out)
 
 
+@pytest.mark.parametrize("digit", [8, 4])
+@pytest.mark.parametrize("width", [8, 16])
+def test_partial_reference_size(dev, width, digit):
+    """The reference's own benchmark workload (localTest/benchmarks.cpp:38-51,
+    212-215 -> gpuPartialProfile(first 2^28 PCG keys, offset 0, width 16);
+    analysis/libsort8b.csv is the same call at width 8), through both forms:
+    the device-resident libsortSortKeysU32(..., d_boundaries) and the host
+    ABI gpuPartial on a pageable buffer.  Parity: sha256 of the data and of
+    the 2^width boundaries equal to the oracle's stable counting partition of
+    the same keys (tests/golden/big_golden.json "partial_u32", which
+    make_big_golden.py also checked against the exact emulation of the
+    reference's Step kernels and GetBoundaries)."""
+    import ctypes
+    import pylibsort
+    n = 1 << 28
+    g = _big_golden()["partial_u32"]["%d/0/%d" % (n, width)]
+    prev = pylibsort.setDigitBits(digit)
+    try:
+        x = dev.populate_u32(n)
+        b = torch.empty(1 << width, dtype=torch.int32, device="cuda")
+        out = dev.sort_keys_u32(x, offset=0, width=width, boundaries=b)
+        torch.cuda.synchronize()
+        assert pylibsort.lib().libsortDeviceErrors() == 0
+        assert _device_sha256(out, np.dtype(np.uint32)) == g["data"]
+        hb = _u32(b)
+        assert list(hb[:4]) == g["boundaries_head"] and list(hb[-4:]) == g["boundaries_tail"]
+        assert hashlib.sha256(hb.astype("<u4").tobytes()).hexdigest() == g["boundaries"]
+        del out
+        host = x.cpu().numpy().view(np.uint32).copy()
+        del x
+        bnd = (ctypes.c_uint32 * (1 << width))()
+        assert pylibsort.lib().gpuPartial(host.ctypes.data, ctypes.addressof(bnd), n, 0, width) == 1, \
+            pylibsort.last_error()
+        assert hashlib.sha256(host.astype("<u4").tobytes()).hexdigest() == g["data"]
+        assert hashlib.sha256(np.frombuffer(bnd, dtype=np.uint32).astype("<u4").tobytes()).hexdigest() == \
+            g["boundaries"]
+    finally:
+        pylibsort.setDigitBits(prev)
+        torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("bits", [8, 4])
 def test_config3_2pow30(dev, bits):
     # C3: 2^30 keys of the PCG stream (device skip-ahead), full sort on one GPU

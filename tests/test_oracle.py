@@ -144,3 +144,22 @@ def test_counting_sort_restatement_pinned(oracle_mod, golden):
     # 2^30 (configs[2]), 2^32 - 1 (the ABI maximum), 2^32 (configs[3]'s global input, round 5)
     assert set(big["sorted_u32"]) == {str(1 << 30), str((1 << 32) - 1), str(1 << 32)}
     assert set(big["c5_pairs"][str(1 << 28)]) == {"keys", "payloads"}
+
+
+def test_partial_reference_workload_golden(oracle_mod, golden):
+    """big_golden.json "partial_u32" (the reference's own benchmark call,
+    localTest/benchmarks.cpp:38-51,212-215: first 2^28 keys, offset 0) is
+    reproduced by the oracle at width 8 from the pinned input stream."""
+    import json
+    import pathlib
+    g, _ = golden
+    n = 1 << 28
+    x = oracle_mod.pcg(n)
+    assert sha16(x) == g["sha256_prefix"][str(n)]["input"]
+    big = json.loads((pathlib.Path(__file__).resolve().parent / "golden" / "big_golden.json").read_text())
+    assert set(big["partial_u32"]) == {"%d/0/8" % n, "%d/0/16" % n}
+    d, b = oracle_mod.partial_u32(x, 0, 8)
+    want = big["partial_u32"]["%d/0/8" % n]
+    assert hashlib.sha256(d.astype("<u4").tobytes()).hexdigest() == want["data"]
+    assert hashlib.sha256(b.astype("<u4").tobytes()).hexdigest() == want["boundaries"]
+    assert b[:4].tolist() == want["boundaries_head"]
