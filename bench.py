@@ -14,22 +14,22 @@ c2 (default; the bench line): configs[1] = "256M uint32, 4-bit digits,
     N>1 = configs[3] ("2^32 uint32 sharded 8xMI355X"): 2^29 keys per GPU
     (2^32 at N=8); rank r holds keys [r*2^29, (r+1)*2^29) of the same stream
     (weak scaling); one step = one distributed sort ending with rank r holding
-    keys [r*S, (r+1)*S) of the sorted array.  Engine (--engine auto): at 4
-    and 8 GPUs the C engine -- rank 0 drives every GPU through the C ABI
-    (libsortDistribSortU32: top-digit partition, K = 4 RCCL point-to-point
-    rounds overlapped with the round sorts), its first step verified before
-    timing; at 2 GPUs the torch engine -- one process per GPU
-    (pylibsort.distrib, schedule "msdz": the same rounds sorted before
-    sending and exchanged gap-coded, since one xGMI link carries half of
-    every shard).  `python bench.py --gpus N` with no launcher starts its N ranks
+    keys [r*S, (r+1)*S) of the sorted array.  Engine (--engine auto): the C
+    engine at every N -- rank 0 drives every GPU through the C ABI
+    (libsortDistribSortU32, what C and Go callers bind: top-digit partition,
+    K = 4 RCCL point-to-point rounds overlapped with the round sorts; at 2
+    GPUs its gap-coded rounds, LIBSORT_DISTRIB_CODED: the same rounds sorted
+    by the sender and exchanged gap-coded, since one xGMI link carries half
+    of every shard), its first step verified (and stage-traced) before
+    timing; --engine torch = one process per GPU (pylibsort.distrib, the
+    same schedules over torch.distributed).  `python bench.py --gpus N` with no launcher starts its N ranks
     itself: torch.distributed.run as a CHILD process (no exec), rank 0's JSON
     line relayed, non-zero exit if any rank fails.
 c3: configs[2], 2^30 keys, 8-bit digits, one GPU.
 c5: configs[4], stable (u64 key, u32 payload) sort, 2^28 pairs per GPU (2^31
     on 8 GPUs); key = (draw 2i << 32) | draw 2i+1 of the stream, payload = the
     global index; N>1 runs the C pair engine (libsortDistribSortPairsU64U32)
-    at 4 and 8 GPUs and pylibsort.distrib.distrib_sort_pairs at 2 (the same
-    engine choice as c2).
+    (the same engine choice as c2).
 
 Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement").
 """
@@ -46,15 +46,16 @@ for p in (str(ROOT), str(ROOT / "gpu-radix-sort_amd")):
         sys.path.insert(0, p)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-# N>1 engine when --engine auto.  N >= 4: the C engine,
-# the faster of the two on the one-GPU schedule measurement at 2^29 keys per
-# rank (profiles/r03w_msd_schedule_2pow29_shape8.txt: 6.56 vs 6.71 ms in the
-# 8-GPU per-rank shape; profiles/r04*_msd_schedule_* for this round).  N = 2:
-# the torch engine, whose "msdz" schedule sends the rounds gap-coded (~9.5 of
-# 32 bits per key) -- two GPUs share ONE xGMI link, so the link, not the GPU
-# work, bounds that step, and only the torch engine has the coded exchange.
+# N>1 engine when --engine auto: the C engine at every
+# world size (the engine Go/C callers bind is the one
+# measured).  It was the faster of the two on the one-GPU schedule
+# measurement at 2^29 keys per rank (profiles/r03w_msd_schedule_2pow29_shape8.txt:
+# 6.56 vs 6.71 ms in the 8-GPU per-rank shape); at N = 2 it runs the
+# gap-coded rounds (~9.5 of 32 bits per key on the wire) that were the torch
+# engine's reason to exist there -- two GPUs share ONE xGMI link, so the link,
+# not the GPU work, bounds that step.
 def default_engine(world):
-    return "torch" if world == 2 else "cabi"
+    return "cabi"
 PASS_KERNELS = "tilepass,onesweep,downsweep"  # the roofline kernel candidates (timed-region events)
 EVENT_STRIDE = 5  # N=1 timed region: events around every 5th pass launch (libsortTimingSample)
 
@@ -68,13 +69,12 @@ def parse():
     ap.add_argument("--keys-log2", type=int, default=None, help="keys (pairs) per GPU = 2^k")
     ap.add_argument("--digit-bits", type=int, default=None, help="configs[1] names 4-bit digits")
     ap.add_argument("--schedule", default="auto", choices=["auto", "msd", "msdz", "lsd"],
-                    help="auto: msdz (delta-coded exchange) at 2 GPUs, msd otherwise")
+                    help="auto: msdz (gap-coded exchange) at 2 GPUs, msd otherwise")
     ap.add_argument("--rounds", type=int, default=4, help="msd exchange rounds (pylibsort.distrib.ROUNDS)")
     ap.add_argument("--engine", default="auto", choices=["auto", "torch", "cabi"],
                     help="N>1: torch = one process per GPU (pylibsort.distrib over torch.distributed); cabi = rank "
                          "0 drives every GPU through the C ABI (libsortDistribSortU32 / ...PairsU64U32, the "
-                         "single-process RCCL engine C and Go callers bind); auto = torch at 2 GPUs (the delta-coded "
-                         "msdz exchange), cabi otherwise")
+                         "single-process RCCL engine C and Go callers bind; gap-coded rounds at 2 GPUs); auto = cabi")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log2", type=int, default=28,
                     help="keys of the providedCpu baseline sample (BASELINE.md section 3: 2^28)")
@@ -144,10 +144,24 @@ def launch_probe(mode):
     dist.destroy_process_group()
 
 
+def stage(rank, world, what):
+    """One stderr line per bench phase at N > 1 (the driver's record keeps the
+    stderr tail: a run that hangs names its phase; with the C engine's own
+    stage trace on for its first step, libsortSetDistribTrace)."""
+    if world > 1:
+        sys.stderr.write("bench.py [rank %d, %.1f s]: %s\n" % (rank, time.perf_counter() - _T0, what))
+        sys.stderr.flush()
+
+
+_T0 = time.perf_counter()
+
+
 def main():
     args = parse()
     if args.algo:
         os.environ["LIBSORT_ALGO"] = args.algo
+    if args.schedule == "msd" and args.gpus == 2:
+        os.environ["LIBSORT_DISTRIB_CODED"] = "0"  # (the C engine's default at 2 GPUs is the coded rounds)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -222,13 +236,17 @@ def main():
             for dv in sorted(set(devs)):
                 torch.cuda.synchronize(dv)
 
+    # C engine flags: the schedule asked for (auto: the engine's own choice --
+    # gap-coded rounds at 2 GPUs, top-digit rounds otherwise)
+    cabi_flags = {"msdz": D.LIBSORT_DISTRIB_CODED, "lsd": D.LIBSORT_DISTRIB_LSD}.get(args.schedule, 0)
+
     def step():
         if cabi:
             if rank != 0:
                 return None
             if pairs:
                 return D.distrib_sort_pairs_u64_u32(shards, vshards)
-            return D.distrib_sort_u32(shards)
+            return D.distrib_sort_u32(shards, cabi_flags)
         if pairs:
             if world == 1:
                 return D.sort_pairs_u64_u32(keys, vals, out_keys=out, out_vals=outv, tmp_keys=tmp, tmp_vals=tmpv)
@@ -251,10 +269,15 @@ def main():
         # node), every rank switches to the torch engine (identical decision
         # via all_reduce)
         failed = 0
+        stage(rank, world, "C-ABI engine: first step (verified; stage trace on)")
         if rank == 0:
             try:
-                first = step()
-                torch.cuda.synchronize()
+                prev_trace = pylibsort.lib().libsortSetDistribTrace(1)
+                try:
+                    first = step()
+                    torch.cuda.synchronize()
+                finally:
+                    pylibsort.lib().libsortSetDistribTrace(prev_trace)
                 if os.environ.get("BENCH_CABI_FAULT") == "1":  # rehearsal of the fallback (tests only)
                     (first[0] if pairs else first)[0][:1] = 0 if pairs else -1
                 if not args.no_verify and not verify_cabi(torch, shards, first, vshards if pairs else None):
@@ -271,10 +294,12 @@ def main():
             engine = "torch"
             if rank == 0:
                 sys.stderr.write("bench.py: %s\n" % engine_note)
+    stage(rank, world, "warmup (%d steps, %s engine)" % (args.warmup, engine))
     for _ in range(args.warmup):
         res = step()
     torch.cuda.synchronize()
     barrier()
+    stage(rank, world, "timed steps (%d)" % args.steps)
 
     # events in the timed region only around the pass kernel the roofline is
     # priced on (every kernel's events cost ~2.5% of the 2^28 sort); the full
@@ -313,6 +338,7 @@ def main():
                 got[name] = {"launches": launches, "avg_us": 1e3 * ms / launches, "keys_per_launch": kk / launches}
         return got
 
+    stage(rank, world, "timed steps done: %.3f s; per-kernel event steps" % elapsed)
     timed_pass = query(PASS_KERNELS.split(","))
     D.timing_reset()
     D.timing_sample(1)
@@ -330,6 +356,7 @@ def main():
     kern.update({name: dict(v, **{"from": "the timed steps"}) for name, v in timed_pass.items()})
 
     # verification outside the timed region: sorted + same multiset (checksums)
+    stage(rank, world, "verification")
     verified = None
     if not args.no_verify and cabi:
         verified = verify_cabi(torch, shards, res, vshards if pairs else None) if rank == 0 else None
@@ -340,6 +367,7 @@ def main():
     # part; max over ranks), reported beside the 4-bit line, never as `value`
     variant8 = None
     if world > 1 and not args.no_variants and not pairs:
+        stage(rank, world, "8-bit digit variant")
         prev = pylibsort.setDigitBits(8)
         for _ in range(2):
             step()
@@ -440,8 +468,8 @@ def main():
         if world > 1:
             sname = args.schedule
             if sname == "auto":
-                sname = "msdz" if world == 2 else "msd"
-            if pairs or cabi:
+                sname = "msdz" if world == 2 and not rehearsal else "msd"
+            if pairs:
                 sname = "msd"
             sched = (", %s schedule (top-digit rounds)%s, %d rounds, over %d GPUs (RCCL point-to-point)"
                      % (sname, " with delta-coded exchange" if sname == "msdz" else "", args.rounds, world)

@@ -204,11 +204,13 @@ struct RankState {
   DevState* d = nullptr;
   DBuf bounds, part, pv, recv, rv, outb, ov, alt;  // pv / rv / ov: pair payloads
   DBuf mm;                                          // smallest and largest key (range partition)
+  DBuf csend, crecv, mg, mtmp;                      // coded rounds: coded pieces out / in, largest gaps, merge levels
   DBuf hin, hout;  // staging of the host-pointer entry point
   uint64_t pn = 0;  // keys in `part` (24-bit planes: the 8-bit plane starts at byte 2 * pn)
   hipEvent_t ev_part = nullptr, ev_bounds = nullptr, ev_done = nullptr;
   hipEvent_t ev_part0 = nullptr;  // the first partition part written (two parts: partition_top)
   hipEvent_t ev_x[kMaxRounds] = {};
+  hipEvent_t ev_c[kMaxRounds] = {};  // coded rounds: round i sorted and coded (largest gaps on the host)
 };
 
 struct Ctx {
@@ -218,6 +220,7 @@ struct Ctx {
   std::vector<ncclComm_t> comms;               // RCCL communicator of each rank (distinct devices only)
   uint32_t* h_bounds = nullptr;                // pinned: R x kMaxParts x 256 bucket starts
   uint64_t* h_mm = nullptr;                    // pinned: R x (min, max) keys
+  uint32_t* h_mg = nullptr;                    // pinned: R x (R * kMaxRounds) largest gaps (coded rounds)
   bool distinct = false;
   std::vector<uint64_t> sent;                  // bytes each rank sent to others in the last sort
 
@@ -225,12 +228,15 @@ struct Ctx {
     for (ncclComm_t c : comms)
       if (c && g_rccl.loaded) (void)g_rccl.commDestroy(c);
     for (auto& r : ranks) {
-      for (DBuf* b : {&r.bounds, &r.part, &r.pv, &r.recv, &r.rv, &r.outb, &r.ov, &r.alt, &r.mm, &r.hin, &r.hout})
+      for (DBuf* b : {&r.bounds, &r.part, &r.pv, &r.recv, &r.rv, &r.outb, &r.ov, &r.alt, &r.mm, &r.hin, &r.hout,
+                      &r.csend, &r.crecv, &r.mg, &r.mtmp})
         b->release();
       (void)hipSetDevice(r.dev);
       for (hipEvent_t e : {r.ev_part, r.ev_bounds, r.ev_done, r.ev_part0})
         if (e) (void)hipEventDestroy(e);
       for (hipEvent_t e : r.ev_x)
+        if (e) (void)hipEventDestroy(e);
+      for (hipEvent_t e : r.ev_c)
         if (e) (void)hipEventDestroy(e);
     }
     for (auto& u : uniq) {
@@ -245,6 +251,7 @@ struct Ctx {
     }
     if (h_bounds) (void)hipHostFree(h_bounds);
     if (h_mm) (void)hipHostFree(h_mm);
+    if (h_mg) (void)hipHostFree(h_mg);
   }
 
   bool init(const std::vector<int>& d) {
@@ -287,12 +294,16 @@ struct Ctx {
         if (!ok_hip(hipEventCreateWithFlags(e, hipEventDisableTiming), "hipEventCreate")) return false;
       for (hipEvent_t& e : s.ev_x)
         if (!ok_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate")) return false;
+      for (hipEvent_t& e : s.ev_c)
+        if (!ok_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate")) return false;
+      if (!s.mg.ensure(s.dev, (size_t)R * kMaxRounds * sizeof(uint32_t))) return false;
       if (!s.bounds.ensure(s.dev, kMaxParts * dplan::kTopDigits * 4) || !s.mm.ensure(s.dev, 2 * sizeof(uint64_t)))
         return false;
     }
     return ok_hip(hipHostMalloc(&h_bounds, (size_t)R * kMaxParts * dplan::kTopDigits * sizeof(uint32_t), 0),
                   "hipHostMalloc") &&
-           ok_hip(hipHostMalloc(&h_mm, (size_t)R * 2 * sizeof(uint64_t), 0), "hipHostMalloc");
+           ok_hip(hipHostMalloc(&h_mm, (size_t)R * 2 * sizeof(uint64_t), 0), "hipHostMalloc") &&
+           ok_hip(hipHostMalloc(&h_mg, (size_t)R * R * kMaxRounds * sizeof(uint32_t), 0), "hipHostMalloc");
   }
 
   bool ensure_comms() {
@@ -874,7 +885,303 @@ bool run_digit_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<K*>& 
          (!pairs || move_pieces(c, cut, vsrc, vdst, 4, use_rccl, self_rccl, false));
 }
 
-// Partition parts per rank: two when there is an RCCL exchange between
+// ---------------------------------------------------------------------------
+// Gap-coded rounds ("msdz"; the torch engine's pylibsort.distrib.sort_msdz,
+// one engine for every world size).  The same partition
+// and plan as run_digit_rounds, but the SENDER sorts: rank s sorts each of its
+// outgoing (round i, destination d) pieces from its partition's digit pieces
+// (sort_pieces_u32: the pieces are disjoint key ranges), codes every remote
+// piece as 64-key groups of gaps (delta_pack_u32: a base word + 2w words per
+// group, w = the bits of the piece's largest gap -- ~9.5 of 32 bits per key
+// for uniform keys at 2^29 per rank), the host reads round i's largest gaps
+// (exact coded sizes on both sides), the coded pieces cross the links, and
+// the receiver decodes them (delta_unpack_u32) and merges its R sorted runs
+// (merge_u32, pairwise levels) into its slice of the output; then the equal
+// re-cut.  Fewer bytes on the wire (~0.3x), more GPU work (a merge level per
+// doubling of R) -- for link-bound world sizes (2 GPUs: one xGMI link
+// carries half of every shard).  Keys only, 32-bit partition (no planes).
+// Per device one host thread issues its ranks' sender sorts of every round up
+// front (the sorts' small host read-backs hold only that device), then each
+// round's decode + merge once the exchange of that round is issued.
+// ---------------------------------------------------------------------------
+bool coded_rounds_on(int R, unsigned flags, bool rccl_between_gpus) {
+  static const int env = [] {
+    const char* e = getenv("LIBSORT_DISTRIB_CODED");
+    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' + 1 : 0;  // 0: auto, 1: off, 2: on
+  }();
+  if (flags & kDistribCoded) return true;
+  if (env) return env == 2;
+  return R == 2 && rccl_between_gpus;
+}
+
+bool run_coded_rounds(Ctx& c, const dplan::DigitPlan& p, const std::vector<std::vector<uint64_t>>& C,
+                      const std::vector<uint32_t*>& out, bool use_rccl, bool self_rccl, int bits,
+                      const PartDigit& pd) {
+  const int R = (int)c.ranks.size(), K_ = p.K;
+  const bool self_coded = use_rccl && self_rccl;
+  auto remote = [&](int s, int d) { return s != d || self_coded; };
+  // the coded layout (distrib_plan.h: digit starts, piece sizes M[s][i * R +
+  // d], worst-case coded regions on both sides)
+  const dplan::CodedPlan cp = dplan::coded_plan(p, C, self_coded);
+  const auto& start = cp.start;
+  const auto& M = cp.M;
+  const auto& coff = cp.coff;
+  const auto& cr_off = cp.cr_off;
+  const auto& rcap = cp.rcap;
+  std::map<DevState*, uint64_t> piece_max;
+  for (int s = 0; s < R; ++s)
+    for (int j = 0; j < R * K_; ++j) piece_max[c.ranks[s].d] = std::max(piece_max[c.ranks[s].d], M[s][j]);
+  for (int r = 0; r < R; ++r) {
+    RankState& s = c.ranks[r];
+    const uint64_t m = std::max<uint64_t>(p.n_recv[r], 1);
+    if (!s.alt.ensure(s.dev, std::max<uint64_t>(start[r][dplan::kTopDigits], 1) * 4) ||
+        !s.csend.ensure(s.dev, std::max<uint64_t>(coff[r][(size_t)R * K_], 1) * 4) ||
+        !s.crecv.ensure(s.dev, std::max<uint64_t>(rcap[r], 1) * 4) || !s.recv.ensure(s.dev, m * 4) ||
+        !s.outb.ensure(s.dev, m * 4) || (R > 2 && !s.mtmp.ensure(s.dev, m * 4)))
+      return false;
+  }
+  for (auto& kv : piece_max)
+    if (!kv.first->tmp.ensure(kv.first->dev, std::max<uint64_t>(kv.second, 1) * 4)) return false;
+  const dplan::Placement pl = dplan::place_rounds(p.roff, p.n_recv, K_);
+  // the destination of rank r's round i (its output shard, or outb)
+  auto round_dst = [&](int r, int i) -> uint32_t* {
+    const size_t q = (size_t)r * K_ + i;
+    return pl.direct[q] ? out[r] + pl.out_off[q] : c.ranks[r].outb.u32() + p.roff[(size_t)r * (K_ + 1) + i];
+  };
+  // a round whose only keys are the receiver's own piece: sorted straight
+  // into its destination (no copy)
+  auto only_self = [&](int r, int i) { return cp.self_only[(size_t)r * K_ + i] != 0; };
+  uint32_t* const hmg = c.h_mg;
+  const size_t mg_stride = (size_t)R * kMaxRounds;
+  // sender side of rank r: sort, then code, every outgoing piece of round i
+  auto send_round = [&](int r, int i) -> bool {
+    RankState& s = c.ranks[r];
+    DevState& d = *s.d;
+    for (int dd = 0; dd < R; ++dd) {
+      const size_t j = (size_t)i * R + dd;
+      const uint64_t m = M[r][j];
+      if (!m) continue;
+      const int a = p.lo[j], b = p.hi[j];
+      std::vector<uint64_t> offs, lens;
+      std::vector<uint32_t> segs;
+      for (int g = a; g < b; ++g) {
+        offs.push_back(start[r][g] - start[r][a]);
+        lens.push_back(C[r][g]);
+        segs.push_back((uint32_t)(g - a));
+      }
+      uint32_t* const srt = (dd == r && only_self(r, i)) ? round_dst(r, i) : s.alt.u32() + start[r][a];
+      if (!ok_hip(sort_pieces_u32(*d.ws, s.part.u32() + start[r][a], srt, d.tmp.u32(), m, offs.data(), lens.data(),
+                                  segs.data(), offs.size(), (uint32_t)(b - a), pd.shift, bits, d.st,
+                                  (uint32_t)pd.bias),
+                  "sender round sort"))
+        return false;
+      if (remote(r, dd) &&
+          (!ok_hip(delta_maxgap_u32(srt, m, s.mg.u32() + j, d.st), "largest gap") ||
+           !ok_hip(delta_pack_u32(srt, m, s.mg.u32() + j, s.csend.u32() + coff[r][j], d.st), "gap coding")))
+        return false;
+    }
+    return ok_hip(hipMemcpyAsync(hmg + (size_t)r * mg_stride + (size_t)i * R, s.mg.u32() + (size_t)i * R,
+                                 (size_t)R * sizeof(uint32_t), hipMemcpyDeviceToHost, d.st),
+                  "D2H largest gaps") &&
+           ok_hip(hipEventRecord(s.ev_c[i], d.st), "hipEventRecord");
+  };
+  // receiver side of rank r, round i (after its exchange was issued): decode
+  // the coded runs, merge them with the own piece into the round's destination
+  auto merge_round = [&](int r, int i) -> bool {
+    RankState& s = c.ranks[r];
+    DevState& d = *s.d;
+    if (!ok_hip(hipStreamWaitEvent(d.st, s.ev_x[i], 0), "wait")) return false;
+    if (tracing()) {
+      if (!ok_hip(hipEventSynchronize(s.ev_x[i]), "hipEventSynchronize")) return false;
+      trace("round %d rank %d: arrived", i, r);
+    }
+    if (only_self(r, i)) return true;  // (sorted in place by the sender side)
+    const uint64_t r0 = p.roff[(size_t)r * (K_ + 1) + i], r1 = p.roff[(size_t)r * (K_ + 1) + i + 1];
+    if (r1 == r0) return true;
+    std::vector<std::pair<const uint32_t*, uint64_t>> runs;
+    uint64_t at = r0;
+    for (int src = 0; src < R; ++src) {
+      const size_t j = (size_t)i * R + r;
+      const uint64_t m = M[src][j];
+      if (!m) continue;
+      if (!remote(src, r)) {
+        runs.push_back({s.alt.u32() + start[r][p.lo[j]], m});
+        continue;
+      }
+      const uint32_t w = dplan::gap_bits(hmg[(size_t)src * mg_stride + j]);
+      if (!ok_hip(delta_unpack_u32(s.crecv.u32() + cr_off[r][(size_t)i * R + src], m, w, s.recv.u32() + at, d.st),
+                  "gap decoding"))
+        return false;
+      runs.push_back({s.recv.u32() + at, m});
+      at += m;
+    }
+    uint32_t* const dst = round_dst(r, i);
+    // pairwise merge levels, ping-pong between mtmp and recv (the runs of a
+    // level are consumed by the time the next level writes them)
+    int level = 0;
+    while (runs.size() > 2) {
+      uint32_t* const buf = (level & 1) ? s.recv.u32() : s.mtmp.u32();
+      std::vector<std::pair<const uint32_t*, uint64_t>> nxt;
+      uint64_t o = r0;
+      for (size_t k = 0; k + 1 < runs.size(); k += 2) {
+        if (!ok_hip(merge_u32(runs[k].first, runs[k].second, runs[k + 1].first, runs[k + 1].second, buf + o, d.st),
+                    "merge"))
+          return false;
+        nxt.push_back({buf + o, runs[k].second + runs[k + 1].second});
+        o += runs[k].second + runs[k + 1].second;
+      }
+      if (runs.size() & 1) nxt.push_back(runs.back());
+      runs.swap(nxt);
+      ++level;
+    }
+    hipError_t e = runs.size() == 2 ? merge_u32(runs[0].first, runs[0].second, runs[1].first, runs[1].second, dst, d.st)
+                                    : hipMemcpyAsync(dst, runs[0].first, runs[0].second * 4, hipMemcpyDeviceToDevice,
+                                                     d.st);
+    if (!ok_hip(e, "final merge")) return false;
+    if (tracing()) {
+      if (!ok_hip(hipStreamSynchronize(d.st), "hipStreamSynchronize")) return false;
+      trace("round %d rank %d: decoded and merged (%zu runs)", i, r, runs.size());
+    }
+    return true;
+  };
+  // the exchange of round i: every sender's coded pieces, exact sizes from
+  // the largest gaps the host read back (counted in c.sent: the coded bytes)
+  auto exchange_round = [&](int i) -> bool {
+    for (int r = 0; r < R; ++r)
+      if (!ok_hip(hipEventSynchronize(c.ranks[r].ev_c[i]), "hipEventSynchronize")) return false;
+    trace("round %d: sorted and coded on every rank", i);
+    const std::vector<dplan::Piece> ps = dplan::coded_round_pieces(cp, i, hmg, mg_stride, self_coded);
+    // every communication stream after every rank's round-i coding
+    for (auto& u : c.uniq) {
+      if (!ok_hip(hipSetDevice(u->dev), "hipSetDevice")) return false;
+      for (auto& rk : c.ranks)
+        if (!ok_hip(hipStreamWaitEvent(u->cs, rk.ev_c[i], 0), "hipStreamWaitEvent")) return false;
+    }
+    std::vector<const void*> src(R);
+    std::vector<void*> dst(R);
+    for (int r = 0; r < R; ++r) {
+      src[r] = c.ranks[r].csend.p;
+      dst[r] = c.ranks[r].crecv.p;
+    }
+    if (!move_pieces(c, ps, src, dst, 4, use_rccl, self_rccl)) return false;
+    for (int r = 0; r < R; ++r) {
+      RankState& s = c.ranks[r];
+      if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !ok_hip(hipEventRecord(s.ev_x[i], s.d->cs), "record"))
+        return false;
+    }
+    trace("round %d: coded exchange issued (%zu pieces)", i, ps.size());
+    return true;
+  };
+  // Several devices (or LIBSORT_DISTRIB_THREADS=1): one host thread per
+  // device -- its ranks' sender sorts of every round, then round by round
+  // (once issued) their decode + merge; this thread issues the exchanges.
+  static const bool force_threads = [] {
+    const char* e = getenv("LIBSORT_DISTRIB_THREADS");
+    return e && e[0] == '1';
+  }();
+  const bool threaded = c.uniq.size() > 1 || force_threads;
+  std::mutex mu;
+  std::condition_variable cv;
+  int issued = 0;
+  bool stop = false;
+  std::vector<std::string> err(c.uniq.size());
+  std::vector<char> good(c.uniq.size(), 1);
+  // rounds whose sender sorts each device thread has issued (the issue loop
+  // may wait on their events only after that: an event not recorded yet
+  // would not hold it)
+  std::vector<int> coded(c.uniq.size(), 0);
+  auto device_work = [&](size_t u, bool wait_issue) -> bool {
+    DevState& d = *c.uniq[u];
+    if (!ok_hip(hipSetDevice(d.dev), "hipSetDevice")) return false;
+    for (int i = 0; i < K_; ++i) {
+      for (int r = 0; r < R; ++r)
+        if (c.ranks[r].d == &d && !send_round(r, i)) return false;
+      std::lock_guard<std::mutex> lk(mu);
+      coded[u] = i + 1;
+      cv.notify_all();
+    }
+    for (int i = 0; i < K_; ++i) {
+      if (wait_issue) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return issued > i || stop; });
+        if (issued <= i) return true;  // the exchange failed (its error is reported)
+      }
+      for (int r = 0; r < R; ++r)
+        if (c.ranks[r].d == &d && !merge_round(r, i)) return false;
+    }
+    return true;
+  };
+  bool issue_ok = true;
+  if (threaded) {
+    std::vector<std::thread> th;
+    for (size_t u = 0; u < c.uniq.size(); ++u)
+      th.emplace_back([&, u] {
+        if (!device_work(u, true)) {
+          good[u] = 0;
+          err[u] = last_error();
+          // (a device that failed its sorts never records their events:
+          // stop the issue loop rather than wait for them)
+          std::lock_guard<std::mutex> lk(mu);
+          stop = true;
+          cv.notify_all();
+        }
+      });
+    // (the issue loop waits for events the device threads record: a failed
+    // thread sets stop, checked between rounds)
+    for (int i = 0; issue_ok && i < K_; ++i) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return stop || std::all_of(coded.begin(), coded.end(), [&](int k) { return k > i; }); });
+        if (stop) break;
+      }
+      issue_ok = exchange_round(i);
+      std::lock_guard<std::mutex> lk(mu);
+      if (issue_ok) issued = i + 1;
+      cv.notify_all();
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+      cv.notify_all();
+    }
+    for (auto& t : th) t.join();
+    for (size_t u = 0; u < good.size(); ++u)
+      if (!good[u]) {
+        set_error(err[u]);
+        return false;
+      }
+    if (!issue_ok) return false;
+  } else {
+    // one device: every sender sort, then round by round exchange + merges
+    DevState& d = *c.uniq[0];
+    if (!ok_hip(hipSetDevice(d.dev), "hipSetDevice")) return false;
+    for (int i = 0; i < K_; ++i)
+      for (int r = 0; r < R; ++r)
+        if (!send_round(r, i)) return false;
+    for (int i = 0; i < K_; ++i) {
+      if (!exchange_round(i) || !ok_hip(hipSetDevice(d.dev), "hipSetDevice")) return false;
+      for (int r = 0; r < R; ++r)
+        if (!merge_round(r, i)) return false;
+    }
+  }
+  // the equal re-cut (as run_digit_rounds)
+  for (int r = 0; r < R; ++r) {
+    RankState& s = c.ranks[r];
+    if (!ok_hip(hipSetDevice(s.dev), "hipSetDevice") || !ok_hip(hipEventRecord(s.ev_done, s.d->st), "record"))
+      return false;
+  }
+  if (!comm_waits(c, &RankState::ev_done)) return false;
+  trace("coded rounds merged; re-cut of %zu pieces", pl.moves.size());
+  std::vector<const void*> src(R);
+  std::vector<void*> dst(R);
+  for (int r = 0; r < R; ++r) {
+    src[r] = c.ranks[r].outb.p;
+    dst[r] = out[r];
+  }
+  return move_pieces(c, pl.moves, src, dst, 4, use_rccl, self_rccl, false);
+}
+
+
 // distinct GPUs to overlap with the second part's partition; one otherwise
 // (ranks sharing a GPU exchange by device copies, which two parts only double:
 // +32 us of kernels per rank, 6.9 -> 7.7 ms in DESIGN.md 3d).
@@ -942,8 +1249,11 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
     const char* e = getenv("LIBSORT_DISTRIB_WIRE24");
     return !(e && e[0] == '0');
   }();
-  const bool planar = wire24_env && !(flags & kDistribWire32) && bits == 4;
-  const int H = parts_for(R, c.distinct && !copy);
+  // gap-coded rounds (kDistribCoded; by default at two ranks on two GPUs):
+  // one partition part, 32-bit keys in the partition (the wire is coded)
+  const bool coded = coded_rounds_on(R, flags, c.distinct && !copy);
+  const bool planar = !coded && wire24_env && !(flags & kDistribWire32) && bits == 4;
+  const int H = coded ? 1 : parts_for(R, c.distinct && !copy);
   std::vector<std::vector<uint64_t>> Cp;
   std::vector<uint64_t> first;
   if (!partition_top<uint32_t>(c, in, nullptr, n, C, pd, planar, H, Cp, first)) return hold.finish(false);
@@ -967,6 +1277,11 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
       trace("plan: LSD rounds");
       return hold.finish(run_lsd(c, in, n, out, S, bits, !copy, self_rccl));
     }
+  }
+  if (coded) {
+    trace("plan: gap-coded rounds");
+    return hold.finish(run_coded_rounds(c, dplan::digit_plan_parts(Cp, 1, first, lut.data(), K), Cp, out, !copy,
+                                        self_rccl, bits, pd));
   }
   return hold.finish(run_digit_rounds<uint32_t>(c, dplan::digit_plan_parts(Cp, H, first, lut.data(), K), out, nullptr,
                                                 !copy, self_rccl, bits, pd, planar && !pd.range, H));
@@ -1084,6 +1399,60 @@ bool distrib_last_bytes(uint64_t* per_rank, int nranks) {
 }
 
 int set_distrib_trace(int on) { return g_trace.exchange(on ? 1 : 0); }
+
+namespace {
+// one wave spinning on the constant-rate wall clock (s_memrealtime)
+__global__ void k_spin(long long ticks, uint32_t* never) {
+  const long long t0 = wall_clock64();
+  uint32_t n = 0;
+  while (wall_clock64() - t0 < ticks) ++n;
+  if (n == 0xffffffffu && never) never[0] = n;  // (keeps the loop; never true)
+}
+}  // namespace
+
+// do the engine's compute stream `st` and communication
+// stream `cs` of devices[0] execute concurrently, in this process's exact
+// stream set-up (torch's streams, the workspace streams, RCCL's)?  With
+// GPU_MAX_HW_QUEUES = 4, HIP maps later streams onto shared hardware queues,
+// and two streams on one in-order queue serialise -- an RCCL kernel waiting
+// for its peer on cs would then hold the round sorts on st.  A spinning
+// one-wave kernel on each stream; ms[0..3] = start / end on st, start / end
+// on cs, in ms after a common event on st.
+bool distrib_overlap_probe(const int* devices, int R, uint32_t spin_us, double* ms) {
+  std::lock_guard<std::mutex> glk(g_dist_mu);
+  Ctx* c = ctx_for(devices, R);
+  if (!c) return false;
+  DevState& d = *c->uniq[0];
+  if (!ok_hip(hipSetDevice(d.dev), "hipSetDevice")) return false;
+  int khz = 0;
+  if (!ok_hip(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, d.dev), "hipDeviceGetAttribute"))
+    return false;
+  const long long ticks = (long long)spin_us * khz / 1000;
+  hipEvent_t e[5] = {};
+  bool ok = true;
+  for (hipEvent_t& x : e) ok = ok && ok_hip(hipEventCreate(&x), "hipEventCreate");
+  uint32_t* never = static_cast<uint32_t*>(d.lut.p);
+  ok = ok && ok_hip(hipEventRecord(e[0], d.st), "record") && ok_hip(hipStreamWaitEvent(d.cs, e[0], 0), "wait") &&
+       ok_hip(hipEventRecord(e[1], d.st), "record");
+  if (ok) {
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, d.st, ticks, never);
+    ok = ok_hip(hipGetLastError(), "spin on st") && ok_hip(hipEventRecord(e[2], d.st), "record") &&
+         ok_hip(hipEventRecord(e[3], d.cs), "record");
+  }
+  if (ok) {
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, d.cs, ticks, never);
+    ok = ok_hip(hipGetLastError(), "spin on cs") && ok_hip(hipEventRecord(e[4], d.cs), "record");
+  }
+  ok = ok && ok_hip(hipStreamSynchronize(d.st), "sync") && ok_hip(hipStreamSynchronize(d.cs), "sync");
+  for (int i = 0; ok && i < 4; ++i) {
+    float t = 0.f;
+    ok = ok_hip(hipEventElapsedTime(&t, e[0], e[i + 1]), "hipEventElapsedTime");
+    ms[i] = t;
+  }
+  for (hipEvent_t x : e)
+    if (x) (void)hipEventDestroy(x);
+  return ok;
+}
 
 void distrib_release() {
   std::lock_guard<std::mutex> glk(g_dist_mu);

@@ -291,6 +291,84 @@ inline Placement place_rounds(const std::vector<uint64_t>& roff, const std::vect
 }
 
 // ---------------------------------------------------------------------------
+// gap-coded rounds ("msdz", distrib.cpp run_coded_rounds): the same digit
+// plan, but each sender sorts its (round, destination) pieces and sends them
+// as 64-key groups of gaps -- one base word, then 2w words of w-bit gaps (w =
+// the bits of the piece's largest gap; libsort.h libsortDeltaPackU32).
+// ---------------------------------------------------------------------------
+inline uint64_t delta_words(uint64_t n, uint32_t w) { return (n + 63) / 64 * (1 + 2 * (uint64_t)w); }
+inline uint32_t gap_bits(uint32_t maxgap) {
+  uint32_t b = 0;
+  while (b < 32 && (maxgap >> b)) ++b;
+  return b;
+}
+
+struct CodedPlan {
+  int R = 0, K = 0;
+  std::vector<std::vector<uint64_t>> start;   // [R][257]: digit g's start in rank s's partition
+  std::vector<std::vector<uint64_t>> M;       // [R][R*K]: keys rank s sends in group i * R + d
+  std::vector<std::vector<uint64_t>> coff;    // [R][R*K+1]: coded send regions (32-bit gaps: worst case)
+  std::vector<std::vector<uint64_t>> cr_off;  // [R][R*K]: receiver d's coded region of (round i, source s) at i * R + s
+  std::vector<uint64_t> rcap;                 // [R]: coded receive words (worst case)
+  std::vector<char> self_only;                // [R*K] (rank r, round i) at r * K + i: only r's own piece, uncoded
+};
+
+// self_coded: a rank's own piece is coded and sent through the communicator
+// too (one-rank RCCL tests); otherwise it stays put, uncoded.  Every layout is
+// at worst-case (32-bit) widths, so no round depends on a later round's gaps.
+inline CodedPlan coded_plan(const DigitPlan& p, const std::vector<std::vector<uint64_t>>& C, bool self_coded) {
+  CodedPlan c;
+  const int R = p.R, K = p.K;
+  c.R = R;
+  c.K = K;
+  auto remote = [&](int s, int d) { return s != d || self_coded; };
+  c.start.assign(R, std::vector<uint64_t>(kTopDigits + 1, 0));
+  for (int s = 0; s < R; ++s)
+    for (int g = 0; g < kTopDigits; ++g) c.start[s][g + 1] = c.start[s][g] + C[s][g];
+  c.M.assign(R, std::vector<uint64_t>((size_t)R * K, 0));
+  c.coff.assign(R, std::vector<uint64_t>((size_t)R * K + 1, 0));
+  for (int s = 0; s < R; ++s)
+    for (int j = 0; j < R * K; ++j) {
+      c.M[s][j] = c.start[s][p.hi[j]] - c.start[s][p.lo[j]];
+      c.coff[s][j + 1] = c.coff[s][j] + (remote(s, j % R) ? delta_words(c.M[s][j], 32) : 0);
+    }
+  c.cr_off.assign(R, std::vector<uint64_t>((size_t)R * K, 0));
+  c.rcap.assign(R, 0);
+  c.self_only.assign((size_t)R * K, 0);
+  for (int d = 0; d < R; ++d) {
+    uint64_t o = 0;
+    for (int i = 0; i < K; ++i) {
+      bool others = false;
+      for (int s = 0; s < R; ++s) {
+        const uint64_t m = c.M[s][(size_t)i * R + d];
+        c.cr_off[d][(size_t)i * R + s] = o;
+        if (remote(s, d)) o += delta_words(m, 32);
+        if (s != d && m) others = true;
+      }
+      c.self_only[(size_t)d * K + i] = !others && !remote(d, d);
+    }
+    c.rcap[d] = o;
+  }
+  return c;
+}
+
+// The coded exchange of round i: maxgap[s * stride + i * R + d] = the largest
+// gap of rank s's piece for d (read back after round i's coding).
+inline std::vector<Piece> coded_round_pieces(const CodedPlan& c, int i, const uint32_t* maxgap, size_t stride,
+                                             bool self_coded) {
+  std::vector<Piece> ps;
+  const int R = c.R;
+  for (int s = 0; s < R; ++s)
+    for (int d = 0; d < R; ++d) {
+      const size_t j = (size_t)i * R + d;
+      if ((s == d && !self_coded) || !c.M[s][j]) continue;
+      ps.push_back(Piece{s, d, c.coff[s][j], c.cr_off[d][(size_t)i * R + s],
+                         delta_words(c.M[s][j], gap_bits(maxgap[(size_t)s * stride + j]))});
+    }
+  return ps;
+}
+
+// ---------------------------------------------------------------------------
 // BSP LSD round ("lsd", the reference's semantics)
 // ---------------------------------------------------------------------------
 // C[s][b] = keys of rank s in bucket b after its local stable partition

@@ -1235,6 +1235,25 @@ LS_BOOL_ENTRY(libsortDistribLastBytes, int nranks, uint64_t* per_rank) {
 
 LIBSORT_EXPORT int libsortSetDistribTrace(int on) { return set_distrib_trace(on ? 1 : 0); }
 
+LS_BOOL_ENTRY(libsortDistribOverlapProbe, int nranks, const int* devices, uint32_t spin_us, double* ms) {
+  if (nranks < 1 || !devices || !ms || spin_us == 0 || spin_us > 10000000u) {
+    set_error("libsortDistribOverlapProbe: need nranks >= 1, devices, ms[4] and 0 < spin_us <= 10 s");
+    return 0;
+  }
+  int ndev = 0;
+  if (!hip_ok(hipGetDeviceCount(&ndev), "hipGetDeviceCount")) return 0;
+  for (int r = 0; r < nranks; ++r)
+    if (devices[r] < 0 || devices[r] >= ndev) {
+      set_error("libsortDistribOverlapProbe: device out of range");
+      return 0;
+    }
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  const bool ok = distrib_overlap_probe(devices, nranks, spin_us, ms);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return ok ? 1 : 0;
+}
+
 LS_BOOL_ENTRY(libsortDistribRangeDigit, uint64_t lo, uint64_t hi, uint32_t key_bits, uint64_t* bias,
               uint32_t* shift) {
   if (!bias || !shift || (key_bits != 32 && key_bits != 64)) {
@@ -1265,7 +1284,7 @@ LS_BOOL_ENTRY(libsortDistribSortU32, int nranks, const int* devices, const uint3
     set_error("libsortDistribSortU32: need nranks >= 1 and non-NULL tables");
     return 0;
   }
-  if (flags & ~(kDistribLsd | kDistribCopy | kDistribSelfRccl | kDistribWire32)) {
+  if (flags & ~(kDistribLsd | kDistribCopy | kDistribSelfRccl | kDistribWire32 | kDistribCoded)) {
     set_error("libsortDistribSortU32: unknown flags");
     return 0;
   }

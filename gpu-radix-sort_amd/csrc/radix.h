@@ -273,6 +273,7 @@ constexpr unsigned kDistribLsd = 1u;       // the reference's BSP LSD rounds ins
 constexpr unsigned kDistribCopy = 2u;      // exchanges as peer copies instead of RCCL
 constexpr unsigned kDistribSelfRccl = 4u;  // a rank's own pieces through RCCL too (tests)
 constexpr unsigned kDistribWire32 = 8u;    // 32-bit keys on the wire (default: 24-bit planes, top-digit rounds)
+constexpr unsigned kDistribCoded = 16u;    // gap-coded rounds: sender sorts, coded exchange, receiver merges
 // Rank r's shard d_in[r] (n_in[r] keys, on device devices[r]; devices may
 // repeat) -> d_out[r] = keys [r*S, (r+1)*S) of the sorted whole, S =
 // ceil(N/R); n_out[r] receives the count.  Synchronous.
@@ -282,6 +283,9 @@ constexpr unsigned kDistribWire32 = 8u;    // 32-bit keys on the wire (default: 
 bool distrib_last_bytes(uint64_t* per_rank, int nranks);
 // stage trace on stderr (libsortSetDistribTrace); returns the previous setting
 int set_distrib_trace(int on);
+// concurrency of the engine's compute and communication streams on devices[0]
+// (two spinning kernels; ms[4] = their start / end times)
+bool distrib_overlap_probe(const int* devices, int R, uint32_t spin_us, double* ms);
 bool distrib_sort_u32(const int* devices, int R, const uint32_t* const* d_in, const size_t* n_in, uint32_t* const* d_out,
                       size_t* n_out, unsigned flags, int digit_bits);
 // (u64 key, u32 payload) pairs, stable (configs[4]): the top-digit rounds on

@@ -97,6 +97,7 @@ _SIGS = [
      [ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint32]),
     ("libsortDistribLastBytes", ctypes.c_int, [ctypes.c_int, _u64p]),
     ("libsortSetDistribTrace", ctypes.c_int, [ctypes.c_int]),
+    ("libsortDistribOverlapProbe", ctypes.c_int, [ctypes.c_int, _vp, ctypes.c_uint32, _vp]),
     ("libsortDistribPlanDigits", ctypes.c_int,
      [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_double, _vp, _vp]),
     ("libsortDistribRangeDigit", ctypes.c_int,

@@ -429,6 +429,7 @@ def merge_u32(a, b, out=None):
 
 
 LIBSORT_DISTRIB_LSD, LIBSORT_DISTRIB_COPY, LIBSORT_DISTRIB_SELF_RCCL, LIBSORT_DISTRIB_WIRE32 = 1, 2, 4, 8
+LIBSORT_DISTRIB_CODED = 16
 
 
 def distrib_last_bytes(nranks):

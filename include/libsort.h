@@ -283,6 +283,16 @@ LIBSORT_API bool gpuDistribSort(uint32_t* h_in, size_t len, int ngpu);
  * already names), 3 bytes instead of 4; LIBSORT_DISTRIB_WIRE24=0 in the
  * environment does the same as this flag. */
 #define LIBSORT_DISTRIB_WIRE32 8u
+/* LIBSORT_DISTRIB_CODED: gap-coded rounds -- each sender sorts its outgoing
+ * pieces of a round and sends them as gaps (64-key groups: a base word and
+ * 2w words, w = the bits of the piece's largest gap; ~0.3 of the 32-bit
+ * bytes for uniform keys), the receiver decodes them and merges its sorted
+ * runs.  Fewer bytes on the links for more GPU work (a merge level per
+ * doubling of nranks): the default at two ranks on two GPUs over RCCL, where
+ * one xGMI link carries half of every shard.  LIBSORT_DISTRIB_CODED=1 / 0 in
+ * the environment forces it on / off.  Same result (a full sort is unique);
+ * the skew fallback to the LSD rounds is unchanged. */
+#define LIBSORT_DISTRIB_CODED 16u
 LIBSORT_API bool libsortDistribSortU32(int nranks, const int* devices, const uint32_t* const* d_in,
                                        const size_t* n_in, uint32_t* const* d_out, size_t* n_out,
                                        uint32_t flags);
@@ -314,6 +324,15 @@ LIBSORT_API bool libsortDistribSortPairsU64U32(int nranks, const int* devices, c
  * timing mode.  on: 1 / 0; returns the previous setting (initially
  * LIBSORT_DISTRIB_TRACE=1 in the environment). */
 LIBSORT_API int libsortSetDistribTrace(int on);
+
+/* Whether the multi-GPU engine's compute and communication streams of
+ * devices[0] (its context over these nranks devices) run concurrently in the
+ * calling process: one spinning single-wave kernel of spin_us microseconds on
+ * each; ms[0..3] receives the start and end of the first and the start and
+ * end of the second, in milliseconds after a common event.  Windows that do
+ * not overlap mean the two streams share one hardware queue (more streams on
+ * the device than GPU_MAX_HW_QUEUES).  A diagnostic; synchronous. */
+LIBSORT_API bool libsortDistribOverlapProbe(int nranks, const int* devices, uint32_t spin_us, double* ms);
 
 /* Bytes each rank sent to the other ranks in the exchange rounds (its own
  * pieces and the final re-cut's surplus keys excluded) in the last

@@ -164,6 +164,146 @@ static bool run_msd(const Vec& x, int R, int K, double growth, bool range = fals
   return true;
 }
 
+// The coded words of a sorted piece, as libsortDeltaPackU32 lays them out
+// (k_delta_pack): ng = ceil(n / 64) base words (each group's first key), then
+// per group 2w words holding lane l's gap (key l - key l-1, 0 for lane 0) at
+// bits [l w, l w + w).  A host restatement for the simulation only.
+static void delta_pack(const uint32_t* k, uint64_t n, uint32_t w, uint32_t* out) {
+  const uint64_t ng = (n + 63) / 64;
+  uint32_t* payload = out + ng;
+  for (uint64_t g = 0; g < ng; ++g) {
+    out[g] = k[g * 64];
+    uint32_t* words = payload + g * 2 * w;
+    for (uint32_t q = 0; q < 2 * w; ++q) words[q] = 0;
+    for (uint32_t l = 1; l < 64 && g * 64 + l < n; ++l) {
+      const uint32_t gap = k[g * 64 + l] - k[g * 64 + l - 1];
+      const uint32_t bit = l * w, q = bit >> 5, r = bit & 31u;
+      words[q] |= gap << r;
+      if (r + w > 32u) words[q + 1] |= gap >> (32u - r);
+    }
+  }
+}
+
+static void delta_unpack(const uint32_t* in, uint64_t n, uint32_t w, uint32_t* k) {
+  const uint64_t ng = (n + 63) / 64;
+  const uint32_t* payload = in + ng;
+  const uint32_t mask = w >= 32 ? 0xffffffffu : ((1u << w) - 1u);
+  for (uint64_t g = 0; g < ng; ++g) {
+    uint32_t acc = in[g];
+    const uint32_t* words = payload + g * 2 * w;
+    for (uint32_t l = 0; l < 64 && g * 64 + l < n; ++l) {
+      uint32_t gap = 0;
+      if (w) {
+        const uint32_t bit = l * w, q = bit >> 5, r = bit & 31u;
+        const uint64_t two = ((uint64_t)(r + w > 32u ? words[q + 1] : 0u) << 32) | words[q];
+        gap = (uint32_t)(two >> r) & mask;
+      }
+      acc += gap;
+      k[g * 64 + l] = acc;
+    }
+  }
+}
+
+// gap-coded rounds (distrib.cpp run_coded_rounds): the partition and plan of
+// the top-digit rounds, then the coded layout (distrib_plan.h coded_plan,
+// coded_round_pieces): each sender sorts its (round, destination) pieces,
+// codes the remote ones into its worst-case send regions, the pieces move at
+// their exact coded sizes into the receivers' regions, each receiver decodes
+// and merges its runs into the round's place (direct or scratch), re-cut.
+// self_coded: the own piece coded and moved too (one-rank RCCL tests).
+static bool run_coded(const Vec& x, int R, int K, double growth, bool self_coded) {
+  std::vector<Vec> in = split(x, R);
+  auto dig = [&](uint32_t k) -> uint32_t { return k >> kTopShift; };
+  std::vector<std::vector<uint64_t>> C(R, std::vector<uint64_t>(kTopDigits, 0));
+  std::vector<Vec> part(R);
+  for (int r = 0; r < R; ++r) {
+    for (uint32_t k : in[r]) C[r][dig(k)]++;
+    std::vector<uint64_t> at(kTopDigits + 1, 0);
+    for (int g = 0; g < kTopDigits; ++g) at[g + 1] = at[g] + C[r][g];
+    part[r].resize(in[r].size());
+    for (uint32_t k : in[r]) part[r][at[dig(k)]++] = k;
+  }
+  std::vector<uint8_t> lut(kTopDigits);
+  std::vector<int64_t> est(R);
+  plan_digit_rounds(C, K, growth, lut.data(), est.data());
+  DigitPlan p = digit_plan(C, lut.data(), K);
+  CodedPlan cp = coded_plan(p, C, self_coded);
+  std::vector<Vec> srt(R), csend(R), crecv(R), out(R), fin(R);
+  for (int r = 0; r < R; ++r) {
+    srt[r].assign(part[r].size(), 0xdeadbeefu);
+    csend[r].assign(cp.coff[r][(size_t)R * K], 0xdeadbeefu);
+    crecv[r].assign(cp.rcap[r], 0xdeadbeefu);
+    out[r].assign(p.n_recv[r], 0);
+    CHECK(cp.start[r][kTopDigits] == part[r].size(), "digit starts of rank %d", r);
+  }
+  const uint64_t S = shard_size(x.size(), R);
+  for (int r = 0; r < R; ++r) fin[r].assign(std::min<uint64_t>(S, x.size() - std::min<uint64_t>(x.size(), r * S)), 0);
+  Placement pl = place_rounds(p.roff, p.n_recv, K);
+  const size_t stride = (size_t)R * K;
+  std::vector<uint32_t> mg((size_t)R * stride, 0xffffffffu);
+  for (int i = 0; i < K; ++i) {
+    for (int s = 0; s < R; ++s)
+      for (int d = 0; d < R; ++d) {
+        const size_t j = (size_t)i * R + d;
+        const uint64_t m = cp.M[s][j], a = cp.start[s][p.lo[j]];
+        if (!m) continue;
+        std::copy(part[s].begin() + a, part[s].begin() + a + m, srt[s].begin() + a);
+        std::sort(srt[s].begin() + a, srt[s].begin() + a + m);
+        if (s == d && !self_coded) continue;
+        uint32_t g = 0;
+        for (uint64_t t = 1; t < m; ++t) g = std::max(g, srt[s][a + t] - srt[s][a + t - 1]);
+        mg[(size_t)s * stride + j] = g;
+        const uint32_t w = gap_bits(g);
+        CHECK(delta_words(m, w) <= cp.coff[s][j + 1] - cp.coff[s][j], "coded piece overflows its send region");
+        delta_pack(srt[s].data() + a, m, w, csend[s].data() + cp.coff[s][j]);
+      }
+    const std::vector<Piece> ps = coded_round_pieces(cp, i, mg.data(), stride, self_coded);
+    for (const Piece& q : ps) {
+      CHECK(q.dst_off == cp.cr_off[q.dst][(size_t)i * R + q.src], "coded piece not at its receive region");
+      CHECK(q.src_off + q.count <= csend[q.src].size() && q.dst_off + q.count <= crecv[q.dst].size(),
+            "coded piece out of range");
+      memcpy(crecv[q.dst].data() + q.dst_off, csend[q.src].data() + q.src_off, q.count * 4);
+    }
+    for (int d = 0; d < R; ++d) {
+      const size_t q2 = (size_t)d * K + i;
+      const uint64_t r0 = p.roff[(size_t)d * (K + 1) + i], r1 = p.roff[(size_t)d * (K + 1) + i + 1];
+      Vec merged;
+      for (int s = 0; s < R; ++s) {
+        const size_t j = (size_t)i * R + d;
+        const uint64_t m = cp.M[s][j];
+        if (!m) continue;
+        Vec run(m);
+        if (s == d && !self_coded) {
+          std::copy(srt[d].begin() + cp.start[d][p.lo[j]], srt[d].begin() + cp.start[d][p.lo[j]] + m, run.begin());
+        } else {
+          delta_unpack(crecv[d].data() + cp.cr_off[d][(size_t)i * R + s], m, gap_bits(mg[(size_t)s * stride + j]),
+                       run.data());
+        }
+        Vec nx(merged.size() + m);
+        std::merge(merged.begin(), merged.end(), run.begin(), run.end(), nx.begin());
+        merged.swap(nx);
+      }
+      CHECK(merged.size() == r1 - r0, "rank %d round %d merges %zu of %llu keys", d, i, merged.size(),
+            (unsigned long long)(r1 - r0));
+      bool others = false;
+      for (int s = 0; s < R; ++s)
+        if (s != d && cp.M[s][(size_t)i * R + d]) others = true;
+      CHECK((cp.self_only[q2] != 0) == (!others && !self_coded), "self_only of rank %d round %d", d, i);
+      Vec& dst = pl.direct[q2] ? fin[d] : out[d];
+      const uint64_t at = pl.direct[q2] ? pl.out_off[q2] : r0;
+      CHECK(at + merged.size() <= dst.size(), "round placed past its buffer");
+      std::copy(merged.begin(), merged.end(), dst.begin() + at);
+    }
+  }
+  apply(pl.moves, out, fin);
+  Vec want(x);
+  std::sort(want.begin(), want.end());
+  std::vector<Vec> ws = split(want, R);
+  for (int r = 0; r < R; ++r)
+    CHECK(fin[r] == ws[r], "coded shard %d differs (R=%d K=%d n=%zu self=%d)", r, R, K, x.size(), (int)self_coded);
+  return true;
+}
+
 // reference BSP rounds: stable 8-bit partial sort per rank, exchange, gather
 static bool run_lsd(const Vec& x, int R, int width) {
   std::vector<Vec> cur = split(x, R);
@@ -389,6 +529,11 @@ int main() {
         }
         if (n <= 40001) {
           run_lsd(x, R, 8);
+          ++cases;
+        }
+        for (int K : {1, 4}) {
+          run_coded(x, R, K, 1.2, false);
+          if (R <= 2) run_coded(x, R, K, 1.2, true);
           ++cases;
         }
       }

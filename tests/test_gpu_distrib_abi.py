@@ -23,7 +23,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
-LSD, COPY, SELF_RCCL, WIRE32 = 1, 2, 4, 8
+LSD, COPY, SELF_RCCL, WIRE32, CODED = 1, 2, 4, 8, 16
 
 
 @pytest.fixture(scope="module")
@@ -216,10 +216,49 @@ def test_wire24(D, oracle_mod, R, n):
         pylibsort.setDigitBits(prev)
 
 
+@pytest.mark.parametrize("R", [1, 2, 3, 8])
+@pytest.mark.parametrize("case", ["pcg", "dups", "skewtop", "allequal", "small", "tiny"])
+def test_coded_rounds(D, oracle_mod, bits, R, case):
+    """The gap-coded rounds (LIBSORT_DISTRIB_CODED; VERDICT r05 item 2: the
+    torch engine's msdz in the C engine): every sender sorts its outgoing
+    pieces, codes them as gaps, the receiver decodes and merges R runs.  R = 1
+    sends every coded piece through a one-rank RCCL communicator; R > 1 shares
+    the GPU (device copies).  Exact against the oracle, shards of ceil(N/R);
+    skewed inputs take the range digit or the LSD rounds as without coding."""
+    x = _cases(oracle_mod)[case]
+    flags = (SELF_RCCL if R == 1 else COPY) | CODED
+    _check(oracle_mod, x, _run(D, x, R, flags, ragged=(case == "pcg")), R, False)
+
+
+@pytest.mark.parametrize("R", [2, 4])
+def test_coded_rounds_bytes(D, oracle_mod, R):
+    """The coded exchange's bytes (libsortDistribLastBytes counts the coded
+    words): for 2^23 uniform keys well under half the 32-bit format's -- the
+    gap width is ~log2(2^32 R K / n) + 2 bits -- and exact against the oracle
+    with and without the stage trace."""
+    import pylibsort
+    x = oracle_mod.pcg((1 << 23) + 3, first=21)
+    o32 = _run(D, x, R, COPY | WIRE32)
+    b32 = D.distrib_last_bytes(R)
+    oz = _run(D, x, R, COPY | CODED)
+    bz = D.distrib_last_bytes(R)
+    _check(oracle_mod, x, o32, R, False)
+    _check(oracle_mod, x, oz, R, False)
+    assert all(0 < z < 0.5 * w for z, w in zip(bz, b32)), (bz, b32)
+    L = pylibsort.lib()
+    prev = L.libsortSetDistribTrace(1)
+    try:
+        _check(oracle_mod, x, _run(D, x, R, COPY | CODED), R, False)
+    finally:
+        L.libsortSetDistribTrace(prev)
+    assert pylibsort.lib().libsortDeviceErrors() == 0
+
+
 @pytest.mark.parametrize("reserve", ["on", "nomem"])
 def test_wire24_reserved_depth0_odd_offsets(D, oracle_mod, reserve):
-    """Two ranks, 2^24 + 77 keys: rounds of ~2^21 keys over <= 32 segments, so
-    the round sorts read the 24-bit planes through the reserved depth 0's
+    """Two ranks, 2^26 + 77 keys: rounds of ~2^23 keys over <= 32 segments
+    (two digit depths below the top digit), so the round sorts read the 24-bit
+    planes through the reserved depth 0's
     planar loader, at round offsets (and 8-bit plane starts 2 n_recv + a) that
     are not multiples of 4 (the loader aligns on the absolute
     address).  reserve=nomem: the reserved depth 0 is unavailable, so the
@@ -232,7 +271,7 @@ def test_wire24_reserved_depth0_odd_offsets(D, oracle_mod, reserve):
     if reserve == "nomem":
         os.environ["LIBSORT_HYB_RESERVE"] = "nomem"
     try:
-        x = oracle_mod.pcg((1 << 24) + 77, first=11)
+        x = oracle_mod.pcg((1 << 26) + 77, first=11)
         outs, (nrsv, nseg) = _timed_names(D, lambda: _run(D, x, 2, COPY), "rsvsample", "segcopy")
         _check(oracle_mod, x, outs, 2, False)
         if reserve == "on":
@@ -390,12 +429,14 @@ sys.path[:0] = [%r, %r]
 import pylibsort.device as D
 from oracle import oracle
 x = oracle.pcg((1 << 22) + 999, first=4)
-for R, flags in ((1, 4), (3, 2)):
+for R, flags in ((1, 4), (3, 2), (2, 2 | 16), (3, 2 | 16)):
     S = -(-x.size // R)
     sh = [torch.from_numpy(x[r * S:(r + 1) * S].view(np.int32).copy()).cuda() for r in range(R)]
     outs = D.distrib_sort_u32(sh, flags)
     got = np.concatenate([o.cpu().numpy().view(np.uint32) for o in outs])
     assert np.array_equal(got, oracle.sort_u32(x)), R
+    if flags & 16:
+        continue  # (the coded rounds are for keys only)
     k = (x.astype(np.uint64) << np.uint64(32)) | x.astype(np.uint64)[::-1]
     v = np.arange(x.size, dtype=np.uint32)
     ks = [torch.from_numpy(k[r * S:(r + 1) * S].view(np.int64).copy()).cuda() for r in range(R)]
@@ -452,3 +493,29 @@ def test_stage_trace(D, oracle_mod, capfd, lsd):
     capfd.readouterr()
     _run(D, x, 4, COPY)
     assert "libsort distrib [" not in capfd.readouterr().err
+
+
+def test_engine_streams_overlap(D, oracle_mod):
+    """in the C engine's driving process -- torch's
+    streams in use, libsort's workspace streams, the engine's compute (st) and
+    communication (cs) streams and RCCL's communicator (a one-rank RCCL sort
+    first) -- a spinning kernel on st and one on cs run at the same time, so
+    with the box's GPU_MAX_HW_QUEUES = 4 the two streams are not multiplexed
+    onto one in-order hardware queue (where an RCCL kernel waiting for its
+    peer on cs would hold the round sorts on st)."""
+    import ctypes
+    import os
+    import pylibsort
+    x = D.populate_u32(1 << 22)                       # torch's stream
+    D.sort_keys_u32(x)                                # libsort's workspace stream
+    torch.cuda.synchronize()
+    xs = oracle_mod.pcg((1 << 20) + 7, first=2)
+    _check(oracle_mod, xs, _run(D, xs, 1, SELF_RCCL), 1, False)  # the engine's streams + RCCL's
+    ms = (ctypes.c_double * 4)()
+    devs = (ctypes.c_int * 1)(0)
+    assert pylibsort.lib().libsortDistribOverlapProbe(1, devs, 20000, ms) == 1, pylibsort.last_error()
+    st0, st1, cs0, cs1 = list(ms)
+    print("GPU_MAX_HW_QUEUES=%s st [%.3f, %.3f] ms, cs [%.3f, %.3f] ms" % (
+        os.environ.get("GPU_MAX_HW_QUEUES"), st0, st1, cs0, cs1))
+    assert st1 - st0 > 15.0 and cs1 - cs0 > 15.0, list(ms)   # both spun ~20 ms
+    assert cs0 < st1 - 10.0 and st0 < cs1 - 10.0, list(ms)   # the windows overlap

@@ -14,7 +14,9 @@ Parity:
   make_big_golden.py 2pow32 after re-pinning the reference's own 2^20 hash).
   Shard r holds ceil(N/R) keys (the reference's equal re-cut,
   benchmark/pkg/sort/distrib.go:107-113).  Both schedules: the top-digit
-  rounds and the reference's BSP LSD rounds (localTest/benchmarks.cpp:70-160,
+  rounds, the gap-coded rounds (msdz: sender sorts, coded exchange, receiver
+  merges; 8 ranks of 2^29 and the reference's own 2-worker shape at 2 ranks
+  of 2^31) and the reference's BSP LSD rounds (localTest/benchmarks.cpp:70-160,
   distrib.go:119-176), plus a ragged 5-rank cut of the same keys.
 - pairs (configs[4], 2^31 (u64 key, u32 payload) pairs, payload = global
   input index): a complete proof of equality with std::stable_sort by key,
@@ -34,7 +36,7 @@ import pytest
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 torch = pytest.importorskip("torch")
 
-LSD, COPY = 1, 2
+LSD, COPY, CODED = 1, 2, 16
 BIG = pathlib.Path(__file__).with_name("golden") / "big_golden.json"
 
 
@@ -76,8 +78,10 @@ def _keys_input(D, cuts):
 
 
 @pytest.mark.parametrize("R, flags, ragged, bits", [(8, COPY, False, 8), (8, COPY, False, 4), (8, COPY | LSD, False, 8),
-                                                     (5, COPY, True, 4)],
-                         ids=["msd-8x2^29", "msd-8x2^29-wire24", "lsd-8x2^29", "msd-5ragged-wire24"])
+                                                     (5, COPY, True, 4), (8, COPY | CODED, False, 4),
+                                                     (2, COPY | CODED, False, 4)],
+                         ids=["msd-8x2^29", "msd-8x2^29-wire24", "lsd-8x2^29", "msd-5ragged-wire24", "msdz-8x2^29",
+                              "msdz-2x2^31"])
 def test_config3_full(D, R, flags, ragged, bits):
     """bits = the round sorts' digit width; at 4 the exchange carries 24-bit
     keys (the default wire format of the top-digit rounds)."""
