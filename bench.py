@@ -562,6 +562,24 @@ def committed_profile(bytes_per_launch):
     return out
 
 
+def committed_leg(leg):
+    """The committed rocprof average and PMC traffic of a leg's kernel
+    (profiles/<PROFILE_TAG>_legs.json, tools/make_profile_summary.py), for the
+    legs' live `frac` to be checked against (same command as the line)."""
+    try:
+        d = json.loads((ROOT / "profiles" / ("%s_legs.json" % PROFILE_TAG)).read_text())
+        g = d["legs"][leg]
+    except (OSError, ValueError, KeyError):
+        return {}
+    out = {"rocprof": {"avg_launch_us": round(g["avg_launch_us"], 2), "launches": g["launches"],
+                       "frac": g["frac_rocprof"], "kernel": g["kernel"],
+                       "source": "profiles/%s_legs.json" % PROFILE_TAG, "cmd": d.get("cmd")}}
+    if "hbm_bytes_per_launch" in g:
+        out["traffic"] = g["hbm_bytes_per_launch"]
+        out["traffic_over_algorithmic"] = g["traffic_over_algorithmic"]
+    return out
+
+
 def step_roofline(n, digit_bits, ms_per_step, kern):
     """The whole N=1 step against HBM: the bytes the
     hybrid sort actually moves per step -- one count read (4 B/key; none with
@@ -736,6 +754,21 @@ def config_leg(torch, pylibsort, D, which, reps):
             leg["scatter_roofline"] = {"achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                        "frac": round(ach / HBM_PEAK_GBPS, 4),
                                        "bytes_per_unit": unit_bytes}
+            # cross-checks from this round's committed profiles (pairs: the
+            # 16384-pair depth-0 and the 8192-pair table-depth passes)
+            for name in (("c3_pass",) if which == "c3" else ("c5_pass_depth0", "c5_pass_table")):
+                got = committed_leg(name)
+                if got:
+                    leg["scatter_roofline"].setdefault("committed", {})[name] = got
+        bk = kern.get("bucketsort")
+        if bk:
+            ach = unit_bytes * n / (bk["avg_us"] * 1e-6) / 1e9
+            bk["achieved_gbps"] = round(ach, 1)
+            bk["frac"] = round(ach / HBM_PEAK_GBPS, 4)
+            bk["bytes_per_unit"] = unit_bytes
+            got = committed_leg("c3_bucket" if which == "c3" else "c5_bucket")
+            if got:
+                bk["committed"] = got
         if not ok:
             raise RuntimeError("%s leg failed verification" % which)
         return leg
@@ -764,6 +797,17 @@ def partial_leg(torch, pylibsort, D, keys, out, tmp, width, reps, calls=3):
     host ABI returns the same data and boundaries."""
     import ctypes
     import numpy as np
+    # the library's default digit width (8 bits: LIBSORT_DIGIT_BITS unset),
+    # what gpuPartial callers get, not the 4-bit digits configs[1] names for
+    # the full sort
+    prev_bits = pylibsort.setDigitBits(8)
+    try:
+        return _partial_leg(torch, pylibsort, D, keys, out, tmp, width, reps, calls, ctypes, np)
+    finally:
+        pylibsort.setDigitBits(prev_bits)
+
+
+def _partial_leg(torch, pylibsort, D, keys, out, tmp, width, reps, calls, ctypes, np):
     n = keys.numel()
     b = torch.empty(1 << width, dtype=torch.int32, device="cuda")
 
@@ -820,6 +864,9 @@ def partial_leg(torch, pylibsort, D, keys, out, tmp, width, reps, calls=3):
         ach = 8.0 * tp["keys_per_launch"] / (tp["avg_us"] * 1e-6) / 1e9
         leg["pass_roofline"] = {"achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                 "frac": round(ach / HBM_PEAK_GBPS, 4), "bytes_per_key": 8.0}
+        got = committed_leg("partial_pass")
+        if got:
+            leg["pass_roofline"]["committed"] = got
     # the whole call against HBM: per digit pass one count read (4 B/key) and
     # the pass (8 B/key); the boundaries are 2^width words
     passes = -(-width // pylibsort.getDigitBits())

@@ -84,6 +84,7 @@ struct Workspace {
   size_t os_status_cap = 0;  // words per buffer
   uint32_t* os_small = nullptr;
   int last_algo = 0;  // 1 = onesweep, 2 = reduce-then-scan, 3 = tile offsets (last sort)
+  uint32_t* last_pass_counts = nullptr;  // tile path: the last pass's scanned count rows (gpuPartial boundaries)
 
   // tile-offset path: per-tile digit counts (two buffers) and chunk totals
   uint32_t* tc[2] = {nullptr, nullptr};

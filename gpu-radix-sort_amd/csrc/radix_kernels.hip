@@ -3079,6 +3079,113 @@ __global__ void k_bounds_mark(const K* __restrict__ sorted, uint32_t n, uint32_t
   }
 }
 
+// The same for uint32 keys, 16 consecutive keys per thread (four 16-byte
+// loads when the array is 16-byte aligned) and the previous key once: the
+// grid-stride form above ran the 2^28-key, width-16 gpuPartial's boundaries
+// at ~550 us against ~200 us for one read of the keys.
+constexpr int kBmkItems = 16;
+__global__ __launch_bounds__(256) void k_bounds_mark_u32(const uint32_t* __restrict__ sorted, uint32_t n,
+                                                         uint32_t shift, uint32_t gmask, uint32_t vec,
+                                                         uint32_t* __restrict__ bounds) {
+  const uint64_t i0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * kBmkItems;
+  if (i0 >= n) return;
+  uint32_t k[kBmkItems];
+  if (vec && i0 + kBmkItems <= n) {
+    const uint4* p = reinterpret_cast<const uint4*>(sorted + i0);
+#pragma unroll
+    for (int q = 0; q < kBmkItems / 4; ++q) {
+      const uint4 v = load_count_vec(&p[q]);
+      k[4 * q] = v.x;
+      k[4 * q + 1] = v.y;
+      k[4 * q + 2] = v.z;
+      k[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kBmkItems; ++j) k[j] = i0 + j < n ? sorted[i0 + j] : 0u;
+  }
+  // (the sentinel ~0u is no group: width <= 31)
+  uint32_t prev = i0 ? (sorted[i0 - 1] >> shift) & gmask : ~0u;
+#pragma unroll
+  for (int j = 0; j < kBmkItems; ++j) {
+    if (i0 + j >= n) break;
+    const uint32_t g = (k[j] >> shift) & gmask;
+    if (g != prev) bounds[g] = (uint32_t)(i0 + j);
+    prev = g;
+  }
+}
+
+// Boundaries of a two-pass LSD partial sort (tile path) without reading the
+// sorted keys: pass 0 sorted by the low digit l (BITS bits), pass 1 by the
+// high digit d (the remaining width - BITS bits) of its input `mid` (= pass
+// 0's output, ordered by l).  The number of keys of group (d, l) or below in
+// (d, l) order is D[d] + the keys of digit d in mid[0, pos_l), pos_l = the
+// first position of mid whose low digit is >= l -- which is the run start of
+// digit d in pos_l's tile (C + B + D of pass 1's column scan: the offset
+// k_tile_pass gives that tile's run) plus the keys of digit d in the tile
+// before pos_l.  Block l: pos_l by a 256-ary search over mid, the partial
+// tile's digit counts in LDS, then bounds[(d << BITS) | l] for every d.
+// ~4 KB x 2^BITS of reads instead of a pass over the keys (the 2^28-key,
+// width-16 gpuPartial: ~200 us of k_bounds_mark_u32 otherwise).
+template <int BITS, int TILE>
+__global__ __launch_bounds__(256) void k_bounds_lsd2(const uint32_t* __restrict__ mid, uint32_t n, uint32_t lo,
+                                                     uint32_t dmask, const uint32_t* __restrict__ C,
+                                                     const uint32_t* __restrict__ B, const uint32_t* __restrict__ D,
+                                                     uint32_t* __restrict__ bounds) {
+  constexpr uint32_t RADIX = 1u << BITS;
+  constexpr int CH = col_chunk_rows(RADIX);
+  __shared__ uint32_t s_h[RADIX];
+  __shared__ uint32_t s_first;
+  __shared__ uint64_t s_lo, s_hi;
+  const uint32_t l = blockIdx.x, tid = threadIdx.x;
+  auto low = [&](uint64_t i) { return (mid[i] >> lo) & (RADIX - 1u); };
+  for (uint32_t d = tid; d < RADIX; d += 256) s_h[d] = 0u;
+  if (tid == 0) {
+    s_lo = 0;
+    s_hi = n;
+  }
+  __syncthreads();
+  // pos_l = the first i in [0, n) with low(i) >= l (n when none): the answer
+  // lies in [s_lo, s_hi]; 256 evenly spaced probes per round narrow it to
+  // one step, then the last <= 256 candidates are checked one per thread
+  for (;;) {
+    const uint64_t a = s_lo, z = s_hi;
+    __syncthreads();
+    if (z - a <= 256) {
+      if (tid == 0) s_first = (uint32_t)z;
+      __syncthreads();
+      if (a + tid < z && low(a + tid) >= l) atomicMin(&s_first, (uint32_t)(a + tid));
+      __syncthreads();
+      break;
+    }
+    const uint64_t step = (z - a + 255) / 256;
+    const uint32_t nv = (uint32_t)((z - a + step - 1) / step);  // probes inside [a, z)
+    if (tid == 0) s_first = nv;
+    __syncthreads();
+    if (tid < nv && low(a + (uint64_t)tid * step) >= l) atomicMin(&s_first, tid);
+    __syncthreads();
+    const uint32_t f = s_first;  // first probe at or past pos_l (nv: none)
+    if (tid == 0) {
+      if (f > 0) s_lo = a + (uint64_t)(f - 1) * step + 1;
+      s_hi = f < nv ? a + (uint64_t)f * step : z;
+    }
+    __syncthreads();
+  }
+  const uint32_t pos = s_first;
+  const uint32_t t = pos / TILE, t0 = t * TILE;
+  for (uint32_t i = t0 + tid; i < pos; i += 256) atomicAdd(&s_h[(mid[i] >> (lo + BITS)) & dmask], 1u);
+  __syncthreads();
+  const uint32_t tiles = (n + TILE - 1) / TILE;
+  for (uint32_t d = tid; d <= dmask; d += 256) {
+    uint32_t base;
+    if (t < tiles)
+      base = C[(size_t)t * RADIX + d] + B[(size_t)(t / CH) * RADIX + d] + D[d];
+    else  // pos == n at a tile edge: every key of digit d lies before
+      base = d < dmask ? D[d + 1] : n;
+    bounds[((size_t)d << BITS) | l] = base + s_h[d];
+  }
+}
+
 // min over each kBmTile-entry block of bounds -> mins[block]
 __global__ __launch_bounds__(kBmBlock) void k_bounds_min_blocks(const uint32_t* __restrict__ bounds, uint64_t ng,
                                                               uint32_t* __restrict__ mins) {
@@ -3942,6 +4049,20 @@ inline bool dstream_on() {
   return on;
 }
 
+// The same digit stream for the 32-bit keys-only hybrid at 8-bit digits
+// (configs[2]): the reserved depth 0 writes each key's next digit at its
+// slice position, and depth 1 counts those bytes instead of re-reading the
+// keys (804 us per 2^30-key sort).  LIBSORT_DSTREAM_U32=1: A/B only (VERDICT
+// r05 item 4b; round 3 measured the byte stores costing the pass more than
+// the count saves).
+inline bool dstream_u32_on() {
+  static const bool on = [] {
+    const char* s = getenv("LIBSORT_DSTREAM_U32");
+    return s && s[0] == '1';
+  }();
+  return on;
+}
+
 // Sort prologue of the tile path: buffers, and (4-bit) the pass-0 counts.
 template <typename K, typename V, typename Op = RadixDigit>
 hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, int bits, hipStream_t st,
@@ -3994,6 +4115,7 @@ hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vou
   else if (!fused_counts && !(BITS == 4 && p == 0))
     LS_TRY((tiles_counts<BITS, K, Op, V>(ws, kin, n, op, tiles, cur, nullptr, 0, st)));
   LS_TRY(tiles_colscan<BITS>(ws, cur, tiles, st));
+  ws.last_pass_counts = cur;
   const bool fuse = fused_counts && p + 1 < P;
   const bool dnext = dstream && p + 1 < P;
   const int nb2 = (fuse || dnext) ? std::min(BITS, hi - shift - BITS) : 1;
@@ -4170,9 +4292,10 @@ hipError_t group_bounds(Workspace& ws, const uint32_t* sorted, size_t n, int lo,
     ws.hist_tmp_cap = nb;
   }
   LS_TRY(hipMemsetAsync(d_bounds, 0xff, (size_t)ngroups * sizeof(uint32_t), st));
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + 255) / 256, 8192);
-  hipLaunchKernelGGL(k_bounds_mark<uint32_t>, dim3(blocks), dim3(256), 0, st, sorted, (uint32_t)n, (uint32_t)lo,
-                     ngroups - 1u, d_bounds);
+  const uint32_t blocks = (uint32_t)((n + 256 * kBmkItems - 1) / (256 * kBmkItems));
+  const uint32_t vec = (reinterpret_cast<uintptr_t>(sorted) & 15u) == 0 ? 1u : 0u;
+  hipLaunchKernelGGL(k_bounds_mark_u32, dim3(blocks), dim3(256), 0, st, sorted, (uint32_t)n, (uint32_t)lo,
+                     ngroups - 1u, vec, d_bounds);
   LS_TRY(hipGetLastError());
   hipLaunchKernelGGL(k_bounds_min_blocks, dim3((uint32_t)nb), dim3(kBmBlock), 0, st, d_bounds, (uint64_t)ngroups,
                      ws.hist_tmp);
@@ -4455,8 +4578,9 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
                        tiles[0], ctile0[0], cstart[0], ctr);
     LS_TRY(hipGetLastError());
   }
-  const bool dstream = BITS == 8 && sizeof(K) == 8 && dstream_on();
-  if (dstream) LS_TRY(ws.ensure_dstream(n));
+  const bool dstream = BITS == 8 && dstream_on() && (sizeof(K) == 8 || (kRsvOk && !pc && dstream_u32_on()));
+  // (reserved depth 0: the stream in the slices' coordinates)
+  if (dstream) LS_TRY(ws.ensure_dstream(rsv ? std::max(n, rcur_off) : n));
   ws.part_pending.valid = false;
 
   // keys only: the passes may reorder within a run (k_tile_pass ANY_ORDER)
@@ -4484,6 +4608,7 @@ hipError_t sort_hybrid(Workspace& ws, const K* in, K* out, K* tmp, const V* vin,
         // Reserved depth 0 (sampled above): the pass reserves its runs in the
         // slices; the next depth's tiles and child starts from the cursors
         HybridGeo g0{tiles[0], ctr, nullptr, nullptr, nullptr, rcur, rslice, ctr + 14, rns};
+        if (dstream && !last) g0.dout = ws.dstream;  // (the next depth's digits, slice positions)
         if (pc) {
           g0.i16 = pc->i16;
           g0.i8 = pc->i8;
@@ -4839,6 +4964,20 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
       // tile path, single pass: the column scan's digit starts
       LS_TRY(hipMemcpyAsync(d_bounds, tiles_digit_starts(ws, tp_tiles<uint32_t>(n, digit_bits), digit_bits),
                             (size_t)ngroups * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+    } else if (ws.last_algo == 3 && num_passes(width, digit_bits) == 2 && ws.last_pass_counts) {
+      // two passes: from the last pass's counts and the middle buffer (tmp)
+      const uint32_t tiles = tp_tiles<uint32_t>(n, digit_bits);
+      const uint32_t dmask = (1u << (width - digit_bits)) - 1u;
+      if (digit_bits == 8) {
+        constexpr int T8 = tp_block<uint32_t>(8) * tp_items<uint32_t>(8);
+        hipLaunchKernelGGL((k_bounds_lsd2<8, T8>), dim3(256), dim3(256), 0, st, tmp, (uint32_t)n, (uint32_t)lo, dmask,
+                           ws.last_pass_counts, ws.tb, tiles_digit_starts(ws, tiles, 8), d_bounds);
+      } else {
+        constexpr int T4 = tp_block<uint32_t>(4) * tp_items<uint32_t>(4);
+        hipLaunchKernelGGL((k_bounds_lsd2<4, T4>), dim3(16), dim3(256), 0, st, tmp, (uint32_t)n, (uint32_t)lo, dmask,
+                           ws.last_pass_counts, ws.tb, tiles_digit_starts(ws, tiles, 4), d_bounds);
+      }
+      LS_TRY(hipGetLastError());
     } else if (ws.last_algo == 3) {
       LS_TRY(group_bounds(ws, out, n, lo, ngroups, d_bounds, st));
     } else if (ws.last_algo == 1 && width <= 8) {

@@ -18,7 +18,7 @@ BENCH="python3 bench.py --gpus 1 --steps 20 --warmup 5"
 echo "$BENCH" > "$OUT/cmd.txt"
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c -d "$OUT/pmc_$c" -o run --output-format csv \
-    --kernel-include-regex "tile_pass|bucket_sort|bucket_count" -- $BENCH > "$OUT/pmc_$c.log" 2>&1 || { echo "pmc $c failed"; tail -5 "$OUT/pmc_$c.log"; exit 1; }
+    --kernel-include-regex "tile_pass|bucket_sort|bucket_count|bucket_pairs|tile_counts" -- $BENCH > "$OUT/pmc_$c.log" 2>&1 || { echo "pmc $c failed"; tail -5 "$OUT/pmc_$c.log"; exit 1; }
   echo "pmc $c done"
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run --output-format csv -- $BENCH \

@@ -8,6 +8,12 @@ summaries under profiles/ -- all of the driver's exact bench command:
                               timed steps' launches (bench.py reads this)
   TAG_pmc_tilepass.json       HBM bytes per launch of the same launches from
                               FETCH_SIZE / WRITE_SIZE (bench.py's `traffic`)
+  TAG_legs.json               the same (rocprof average + FETCH/WRITE bytes per
+                              launch) for the other legs' dominant kernels:
+                              configs[2]'s 8-bit passes and bucket counter,
+                              configs[4]'s pair passes (16384-pair depth 0,
+                              8192-pair table depths) and k_bucket_pairs, the
+                              gpuPartial legs' 8-bit pass (bench.py reads it)
   TAG_bench.json, TAG_bw_probe.txt, TAG_calib_copy_rocprim.txt
 gfx950 correction (MI355X_MICROARCH.md "HBM"): FETCH_SIZE reports half the
 bytes of a streaming read (verified on the box with tools/calib_copy, 4- and
@@ -134,3 +140,65 @@ if fetch and write and bs:
            "method": "same runs as %s_pmc_tilepass.json" % tag, "round": tag}
     (dst / ("%s_bucketsort.json" % tag)).write_text(json.dumps(rec, indent=1) + "\n")
     print(json.dumps(rec))
+
+
+# ---------------------------------------------------------------------------
+# the other legs of the N = 1 line (bench.py variants.c3 / c5 / partial*)
+# ---------------------------------------------------------------------------
+def _name(r):
+    return r.get("Kernel_Name", "")
+
+
+def _wg(r):
+    return int(float(r.get("Workgroup_Size_X", r.get("Workgroup_Size", 0)) or 0))
+
+
+LEGS = {
+    # configs[2]: 2^30 u32 keys, the MSD hybrid at 8-bit digits (depth 0 reserved, depth 1 from the table)
+    "c3_pass": (lambda r: "k_tile_pass<8, 512, 16, unsigned int, lsort::NoValue" in _name(r)
+                and _name(r).split(">(")[0].endswith("true") and _groups(r) >= (1 << 30) // 8192,
+                8.0 * (1 << 30), "k_tile_pass<8,512,16,u32> (configs[2] hybrid digit passes, 2^30 keys)"),
+    "c3_bucket": (lambda r: "k_bucket_count<1024," in _name(r), 8.0 * (1 << 30),
+                  "k_bucket_count<1024,17,...> (configs[2] bucket counter, 2^30 keys)"),
+    "c3_counts": (lambda r: "k_tile_counts<8, 512, 16, unsigned int" in _name(r) and _groups(r) >= (1 << 30) // 8192,
+                  4.0 * (1 << 30), "k_tile_counts<8,...,u32> (configs[2] depth-1 count read, 2^30 keys)"),
+    # configs[4] per-GPU share: 2^28 (u64, u32) pairs
+    "c5_pass_depth0": (lambda r: "k_tile_pass<8," in _name(r) and "unsigned long, unsigned int" in _name(r)
+                       and _wg(r) == 1024, 24.0 * (1 << 28),
+                       "k_tile_pass<8,1024,...,u64,u32> (configs[4] depth 0, 16384-pair tiles)"),
+    "c5_pass_table": (lambda r: "k_tile_pass<8," in _name(r) and "unsigned long, unsigned int" in _name(r)
+                      and _wg(r) == 512, 24.0 * (1 << 28),
+                      "k_tile_pass<8,512,...,u64,u32> (configs[4] table depth, 8192-pair tiles)"),
+    "c5_bucket": (lambda r: "k_bucket_pairs<" in _name(r), 24.0 * (1 << 28),
+                  "k_bucket_pairs<1024,...> (configs[4] bucket sort, 2^28 pairs)"),
+    # gpuPartial at the reference's workload (2^28 keys, stable LSD 8-bit passes)
+    "partial_pass": (lambda r: "k_tile_pass<8, 512, 16, unsigned int, lsort::NoValue" in _name(r)
+                     and _name(r).split(">(")[0].endswith("false")
+                     and (1 << 28) // 8192 <= _groups(r) <= (1 << 28) // 8192 + 1, 8.0 * (1 << 28),
+                     "k_tile_pass<8,512,16,u32> stable LSD pass (gpuPartial legs, 2^28 keys)"),
+}
+legs = {}
+for leg, (pick, alg, label) in LEGS.items():
+    ds = []
+    for f in trace:
+        for r in csv.DictReader(open(f)):
+            if pick(r):
+                ds.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    if not ds:
+        continue
+    rec = {"kernel": label, "launches": len(ds), "avg_launch_us": sum(ds) / len(ds),
+           "algorithmic_bytes_per_launch": alg,
+           "frac_rocprof": round(alg / (sum(ds) / len(ds) * 1e-6) / 1e9 / 8000.0, 4)}
+    fetch, write = pmc("FETCH_SIZE", pick), pmc("WRITE_SIZE", pick)
+    if fetch and write:
+        rec["read_bytes_per_launch"] = sum(fetch) / len(fetch) * 1024 * 2
+        rec["write_bytes_per_launch"] = sum(write) / len(write) * 1024
+        rec["hbm_bytes_per_launch"] = rec["read_bytes_per_launch"] + rec["write_bytes_per_launch"]
+        rec["traffic_over_algorithmic"] = round(rec["hbm_bytes_per_launch"] / alg, 4)
+    legs[leg] = rec
+if legs:
+    out = {"cmd": cmd, "round": tag, "method": "rocprofv3 kernel trace (durations) and --pmc FETCH_SIZE / WRITE_SIZE "
+           "in separate runs of the same command; read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE, KiB -> bytes",
+           "legs": legs}
+    (dst / ("%s_legs.json" % tag)).write_text(json.dumps(out, indent=1) + "\n")
+    print(json.dumps(out))
