@@ -145,8 +145,9 @@ def test_bench_self_launch_rehearsal_world8():
     assert line["config"]["global_keys"] == 8 << 20
 
 
-@pytest.mark.parametrize("world,pairs", [(2, False), (8, False), (3, True)])
-def test_bench_cabi_engine_rehearsal(world, pairs):
+@pytest.mark.parametrize("world,pairs,sched", [(2, False, "auto"), (8, False, "auto"), (3, True, "auto"),
+                                               (2, False, "msdz")])
+def test_bench_cabi_engine_rehearsal(world, pairs, sched):
     """`bench.py --gpus N --engine cabi`: rank 0 drives all N ranks through
     the C ABI (libsortDistribSortU32 / libsortDistribSortPairsU64U32; here
     all on the one GPU, device-copy exchanges) while the other ranks keep the
@@ -162,7 +163,8 @@ def test_bench_cabi_engine_rehearsal(world, pairs):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env["BENCH_REHEARSAL"] = "1"
     cmd = [sys.executable, str(root / "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
-           "--keys-log2", "20", "--engine", "cabi", "--no-variants"] + (["--workload", "c5"] if pairs else [])
+           "--keys-log2", "20", "--engine", "cabi", "--no-variants", "--schedule", sched] + \
+        (["--workload", "c5"] if pairs else [])
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(root))
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -174,6 +176,12 @@ def test_bench_cabi_engine_rehearsal(world, pairs):
     assert line["cabi_first_step"] == "verified"
     sent = line["exchange_bytes_per_rank"]
     assert len(sent) == world and all(b > 0 for b in sent), sent
+    if sched == "msdz":  # the gap-coded rounds (LIBSORT_DISTRIB_CODED): well under 3 B per sent key
+        assert "delta-coded" in line["config"]["workload"]
+        assert all(b < 0.5 * 4 * (1 << 20) * (world - 1) / world for b in sent), sent
+    # the stage trace of the verified first step is in the stderr tail
+    assert "libsort distrib [" in r.stderr and "done: ok" in r.stderr, r.stderr[-3000:]
+    assert "bench.py [rank 0" in r.stderr
 
 
 def test_bench_cabi_bad_first_step_falls_back_to_torch():
