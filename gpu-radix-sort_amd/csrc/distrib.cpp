@@ -1252,7 +1252,12 @@ bool sort_device(Ctx& c, const uint32_t* const* d_in, const size_t* n_in, uint32
   // gap-coded rounds (kDistribCoded; by default at two ranks on two GPUs):
   // one partition part, 32-bit keys in the partition (the wire is coded)
   const bool coded = coded_rounds_on(R, flags, c.distinct && !copy);
-  const bool planar = !coded && wire24_env && !(flags & kDistribWire32) && bits == 4;
+  // (and R >= 3: the round sorts read planes only through the reserved depth
+  // 0, which takes <= 32 segments; at R = 2 the rounds grow x1.2 over 128
+  // digits per rank -- 24, 29, 34, 41 -- and the last two would unpack and
+  // range-sort instead: 2^29 keys per rank sharing one GPU, 9.16 ms of GPU
+  // work per rank against 7.07 ms with 32-bit words, gpurun_out/r06d)
+  const bool planar = !coded && wire24_env && !(flags & kDistribWire32) && bits == 4 && R >= 3;
   const int H = coded ? 1 : parts_for(R, c.distinct && !copy);
   std::vector<std::vector<uint64_t>> Cp;
   std::vector<uint64_t> first;

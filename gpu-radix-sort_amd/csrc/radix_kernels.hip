@@ -3937,6 +3937,23 @@ uint32_t tp_tiles(size_t n, int bits) {
   const uint64_t t = (uint64_t)tp_block<K, V>(bits) * tp_items<K, V>(bits);
   return (uint32_t)((n + t - 1) / t);
 }
+// The LSD passes' tiles (sort_impl's tile path: gpuPartial, range and
+// fallback sorts): 8-bit u32 keys may take their own block size
+// (LIBSORT_TP8_LSD_BLOCK, an A/B build knob: 1024 = 16384-key tiles, 64-key
+// runs) without changing the MSD hybrid's tiles.
+#ifndef LIBSORT_TP8_LSD_BLOCK
+#define LIBSORT_TP8_LSD_BLOCK 512
+#endif
+template <typename K, typename V = NoValue>
+constexpr int tp_block_lsd(int bits) {
+  return (bits == 8 && sizeof(K) == 4 && std::is_same<V, NoValue>::value) ? LIBSORT_TP8_LSD_BLOCK
+                                                                         : tp_block<K, V>(bits);
+}
+template <typename K, typename V = NoValue>
+uint32_t tp_tiles_lsd(size_t n, int bits) {
+  const uint64_t t = (uint64_t)tp_block_lsd<K, V>(bits) * tp_items<K, V>(bits);
+  return (uint32_t)((n + t - 1) / t);
+}
 inline uint32_t tp_chunks(uint32_t tiles, int bits) {
   const uint32_t ch = (uint32_t)col_chunk_rows(1 << bits);
   return (tiles + ch - 1) / ch;
@@ -4067,7 +4084,7 @@ inline bool dstream_u32_on() {
 template <typename K, typename V, typename Op = RadixDigit>
 hipError_t tiles_prologue(Workspace& ws, const K* in, size_t n, int lo, int hi, int bits, hipStream_t st,
                           uint32_t bias = 0) {
-  const uint32_t tiles = tp_tiles<K, V>(n, bits);
+  const uint32_t tiles = tp_tiles_lsd<K, V>(n, bits);
   const uint32_t radix = 1u << bits;
   LS_TRY(ws.ensure_tiles((size_t)tiles * radix, ((size_t)tp_chunks(tiles, bits) + 1) * radix));
   if (bits == 8 && sizeof(K) == 8 && dstream_on() && num_passes(hi - lo, 8) > 1) LS_TRY(ws.ensure_dstream(n));
@@ -4092,8 +4109,8 @@ hipError_t tiles_counts_u8(Workspace& ws, size_t n, uint32_t rows, uint32_t* C, 
 template <int BITS, typename K, typename V, typename Op = RadixDigit>
 hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout, size_t n, int p, int P,
                       int lo, int hi, hipStream_t st, uint32_t bias = 0) {
-  constexpr int B = tp_block<K, V>(BITS);
-  const uint32_t tiles = tp_tiles<K, V>(n, BITS);
+  constexpr int B = tp_block_lsd<K, V>(BITS);
+  const uint32_t tiles = tp_tiles_lsd<K, V>(n, BITS);
   const int shift = lo + BITS * p;
   const int nb = std::min(BITS, hi - shift);
   const Op op = make_digit<Op>((uint32_t)shift, (1u << nb) - 1u, bias);
@@ -4113,7 +4130,7 @@ hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vou
   if (dstream && p >= 1)
     LS_TRY((tiles_counts_u8<K, V>(ws, n, tiles, cur, nullptr, nullptr, st)));
   else if (!fused_counts && !(BITS == 4 && p == 0))
-    LS_TRY((tiles_counts<BITS, K, Op, V>(ws, kin, n, op, tiles, cur, nullptr, 0, st)));
+    LS_TRY((tiles_counts<BITS, K, Op, V, B>(ws, kin, n, op, tiles, cur, nullptr, 0, st)));
   LS_TRY(tiles_colscan<BITS>(ws, cur, tiles, st));
   ws.last_pass_counts = cur;
   const bool fuse = fused_counts && p + 1 < P;
@@ -4962,18 +4979,18 @@ hipError_t sort_u32(Workspace& ws, const uint32_t* in, uint32_t* out, uint32_t* 
       LS_TRY(hipMemsetAsync(d_bounds, 0, (size_t)ngroups * sizeof(uint32_t), st));
     } else if (ws.last_algo == 3 && num_passes(width, digit_bits) == 1) {
       // tile path, single pass: the column scan's digit starts
-      LS_TRY(hipMemcpyAsync(d_bounds, tiles_digit_starts(ws, tp_tiles<uint32_t>(n, digit_bits), digit_bits),
+      LS_TRY(hipMemcpyAsync(d_bounds, tiles_digit_starts(ws, tp_tiles_lsd<uint32_t>(n, digit_bits), digit_bits),
                             (size_t)ngroups * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
     } else if (ws.last_algo == 3 && num_passes(width, digit_bits) == 2 && ws.last_pass_counts) {
       // two passes: from the last pass's counts and the middle buffer (tmp)
-      const uint32_t tiles = tp_tiles<uint32_t>(n, digit_bits);
+      const uint32_t tiles = tp_tiles_lsd<uint32_t>(n, digit_bits);
       const uint32_t dmask = (1u << (width - digit_bits)) - 1u;
       if (digit_bits == 8) {
-        constexpr int T8 = tp_block<uint32_t>(8) * tp_items<uint32_t>(8);
+        constexpr int T8 = tp_block_lsd<uint32_t>(8) * tp_items<uint32_t>(8);
         hipLaunchKernelGGL((k_bounds_lsd2<8, T8>), dim3(256), dim3(256), 0, st, tmp, (uint32_t)n, (uint32_t)lo, dmask,
                            ws.last_pass_counts, ws.tb, tiles_digit_starts(ws, tiles, 8), d_bounds);
       } else {
-        constexpr int T4 = tp_block<uint32_t>(4) * tp_items<uint32_t>(4);
+        constexpr int T4 = tp_block_lsd<uint32_t>(4) * tp_items<uint32_t>(4);
         hipLaunchKernelGGL((k_bounds_lsd2<4, T4>), dim3(16), dim3(256), 0, st, tmp, (uint32_t)n, (uint32_t)lo, dmask,
                            ws.last_pass_counts, ws.tb, tiles_digit_starts(ws, tiles, 4), d_bounds);
       }

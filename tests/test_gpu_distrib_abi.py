@@ -256,7 +256,7 @@ def test_coded_rounds_bytes(D, oracle_mod, R):
 
 @pytest.mark.parametrize("reserve", ["on", "nomem"])
 def test_wire24_reserved_depth0_odd_offsets(D, oracle_mod, reserve):
-    """Two ranks, 2^26 + 77 keys: rounds of ~2^23 keys over <= 32 segments
+    """Three ranks, 2^26 + 77 keys: rounds of 4-7M keys over <= 32 segments
     (two digit depths below the top digit), so the round sorts read the 24-bit
     planes through the reserved depth 0's
     planar loader, at round offsets (and 8-bit plane starts 2 n_recv + a) that
@@ -272,8 +272,8 @@ def test_wire24_reserved_depth0_odd_offsets(D, oracle_mod, reserve):
         os.environ["LIBSORT_HYB_RESERVE"] = "nomem"
     try:
         x = oracle_mod.pcg((1 << 26) + 77, first=11)
-        outs, (nrsv, nseg) = _timed_names(D, lambda: _run(D, x, 2, COPY), "rsvsample", "segcopy")
-        _check(oracle_mod, x, outs, 2, False)
+        outs, (nrsv, nseg) = _timed_names(D, lambda: _run(D, x, 3, COPY), "rsvsample", "segcopy")
+        _check(oracle_mod, x, outs, 3, False)
         if reserve == "on":
             assert nrsv > 0, nrsv
         else:

@@ -91,7 +91,7 @@ def main():
             cells = []
             for L in rates:
                 if sched == "msd":
-                    st, e = step_msd(int(R), L, d["P"], d["S"])
+                    st, e = step_msd(int(R), L, d["P"], d["S"], wire_bytes=d.get("wire", 3.0))
                     work = d["P"] + d["S"]
                 else:
                     st, e = step_msdz(int(R), L, d["P"], d["S"], d["M"], d["bits"])
