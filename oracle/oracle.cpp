@@ -14,7 +14,69 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 #include <vector>
+
+// std::stable_sort / std::sort of large arrays on several host threads (the
+// checker of the GPU tests sorts up to 2^28 elements; one thread took ~20 s
+// per 2^27 pairs on the box): T contiguous chunks sorted each by the same std
+// algorithm, then merged pairwise with std::merge, which keeps elements of the
+// earlier chunk first among equals -- so the result is exactly the one-thread
+// std::stable_sort (and, for keys only, std::sort) result.
+namespace {
+unsigned host_threads(size_t n) {
+  if (n < ((size_t)1 << 20)) return 1;
+  const unsigned h = std::thread::hardware_concurrency();
+  return std::max(1u, std::min(16u, h ? h : 1u));
+}
+
+template <typename T, typename Cmp>
+void par_sort(T* a, size_t n, Cmp cmp, bool stable) {
+  const unsigned nt = host_threads(n);
+  if (nt == 1) {
+    if (stable) std::stable_sort(a, a + n, cmp); else std::sort(a, a + n, cmp);
+    return;
+  }
+  std::vector<size_t> c(nt + 1);
+  for (unsigned t = 0; t <= nt; ++t) c[t] = n * t / nt;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      if (stable) std::stable_sort(a + c[t], a + c[t + 1], cmp); else std::sort(a + c[t], a + c[t + 1], cmp);
+    });
+  for (auto& x : th) x.join();
+  std::vector<T> buf(n);
+  T* src = a;
+  T* dst = buf.data();
+  for (unsigned w = 1; w < nt; w *= 2) {
+    th.clear();
+    for (unsigned i = 0; i < nt; i += 2 * w)
+      th.emplace_back([&, i] {
+        const size_t lo = c[i], mid = c[std::min(nt, i + w)], hi = c[std::min(nt, i + 2 * w)];
+        std::merge(src + lo, src + mid, src + mid, src + hi, dst + lo, cmp);
+      });
+    for (auto& x : th) x.join();
+    std::swap(src, dst);
+  }
+  if (src != a) std::copy(src, src + n, a);
+}
+
+// stable sort of (key, value) pairs by key, through packed records
+template <typename K, typename V>
+void stable_sort_kv(K* k, V* v, size_t n) {
+  struct E {
+    K k;
+    V v;
+  };
+  std::vector<E> e(n);
+  for (size_t i = 0; i < n; ++i) e[i] = E{k[i], v[i]};
+  par_sort(e.data(), n, [](const E& x, const E& y) { return x.k < y.k; }, true);
+  for (size_t i = 0; i < n; ++i) {
+    k[i] = e[i].k;
+    v[i] = e[i].v;
+  }
+}
+}  // namespace
 
 extern "C" {
 
@@ -37,7 +99,7 @@ void oracle_pcg_fill(uint32_t* out, size_t n, uint64_t* state) {
 uint64_t oracle_pcg_initial_state(void) { return 0x4d595df4d0f33173ull; }  // utils.cu:67
 
 // invokers.cu:68-71 (providedCpu): std::sort.
-void oracle_sort_u32(uint32_t* a, size_t n) { std::sort(a, a + n); }
+void oracle_sort_u32(uint32_t* a, size_t n) { par_sort(a, n, std::less<uint32_t>(), false); }
 
 // The gpuPartial contract (invokers.cu:15-41 as checked by localTest/tests.cpp:
 // 41-83 and benchmark/pkg/sort/testHelpers.go:411-448): stable partition by
@@ -206,58 +268,19 @@ void oracle_distrib_bsp_u32(uint32_t* a, size_t n, uint32_t nworker, uint32_t wi
 }
 
 // Stable key/value sorts (BASELINE configs C5): std::stable_sort by key over
-// the original order.  No reference function exists for KV; this is the
-// definition of the result.
-void oracle_stable_sort_kv64(uint64_t* k, uint32_t* v, size_t n) {
-  std::vector<size_t> idx(n);
-  for (size_t i = 0; i < n; ++i) idx[i] = i;
-  std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return k[x] < k[y]; });
-  std::vector<uint64_t> kk(n);
-  std::vector<uint32_t> vv(n);
-  for (size_t i = 0; i < n; ++i) {
-    kk[i] = k[idx[i]];
-    vv[i] = v[idx[i]];
-  }
-  if (n) {
-    memcpy(k, kk.data(), n * sizeof(uint64_t));
-    memcpy(v, vv.data(), n * sizeof(uint32_t));
-  }
-}
+// the original order (par_sort above: per-chunk std::stable_sort + stable
+// merges).  No reference function exists for KV; this is the definition of
+// the result.
+void oracle_stable_sort_kv64(uint64_t* k, uint32_t* v, size_t n) { stable_sort_kv(k, v, n); }
 
-void oracle_stable_sort_kv32(uint32_t* k, uint32_t* v, size_t n) {
-  std::vector<size_t> idx(n);
-  for (size_t i = 0; i < n; ++i) idx[i] = i;
-  std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return k[x] < k[y]; });
-  std::vector<uint32_t> kk(n), vv(n);
-  for (size_t i = 0; i < n; ++i) {
-    kk[i] = k[idx[i]];
-    vv[i] = v[idx[i]];
-  }
-  if (n) {
-    memcpy(k, kk.data(), n * sizeof(uint32_t));
-    memcpy(v, vv.data(), n * sizeof(uint32_t));
-  }
-}
+void oracle_stable_sort_kv32(uint32_t* k, uint32_t* v, size_t n) { stable_sort_kv(k, v, n); }
 
 // 64-bit keys only / with 64-bit payloads (no
 // reference function: std::sort defines the keys-only result, std::stable_sort
 // by key over the original order the pair result).
-void oracle_sort_u64(uint64_t* k, size_t n) { std::sort(k, k + n); }
+void oracle_sort_u64(uint64_t* k, size_t n) { par_sort(k, n, std::less<uint64_t>(), false); }
 
-void oracle_stable_sort_kv64v64(uint64_t* k, uint64_t* v, size_t n) {
-  std::vector<size_t> idx(n);
-  for (size_t i = 0; i < n; ++i) idx[i] = i;
-  std::stable_sort(idx.begin(), idx.end(), [&](size_t x, size_t y) { return k[x] < k[y]; });
-  std::vector<uint64_t> kk(n), vv(n);
-  for (size_t i = 0; i < n; ++i) {
-    kk[i] = k[idx[i]];
-    vv[i] = v[idx[i]];
-  }
-  if (n) {
-    memcpy(k, kk.data(), n * sizeof(uint64_t));
-    memcpy(v, vv.data(), n * sizeof(uint64_t));
-  }
-}
+void oracle_stable_sort_kv64v64(uint64_t* k, uint64_t* v, size_t n) { stable_sort_kv(k, v, n); }
 
 // The sorted order of a keys-only array is fixed by how often each value
 // occurs (std::sort, invokers.cu:68-71, has a unique result), so the sorted

@@ -24,7 +24,7 @@ def test_host_arithmetic_asan(tmp_path, src):
     exe = tmp_path / src
     subprocess.run([gxx, "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
                     "-fno-sanitize-recover=undefined", "-I", str(ROOT / "gpu-radix-sort_amd" / "csrc"),
-                    str(ROOT / "tests" / "cpp" / (src + ".cpp")), "-o", str(exe)], check=True, timeout=300)
+                    str(ROOT / "tests" / "cpp" / (src + ".cpp")), "-pthread", "-o", str(exe)], check=True, timeout=300)
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600,
                        env={"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0", "PATH": "/usr/bin:/bin"})
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]

@@ -66,6 +66,7 @@ def test_populate_device_matches_oracle(dev, oracle_mod, golden):
     np.testing.assert_array_equal(_u32(t2), oracle_mod.pcg(4099, first=first))
 
 
+@pytest.mark.ab  # (A/B pass algorithms the product path never picks: LIBSORT_TEST_AB=1 runs them)
 @pytest.mark.parametrize("bits", [4, 8])
 @pytest.mark.parametrize("algo", ["onesweep", "rts"])
 def test_non_default_algorithms(dev, oracle_mod, bits, algo):
