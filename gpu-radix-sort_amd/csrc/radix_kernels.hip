@@ -4106,6 +4106,12 @@ hipError_t tiles_counts_u8(Workspace& ws, size_t n, uint32_t rows, uint32_t* C, 
   return hipGetLastError();
 }
 
+// A/B build only (-DLIBSORT_AB_LSD_ANY_ORDER=1): the LSD passes rank by LDS
+// atomics like the hybrid's (NOT stable: wrong partial sorts) -- the price of
+// the stable ballot rank, for timing.
+#ifndef LIBSORT_AB_LSD_ANY_ORDER
+#define LIBSORT_AB_LSD_ANY_ORDER 0
+#endif
 template <int BITS, typename K, typename V, typename Op = RadixDigit>
 hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vout, size_t n, int p, int P,
                       int lo, int hi, hipStream_t st, uint32_t bias = 0) {
@@ -4145,7 +4151,9 @@ hipError_t tiles_pass(Workspace& ws, const K* kin, K* kout, const V* vin, V* vou
                        kin, kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, tiles_digit_starts(ws, tiles, BITS),
                        nxt, HybridGeo{});
   else
-    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K, V>(BITS), K, V, false, Op, Op>), dim3(tiles), dim3(B), 0, st, kin,
+    hipLaunchKernelGGL((k_tile_pass<BITS, B, tp_items<K, V>(BITS), K, V, false, Op, Op, 0,
+                                    LIBSORT_AB_LSD_ANY_ORDER && std::is_same<V, NoValue>::value>),
+                       dim3(tiles), dim3(B), 0, st, kin,
                        kout, vin, vout, (uint32_t)n, op, op_next, cur, ws.tb, tiles_digit_starts(ws, tiles, BITS),
                        nxt, geo);
   return hipGetLastError();
