@@ -58,13 +58,32 @@ def default_engine(world):
     return "cabi"
 PASS_KERNELS = "tilepass,onesweep,downsweep"  # the roofline kernel candidates (timed-region events)
 EVENT_STRIDE = 5  # N=1 timed region: events around every 5th pass launch (libsortTimingSample)
+# N=1 secondary legs: untimed calls for at least this long before each timed
+# region.  The first ~30 ms of calls after the GPU idled (the CPU baseline,
+# the host ABI leg's PCIe copies) run up to 25% slow: an 8-bit digit pass
+# took 550 us falling to 420 us over 16 calls (profiles/r06i_clock_settle.txt)
+SETTLE_S = 0.25
+
+
+def settle(step, torch, seconds=SETTLE_S):
+    """Untimed calls of `step` (each synchronised) until `seconds` have
+    passed, at least 2; returns how many ran.  World size 1 only: the ranks
+    of a multi-process step would disagree on the count."""
+    calls, t_end = 0, time.perf_counter() + seconds
+    while calls < 2 or time.perf_counter() < t_end:
+        step()
+        torch.cuda.synchronize()
+        calls += 1
+    return calls
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 20 (~45 ms at N=1): the clocks settle over the first ~30 ms of sorting
+    # after the GPU idled (--warmup 3: 2.243 ms/step, 60: 2.203; r06i)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="c2", choices=["c2", "c3", "c5"])
     ap.add_argument("--keys-log2", type=int, default=None, help="keys (pairs) per GPU = 2^k")
     ap.add_argument("--digit-bits", type=int, default=None, help="configs[1] names 4-bit digits")
@@ -430,9 +449,7 @@ def main():
         if world == 1 and not args.no_variants and args.workload == "c2":
             ref_out = out.clone()
             prev = pylibsort.setDigitBits(8)
-            for _ in range(2):
-                D.sort_keys_u32(keys, out=out, tmp=tmp)
-            torch.cuda.synchronize()
+            settle(lambda: D.sort_keys_u32(keys, out=out, tmp=tmp), torch)
             if not torch.equal(out, ref_out):
                 raise RuntimeError("8-bit digit variant disagrees with the 4-bit sort")
             del ref_out
@@ -604,9 +621,7 @@ def lsd_variant(torch, pylibsort, D, keys, out, tmp, reps):
     ref = out.clone()
     prev = pylibsort.setHybrid("off")
     try:
-        for _ in range(2):
-            D.sort_keys_u32(keys, out=out, tmp=tmp)
-        torch.cuda.synchronize()
+        settle(lambda: D.sort_keys_u32(keys, out=out, tmp=tmp), torch)
         same = bool(torch.equal(out, ref))
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -631,9 +646,7 @@ def bucket_steps_variant(torch, pylibsort, D, keys, out, tmp, reps):
     lib = pylibsort.lib()
     prev = lib.libsortSetBucketMode(0)
     try:
-        for _ in range(2):
-            D.sort_keys_u32(keys, out=out, tmp=tmp)
-        torch.cuda.synchronize()
+        settle(lambda: D.sort_keys_u32(keys, out=out, tmp=tmp), torch)
         same = bool(torch.equal(out, ref))
         t0 = time.perf_counter()
         for _ in range(reps):
@@ -710,9 +723,7 @@ def config_leg(torch, pylibsort, D, which, reps):
 
             def step():
                 return D.sort_pairs_u64_u32(keys, vals, out_keys=out, out_vals=outv, tmp_keys=tmp, tmp_vals=tmpv)
-        for _ in range(2):
-            res = step()
-        torch.cuda.synchronize()
+        settle(step, torch)
         D.timing_reset()
         D.timing_filter("tilepass")  # events around the pass only while timed (as the main line)
         D.timing_sample(3)           # every 3rd launch: rotates over the leg's two digit passes
@@ -813,9 +824,7 @@ def _partial_leg(torch, pylibsort, D, keys, out, tmp, width, reps, calls, ctypes
 
     def step():
         return D.sort_keys_u32(keys, out=out, tmp=tmp, offset=0, width=width, boundaries=b)
-    for _ in range(2):
-        step()
-    torch.cuda.synchronize()
+    settle(step, torch)
     D.timing_reset()
     D.timing_filter("tilepass")
     D.timing_sample(1)
