@@ -103,6 +103,7 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--algo", default=None, choices=["auto", "tiles", "onesweep", "rts"],
                     help="force the pass algorithm (LIBSORT_ALGO)")
+    ap.add_argument("--cabi-probe", action="store_true", help=argparse.SUPPRESS)  # (rank 0's child: cabi_probe)
     a = ap.parse_args()
     # c2 at N>1 is configs[3]: 2^29 keys per GPU, 2^32 over 8 GPUs
     defaults = {"c2": (28 if a.gpus == 1 else 29, 4), "c3": (30, 8), "c5": (28, 8)}[a.workload]
@@ -181,6 +182,8 @@ def main():
         os.environ["LIBSORT_ALGO"] = args.algo
     if args.schedule == "msd" and args.gpus == 2:
         os.environ["LIBSORT_DISTRIB_CODED"] = "0"  # (the C engine's default at 2 GPUs is the coded rounds)
+    if args.cabi_probe:
+        return cabi_probe(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -233,31 +236,32 @@ def main():
     ops = distrib.HipOps() if world > 1 else None
     engine = default_engine(world) if args.engine == "auto" else args.engine
     cabi = world > 1 and engine == "cabi"
+    # host-side waits: barriers, the engine decision and the max-over-ranks
+    # time go over gloo, so a rank that waits (every rank but 0 while the C
+    # engine runs) holds no spinning RCCL kernel on its GPU
+    cpu_pg = dist.new_group(backend="gloo") if world > 1 and not rehearsal else None
+    engine_note = None
+    probe_note = None  # the line's record of the C engine's probe (N > 1)
+    if cabi and rank == 0 and cabi_probe_on(rehearsal):
+        # one verified C-engine step in a child process first: a hang or a
+        # fault there costs a timeout and the torch engine, not the run
+        tmo = float(os.environ.get("BENCH_CABI_PROBE_S", "240"))
+        stage(rank, world, "C-ABI engine probe: one verified step in a child process (timeout %.0f s)" % tmo)
+        ok, probe_note = run_cabi_probe(tmo)
+        if not ok:
+            engine_note = "C-ABI engine probe %s; torch engine measured" % probe_note
     shards = vshards = None
-    if cabi:
+    if cabi and rank == 0 and engine_note is None:
         # one process drives every GPU through the C ABI (what a C or Go
         # caller binds); the other ranks keep the barriers and the max-over-
         # ranks timing.  Shard r = the same keys rank r holds in torch mode.
         # (every rank keeps its own keys too: the torch engine takes over if
         # the C engine fails its first step)
-        devs = [0] * world if rehearsal else list(range(world))
-        if rank == 0:
-            shards, vshards = [], []
-            for rr, dv in enumerate(devs):
-                if pairs:
-                    w = D.populate_u32(2 * n, first=rr * 2 * n, device=dv).view(n, 2).to(torch.int64)
-                    shards.append((w[:, 0] << 32) | (w[:, 1] & 0xFFFFFFFF))
-                    del w
-                    vshards.append(torch.arange(rr * n, (rr + 1) * n, dtype=torch.int64,
-                                                device=torch.device("cuda", dv)).to(torch.int32))
-                else:
-                    shards.append(D.populate_u32(n, first=rr * n, device=dv))
-            for dv in sorted(set(devs)):
-                torch.cuda.synchronize(dv)
+        shards, vshards = make_shards(torch, D, [0] * world if rehearsal else list(range(world)), n, pairs)
 
     # C engine flags: the schedule asked for (auto: the engine's own choice --
     # gap-coded rounds at 2 GPUs, top-digit rounds otherwise)
-    cabi_flags = {"msdz": D.LIBSORT_DISTRIB_CODED, "lsd": D.LIBSORT_DISTRIB_LSD}.get(args.schedule, 0)
+    cabi_flags = cabi_flags_for(D, args.schedule)
 
     def step():
         if cabi:
@@ -278,18 +282,17 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=cpu_pg)
 
-    engine_note = None
     cabi_first = None  # the line's record of the C engine's verified first step (N > 1)
     if cabi:
         # first step of the C engine, verified; if it fails or its output is
         # wrong on rank 0 (distinct-device paths run only on a multi-GPU
         # node), every rank switches to the torch engine (identical decision
         # via all_reduce)
-        failed = 0
+        failed = 1 if engine_note else 0
         stage(rank, world, "C-ABI engine: first step (verified; stage trace on)")
-        if rank == 0:
+        if rank == 0 and not failed:
             try:
                 prev_trace = pylibsort.lib().libsortSetDistribTrace(1)
                 try:
@@ -306,8 +309,8 @@ def main():
                 del first
             except RuntimeError as e:
                 failed, engine_note = 1, "C-ABI engine failed its first step (%s); torch engine measured" % e
-        flag = torch.tensor([failed], dtype=torch.int32, device="cuda")
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        flag = torch.tensor([failed], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=cpu_pg)
         if int(flag.item()):
             cabi = False
             engine = "torch"
@@ -343,8 +346,8 @@ def main():
     D.timing_enable(False)
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=cpu_pg)
         elapsed = float(t.item())
 
     # live per-kernel durations (hipEvents on libsort's launch stream): the
@@ -398,8 +401,8 @@ def main():
             step()
         torch.cuda.synchronize()
         barrier()
-        tv = torch.tensor([time.perf_counter() - v0], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tv, op=dist.ReduceOp.MAX)
+        tv = torch.tensor([time.perf_counter() - v0], dtype=torch.float64)
+        dist.all_reduce(tv, op=dist.ReduceOp.MAX, group=cpu_pg)
         pylibsort.setDigitBits(prev)
         ms8 = 1e3 * float(tv.item()) / reps
         variant8 = {"ms_per_step": round(ms8, 4), "value": round(n * world / (ms8 * 1e-3) / 1e9, 3),
@@ -539,6 +542,8 @@ def main():
             # measured on the torch engine but shows in the line
             line["cabi_first_step"] = (engine_note and "FAILED: " + engine_note) or cabi_first or \
                 "not run (torch engine chosen)"
+            if probe_note is not None:
+                line["cabi_probe"] = probe_note
             if engine_note:
                 line["engine_note"] = engine_note
             if cabi:
@@ -550,7 +555,7 @@ def main():
             line["rehearsal"] = "gloo, all ranks on one GPU: exercises the N>1 path, not a measurement"
         print(json.dumps(line), flush=True)
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=cpu_pg)
         dist.destroy_process_group()
 
 
@@ -937,6 +942,99 @@ def host_abi_leg(torch, pylibsort, keys, sorted_keys, calls=3):
                     "output checked equal to the device-resident sort" % calls}
 
 
+def make_shards(torch, D, devs, n, pairs):
+    """The C engine's input: shard r (on devs[r]) = the keys (pairs) rank r
+    of the torch engine holds -- the populate stream's r-th block of n."""
+    shards, vshards = [], []
+    for rr, dv in enumerate(devs):
+        if pairs:
+            w = D.populate_u32(2 * n, first=rr * 2 * n, device=dv).view(n, 2).to(torch.int64)
+            shards.append((w[:, 0] << 32) | (w[:, 1] & 0xFFFFFFFF))
+            del w
+            vshards.append(torch.arange(rr * n, (rr + 1) * n, dtype=torch.int64,
+                                        device=torch.device("cuda", dv)).to(torch.int32))
+        else:
+            shards.append(D.populate_u32(n, first=rr * n, device=dv))
+    for dv in sorted(set(devs)):
+        torch.cuda.synchronize(dv)
+    return shards, vshards
+
+
+def cabi_flags_for(D, schedule):
+    return {"msdz": D.LIBSORT_DISTRIB_CODED, "lsd": D.LIBSORT_DISTRIB_LSD}.get(schedule, 0)
+
+
+def cabi_probe_on(rehearsal):
+    """The probe runs on a real multi-GPU node (distinct devices: the paths
+    a one-GPU box never runs); BENCH_CABI_PROBE=1 / 0 forces it on / off."""
+    v = os.environ.get("BENCH_CABI_PROBE")
+    return v == "1" if v in ("0", "1") else not rehearsal
+
+
+def run_cabi_probe(timeout):
+    """Rank 0: `bench.py <same args> --cabi-probe` as a child process (never
+    exec), its stderr (the engine's stage trace) passed through.  Returns
+    (ok, note)."""
+    import subprocess
+    cmd = [sys.executable, str(pathlib.Path(__file__).resolve())] + sys.argv[1:] + ["--cabi-probe"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK")}
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    try:
+        out, err = p.communicate(timeout=timeout)
+        why = None if p.returncode == 0 else "exited with %d" % p.returncode
+    except subprocess.TimeoutExpired:
+        p.kill()
+        out, err = p.communicate()
+        why = "timed out after %.0f s (killed)" % timeout
+    for ln in (err or "").splitlines()[-60:]:
+        sys.stderr.write("bench.py [cabi probe]: %s\n" % ln)
+    sys.stderr.flush()
+    got = None
+    for ln in (out or "").splitlines():
+        if ln.startswith("{"):
+            try:
+                got = json.loads(ln)
+            except ValueError:
+                pass
+    if why is None and not (got and got.get("cabi_probe") is True):
+        why = "did not verify"
+    dt = time.perf_counter() - t0
+    if why:
+        return False, "%s (%.1f s)" % (why, dt)
+    return True, "verified in a child process: first step %.3f s, %.1f s with start-up" % (got["first_step_s"], dt)
+
+
+def cabi_probe(args):
+    """--cabi-probe (rank 0's child, no process group): ONE C-engine step over
+    the line's shards on devices 0..N-1 with the stage trace on, verified
+    like the parent's first step; prints one JSON line, exits 0 when it
+    verified.  BENCH_CABI_PROBE_FAULT=hang|fail rehearses the parent's
+    timeout / failure handling (tests only)."""
+    fault = os.environ.get("BENCH_CABI_PROBE_FAULT")
+    if fault == "hang":
+        time.sleep(3600)
+    import torch
+    import pylibsort
+    import pylibsort.device as D
+    world = args.gpus
+    devs = [0] * world if os.environ.get("BENCH_REHEARSAL") == "1" else list(range(world))
+    pylibsort.setDigitBits(args.digit_bits)
+    pairs = args.workload == "c5"
+    shards, vshards = make_shards(torch, D, devs, 1 << args.keys_log2, pairs)
+    pylibsort.lib().libsortSetDistribTrace(1)
+    t0 = time.perf_counter()
+    res = D.distrib_sort_pairs_u64_u32(shards, vshards) if pairs else D.distrib_sort_u32(
+        shards, cabi_flags_for(D, args.schedule))
+    for dv in sorted(set(devs)):
+        torch.cuda.synchronize(dv)
+    t1 = time.perf_counter()
+    ok = verify_cabi(torch, shards, res, vshards if pairs else None) and fault != "fail"
+    print(json.dumps({"cabi_probe": bool(ok), "first_step_s": round(t1 - t0, 3)}), flush=True)
+    return 0 if ok else 1
+
+
 def verify_cabi(torch, shards, res, vshards=None):
     """The C-ABI engine's result on rank 0: every output shard sorted (and,
     pairs, stable), the shards in order across their edges, the same
@@ -1034,4 +1132,4 @@ def verify(torch, dist, world, keys, res, vals=None):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

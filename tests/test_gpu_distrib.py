@@ -212,6 +212,44 @@ def test_bench_cabi_bad_first_step_falls_back_to_torch():
     assert line["cabi_first_step"].startswith("FAILED")
 
 
+@pytest.mark.parametrize("fault", [None, "fail", "hang"])
+def test_bench_cabi_probe(fault):
+    """On a multi-GPU node rank 0 first runs one verified C-engine step in a
+    child process (`bench.py ... --cabi-probe`, its stage trace passed
+    through): a child that fails or hangs (killed at BENCH_CABI_PROBE_S)
+    hands the measurement to the torch engine instead of ending the run.
+    Here forced on (BENCH_CABI_PROBE=1) with the ranks sharing the GPU; the
+    faults are injected in the child (BENCH_CABI_PROBE_FAULT)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import json
+    import os
+    import pathlib
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(BENCH_REHEARSAL="1", BENCH_CABI_PROBE="1", BENCH_CABI_PROBE_S="30")
+    if fault:
+        env["BENCH_CABI_PROBE_FAULT"] = fault
+    cmd = [sys.executable, str(root / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--keys-log2", "20", "--engine", "cabi", "--no-variants"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300, cwd=str(root))
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["verified"] is True
+    if fault is None:
+        assert line["cabi_probe"].startswith("verified in a child process"), line["cabi_probe"]
+        assert line["engine"].startswith("cabi") and line["cabi_first_step"] == "verified"
+        assert "bench.py [cabi probe]: libsort distrib [" in r.stderr, r.stderr[-3000:]
+    else:
+        want = "timed out after 30 s" if fault == "hang" else "exited with 1"
+        assert want in line["cabi_probe"] and want in line["engine_note"], line
+        assert not line["engine"].startswith("cabi") and line["cabi_first_step"].startswith("FAILED")
+
+
 def test_bench_single_gpu_line_contract():
     """bench.py at N=1 (small steps): one JSON line with the driver's keys,
     the roofline object (live per-launch pass time), a verified sort, the
