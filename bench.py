@@ -317,6 +317,10 @@ def main():
             if rank == 0:
                 sys.stderr.write("bench.py: %s\n" % engine_note)
     stage(rank, world, "warmup (%d steps, %s engine)" % (args.warmup, engine))
+    # N=1: untimed steps for SETTLE_S first, whatever W is (the clocks settle
+    # over the first ~30 ms of sorting: W=3 2.243 ms/step, W=60 2.203; r06i);
+    # reported in the line.  (N>1: the ranks' step counts must agree)
+    settled = settle(step, torch) if world == 1 and os.environ.get("BENCH_SETTLE", "1") != "0" else 0
     for _ in range(args.warmup):
         res = step()
     torch.cuda.synchronize()
@@ -520,6 +524,9 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle": {"steps": settled, "seconds": SETTLE_S if settled else 0,
+                       "note": "untimed steps before the W warm-up steps (N=1): the GPU's clocks settle over the "
+                               "first ~30 ms of sorting after idling (profiles/r06i_clock_settle.txt)"},
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
