@@ -279,3 +279,4 @@ def test_bench_single_gpu_line_contract():
     assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] == 1
     assert d["cpu_baseline"]["nproc"] >= 1 and d["cpu_baseline"]["host_cpu"]
     assert d["host_abi"]["value"] > 0 and d["variants"]["digit8"]["value"] > 0
+    assert d["settle"]["steps"] >= 2 and d["settle"]["seconds"] > 0  # untimed clock-settle steps, reported
