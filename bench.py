@@ -566,7 +566,7 @@ def main():
         dist.destroy_process_group()
 
 
-PROFILE_TAG = "r06x"  # profiles/<tag>_* of this round's build (tools/collect_profiles.sh)
+PROFILE_TAG = "r06y"  # profiles/<tag>_* of this round's build (tools/collect_profiles.sh)
 
 
 def committed_profile(bytes_per_launch):
