@@ -3382,15 +3382,21 @@ constexpr int kDeltaGroup = 64;
 
 __device__ __forceinline__ uint32_t delta_bits(uint32_t maxgap) { return maxgap ? 32u - __clz(maxgap) : 0u; }
 
-// Each wave takes kDeltaUnroll groups per step (group g = lane-contiguous 64
-// keys, one coalesced load each), all loads issued before any use.
-constexpr int kDeltaUnroll = 4;
+// The kernels below step over chunks of kDeltaChunk groups (4096 keys) per
+// 256-thread block: wave v of the block takes the chunk's groups v, v + 4,
+// ... (16 groups, one coalesced load each, all issued before any use); the
+// pack assembles the chunk's payload in LDS and writes it (and the bases)
+// with block-wide coalesced stores, the unpack stages it the same way.  (The
+// per-wave form before, 4 groups per wave and 2w-dword stores per group:
+// 116 / 96 us per 2^26-key piece, 2.5 / 3.0 TB/s; profiles/r06d.)
+constexpr int kDeltaChunk = 64;
+constexpr int kDeltaWaveGroups = kDeltaChunk / 4;
 
 // Largest in-group gap of the sorted run keys[0..n) -> atomicMax into *maxgap
 // (zeroed by the caller).
 __global__ __launch_bounds__(256) void k_delta_maxgap(const uint32_t* __restrict__ keys, uint64_t n,
                                                       uint32_t* __restrict__ maxgap) {
-  constexpr int U = kDeltaUnroll;
+  constexpr int U = kDeltaWaveGroups;
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
   const uint64_t wpb = blockDim.x / kWave;
@@ -3423,83 +3429,118 @@ __global__ __launch_bounds__(256) void k_delta_maxgap(const uint32_t* __restrict
 }
 
 // Pack: w read from *maxgap on the device (so the pack can be queued before
-// the host knows it).  Each wave assembles a group's 2w dwords in LDS with
-// atomicOr, then writes them out.
+// the host knows it).  Gap j of a group goes to bits [j w, j w + w) of its 2w
+// dwords (LDS atomicOr; zero gaps skip it).
 __global__ __launch_bounds__(256) void k_delta_pack(const uint32_t* __restrict__ keys, uint64_t n,
                                                     const uint32_t* __restrict__ maxgap, uint32_t* __restrict__ out) {
-  constexpr int U = kDeltaUnroll;
-  __shared__ uint32_t s_w[256 / kWave][U][2 * kDeltaGroup];
+  constexpr int U = kDeltaWaveGroups;
+  __shared__ uint32_t s_p[kDeltaChunk * 2 * 32];  // 2w <= 64 dwords per group
+  __shared__ uint32_t s_b[kDeltaChunk];
   const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
   const uint32_t w = delta_bits(*maxgap);
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
-  const uint64_t wpb = blockDim.x / kWave;
-  uint32_t* payload = out + ng;
-  for (uint64_t g0 = ((uint64_t)blockIdx.x * wpb + wv) * U; g0 < ng; g0 += (uint64_t)gridDim.x * wpb * U) {
+  const uint64_t nch = (ng + kDeltaChunk - 1) / kDeltaChunk;
+  uint32_t* const payload = out + ng;
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    const uint64_t gb = c * kDeltaChunk;
+    const uint32_t gn = (uint32_t)min((uint64_t)kDeltaChunk, ng - gb);
+    const uint32_t pw = gn * 2u * w;
     uint32_t k[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint64_t i = (g0 + u) * kDeltaGroup + lane;
+      const uint64_t i = (gb + (uint64_t)u * 4 + wv) * kDeltaGroup + lane;
       k[u] = i < n ? keys[i] : 0u;
     }
+    for (uint32_t i = threadIdx.x; i < pw; i += 256) s_p[i] = 0u;
+    __syncthreads();
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint64_t g = g0 + u;
-      if (g >= ng) break;
-      if (lane == 0) out[g] = k[u];
-      if (w == 0) continue;
-      const uint64_t i = g * kDeltaGroup + lane;
-      const uint32_t prev = __shfl_up(k[u], 1, kWave);
-      const uint32_t gap = (lane > 0 && i < n) ? k[u] - prev : 0u;
-      uint32_t* sw = s_w[wv][u];
-      sw[lane] = 0u;
-      sw[lane + kWave] = 0u;
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t bit = lane * w, q = bit >> 5, r = bit & 31u;
-      atomicOr(&sw[q], gap << r);
-      if (r + w > 32u) atomicOr(&sw[q + 1], gap >> (32u - r));
-      __builtin_amdgcn_wave_barrier();
-      uint32_t* dst = payload + g * 2 * w;
-      if (lane < 2 * w) dst[lane] = sw[lane];
-      if (lane + kWave < 2 * w) dst[lane + kWave] = sw[lane + kWave];
+      const uint32_t gl = (uint32_t)u * 4u + wv;  // (wave-uniform)
+      if (gl < gn) {
+        const uint64_t i = (gb + gl) * kDeltaGroup + lane;
+        const uint32_t prev = __shfl_up(k[u], 1, kWave);
+        if (lane == 0) s_b[gl] = k[u];
+        const uint32_t gap = (lane > 0 && i < n) ? k[u] - prev : 0u;
+        if (gap) {
+          const uint32_t bit = lane * w, q = gl * 2u * w + (bit >> 5), r = bit & 31u;
+          atomicOr(&s_p[q], gap << r);
+          if (r + w > 32u) atomicOr(&s_p[q + 1], gap >> (32u - r));
+        }
+      }
     }
+    __syncthreads();
+    if (threadIdx.x < gn) out[gb + threadIdx.x] = s_b[threadIdx.x];
+    uint32_t* const dst = payload + gb * 2u * w;
+    for (uint32_t i = threadIdx.x; i < pw; i += 256) dst[i] = s_p[i];
+    __syncthreads();  // (the next chunk zeroes s_p)
   }
 }
 
-// Unpack: gaps -> inclusive wave scan + base.
+// Unpack: the chunk's bases and payload staged in LDS (coalesced loads); a
+// group's 64 keys are taken by 16 lanes x 4 consecutive keys (a wave: 4
+// groups per step), each lane's 4 gaps summed in registers and the lanes'
+// sums scanned over 16 lanes (a third of the per-key VALU work of a 64-lane
+// scan per group); the keys go out through LDS in 64-key coalesced stores.
 __global__ __launch_bounds__(256) void k_delta_unpack(const uint32_t* __restrict__ in, uint64_t n, uint32_t w,
                                                       uint32_t* __restrict__ keys) {
-  constexpr int U = kDeltaUnroll;
-  const uint32_t lane = threadIdx.x & (kWave - 1);
+  __shared__ uint32_t s_p[kDeltaChunk * 2 * 32];
+  __shared__ uint32_t s_b[kDeltaChunk];
+  const uint32_t lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  const uint32_t sub = lane >> 4, l16 = lane & 15u, j0 = l16 * 4u;
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
-  const uint64_t wpb = blockDim.x / kWave;
-  const uint32_t* payload = in + ng;
+  const uint64_t nch = (ng + kDeltaChunk - 1) / kDeltaChunk;
+  const uint32_t* const payload = in + ng;
   const uint32_t mask = w >= 32u ? 0xffffffffu : ((1u << w) - 1u);
-  const uint32_t bit = lane * w, q = bit >> 5, r = bit & 31u;
-  for (uint64_t g0 = ((uint64_t)blockIdx.x * wpb + threadIdx.x / kWave) * U; g0 < ng;
-       g0 += (uint64_t)gridDim.x * wpb * U) {
-    uint32_t lo[U], hi[U], base[U];
+  for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
+    const uint64_t gb = c * kDeltaChunk;
+    const uint32_t gn = (uint32_t)min((uint64_t)kDeltaChunk, ng - gb);
+    const uint32_t pw = gn * 2u * w;
+    const uint32_t* const src = payload + gb * 2u * w;
+    for (uint32_t i = threadIdx.x; i < pw; i += 256) s_p[i] = src[i];
+    if (threadIdx.x < gn) s_b[threadIdx.x] = in[gb + threadIdx.x];
+    __syncthreads();
+    constexpr int ST = kDeltaWaveGroups / 4;
+    uint32_t v[ST][4];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint64_t g = g0 + u;
-      lo[u] = hi[u] = 0u;
-      base[u] = g < ng ? in[g] : 0u;
-      if (w && g < ng) {
-        const uint32_t* src = payload + g * 2 * w;
-        lo[u] = src[q];
-        if (r + w > 32u) hi[u] = src[q + 1];
+    for (int st = 0; st < ST; ++st) {
+      const uint32_t gl = wv * kDeltaWaveGroups + (uint32_t)st * 4u + sub;
+      const bool live = gl < gn;
+      uint32_t x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        uint32_t gap = 0u;
+        if (w && live) {
+          const uint32_t* const g = s_p + gl * 2u * w;
+          const uint32_t bit = (j0 + (uint32_t)e) * w, q = bit >> 5, r = bit & 31u;
+          const uint32_t lo = g[q], hi = r + w > 32u ? g[q + 1] : 0u;
+          gap = (uint32_t)((((uint64_t)hi << 32) | lo) >> r) & mask;
+        }
+        x[e] = e ? x[e - 1] + gap : gap;
       }
-    }
+      uint32_t t = x[3];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      uint32_t gap = w ? (uint32_t)((((uint64_t)hi[u] << 32) | lo[u]) >> r) & mask : 0u;
-#pragma unroll
-      for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t y = __shfl_up(gap, o, kWave);
-        if ((int)lane >= o) gap += y;
+      for (int o = 1; o < 16; o <<= 1) {
+        const uint32_t y = __shfl_up(t, o, 16);
+        if ((int)l16 >= o) t += y;
       }
-      const uint64_t i = (g0 + u) * kDeltaGroup + lane;
-      if (i < n) keys[i] = base[u] + gap;
+      const uint32_t base = (live ? s_b[gl] : 0u) + (t - x[3]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[st][e] = base + x[e];
     }
+    // the chunk's keys through LDS (over the payload words, read by now), so
+    // every store instruction writes 64 consecutive keys whatever the
+    // destination's alignment (the rounds decode at arbitrary key offsets)
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < ST; ++st) {
+      const uint32_t gl = wv * kDeltaWaveGroups + (uint32_t)st * 4u + sub;
+      *reinterpret_cast<uint4*>(&s_p[gl * kDeltaGroup + j0]) = make_uint4(v[st][0], v[st][1], v[st][2], v[st][3]);
+    }
+    __syncthreads();
+    const uint64_t k0 = gb * kDeltaGroup;
+    const uint32_t nk = (uint32_t)min((uint64_t)kDeltaChunk * kDeltaGroup, n - k0);
+    for (uint32_t i = threadIdx.x; i < nk; i += 256) keys[k0 + i] = s_p[i];
+    __syncthreads();  // (the next chunk restages s_p)
   }
 }
 
@@ -3508,13 +3549,36 @@ __global__ __launch_bounds__(256) void k_delta_unpack(const uint32_t* __restrict
 // two input ranges staged in LDS, then each thread merges ITEMS outputs from
 // its own diagonal.  Ties take a first (keys only: order among equal keys is
 // invisible).
+// The split of diagonal d: the first i in [lo, hi) with a[i] > b[d - 1 - i]
+// (f(i) = a[i] - b[d - 1 - i] is non-decreasing; hi when there is none).  The
+// probes alternate a secant step on f between the bracket's known values and
+// a bisection: exact for any input (only the bracket decides), ~8 dependent
+// probes instead of ~27 for the uniform runs of the coded rounds (each probe
+// is a global load pair; the split kernel is one such chain long).
 __device__ __forceinline__ uint64_t merge_path_split(const uint32_t* a, uint64_t na, const uint32_t* b, uint64_t nb,
                                                      uint64_t d) {
   uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (a[mid] <= b[d - mid - 1]) lo = mid + 1;
-    else hi = mid;
+  // f at the bracket's outer neighbours, when probed (fl <= 0 at lo - 1, fr > 0 at hi)
+  double fl = 0.0, fr = 0.0;
+  bool have_l = false, have_r = false;
+  for (int step = 0; lo < hi; ++step) {
+    uint64_t mid = (lo + hi) >> 1;
+    if ((step & 1) == 0 && have_l && have_r && hi - lo > 8) {
+      // secant between (lo - 1, fl) and (hi, fr) for the zero of f
+      const double x = (double)(lo - 1) + (0.0 - fl) * (double)(hi - lo + 1) / (fr - fl);
+      const double xc = x < (double)lo ? (double)lo : x > (double)(hi - 1) ? (double)(hi - 1) : x;
+      mid = (uint64_t)xc;
+    }
+    const double f = (double)a[mid] - (double)b[d - mid - 1];
+    if (f <= 0.0) {
+      lo = mid + 1;
+      fl = f;
+      have_l = true;
+    } else {
+      hi = mid;
+      fr = f;
+      have_r = true;
+    }
   }
   return lo;
 }
@@ -5561,7 +5625,7 @@ hipError_t delta_maxgap_u32(const uint32_t* keys, size_t n, uint32_t* d_maxgap, 
   LS_TRY(hipMemsetAsync(d_maxgap, 0, sizeof(uint32_t), st));
   if (n < 2) return hipSuccess;
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 15) / 16, 1024);
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + kDeltaChunk - 1) / kDeltaChunk, 1024);
   hipLaunchKernelGGL(k_delta_maxgap, dim3(blocks), dim3(256), 0, st, keys, (uint64_t)n, d_maxgap);
   return hipGetLastError();
 }
@@ -5569,7 +5633,7 @@ hipError_t delta_maxgap_u32(const uint32_t* keys, size_t n, uint32_t* d_maxgap, 
 hipError_t delta_pack_u32(const uint32_t* keys, size_t n, const uint32_t* d_maxgap, uint32_t* out, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 15) / 16, 8192);
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + kDeltaChunk - 1) / kDeltaChunk, 8192);
   hipLaunchKernelGGL(k_delta_pack, dim3(blocks), dim3(256), 0, st, keys, (uint64_t)n, d_maxgap, out);
   return hipGetLastError();
 }
@@ -5578,7 +5642,7 @@ hipError_t delta_unpack_u32(const uint32_t* in, size_t n, uint32_t w, uint32_t* 
   if (n == 0) return hipSuccess;
   if (w > 32) return hipErrorInvalidValue;
   const uint64_t ng = (n + kDeltaGroup - 1) / kDeltaGroup;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + 15) / 16, 8192);
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>((ng + kDeltaChunk - 1) / kDeltaChunk, 8192);
   hipLaunchKernelGGL(k_delta_unpack, dim3(blocks), dim3(256), 0, st, in, (uint64_t)n, w, keys);
   return hipGetLastError();
 }

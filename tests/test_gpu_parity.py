@@ -738,6 +738,14 @@ def test_delta_code_roundtrip(dev, kind, n):
     np.testing.assert_array_equal(coded.cpu().numpy().view(np.uint32), ref)
     back = D.delta_unpack_u32(coded, n, w)
     np.testing.assert_array_equal(back.cpu().numpy().view(np.uint32), x)
+    # into a destination 1..3 words past 16-byte alignment (the rounds decode
+    # at arbitrary key offsets; the aligned case takes 16-byte stores)
+    for off in (1, 2, 3):
+        buf = torch.full((n + off,), -1, dtype=torch.int32, device="cuda")
+        D.delta_unpack_u32(coded, n, w, out=buf[off:])
+        got = buf.cpu().numpy().view(np.uint32)
+        np.testing.assert_array_equal(got[off:], x)
+        assert (got[:off] == 0xFFFFFFFF).all()
 
 
 @pytest.mark.parametrize("na,nb", [(0, 0), (0, 5), (7, 0), (1, 1), (2048, 2048), (100003, 77777), (5, 300000),
