@@ -1251,7 +1251,9 @@ __global__ __launch_bounds__(BLOCK) LS_TP_ATTR void k_tile_pass(const K* __restr
   uint32_t valid, seg = 0, t, row;  // row: the tile's count row (its table entry's w)
   if constexpr ((GEO & 1) != 0) {
     // the grid is a bound: blocks past this depth's tile count exit, and the
-    // XCD-contiguous map is over the count, so every XCD gets its share
+    // XCD-contiguous map is over the count, so every XCD gets its share (a
+    // map over the bound, loading the count and the table entry together:
+    // 424 vs 415 us per pass, 3 interleaved runs, profiles/r06n_tile_map_ab.txt)
     const uint32_t g = *geo.ntiles;
     if (blockIdx.x >= g) return;
     t = xcd_tile_of(blockIdx.x, g);
