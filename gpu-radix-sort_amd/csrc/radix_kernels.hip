@@ -3426,7 +3426,9 @@ __global__ __launch_bounds__(256) void k_delta_maxgap(const uint32_t* __restrict
   __syncthreads();
   if (threadIdx.x == 0) {
     for (uint32_t i = 1; i < blockDim.x / kWave; ++i) m = max(m, s_m[i]);
-    if (m) atomicMax(maxgap, m);
+    // (only a block above the word's current value adds its atomic: the
+    // word only grows, and most blocks' maxima are below it by then)
+    if (m && m > __hip_atomic_load(maxgap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(maxgap, m);
   }
 }
 
